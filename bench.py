@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Headline benchmark: NeRF training-step throughput in ray-samples/s.
+
+Workload (BASELINE.json configs[1]): naive-to-vanilla NeRF at the Lego 400x400
+setting — per GPU 4096 rays x 64 stratified samples per step, NerfModel with
+n_hidden=4, hidden_dim=256, 2 segments, delayed direction + density, Fourier
+position encoding (L=10, scale 2*pi) and direction encoding (L=4, scale 1),
+near/far 0.1/0.333, density factor 3*7 (naive-to-vanilla/main.py:89-102,
+model_interpolation.py:8,97-125,198-235).  A step is the whole training step:
+t sampling -> encodings -> 12-layer MLP -> compositing -> MSE -> backward ->
+(N>1: RCCL all-reduce of the flat gradient) -> Adam.  Synthetic Lego-shaped
+rays and target colours (no dataset is available offline).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+Prints ONE JSON line on rank 0 (schema: see README / DESIGN.md §Measurement).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import platform
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "nerf-experiments_amd"))
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+HBM_PEAK_GBS = 8000.0
+
+RAYS = 4096
+SAMPLES = 64
+NEAR, FAR = 0.1, 1.0 / 3.0
+
+
+def synthetic_batch(n_rays: int, seed: int, device):
+    """Lego-shaped rays in naive-to-vanilla's normalised space: camera centres on the upper
+    hemisphere (radius 0.168) looking at the scene centre, 400x400 pixel cone width."""
+    g = torch.Generator().manual_seed(seed)
+    u = torch.rand(n_rays, 2, generator=g)
+    theta = u[:, 0] * 2 * math.pi
+    z = u[:, 1] * 0.9 + 0.1
+    r = torch.sqrt(1 - z * z)
+    o = torch.stack((r * torch.cos(theta), r * torch.sin(theta), z), dim=1) * 0.168
+    jitter = (torch.rand(n_rays, 3, generator=g) - 0.5) * 0.08
+    d = torch.nn.functional.normalize(-o + jitter, dim=1)
+    pw = torch.full((n_rays,), 1.0 / 555.56)
+    target = 0.5 + 0.5 * torch.sin(torch.stack((3 * d[:, 0], 5 * d[:, 1] + 1, 7 * d[:, 2] + 2), dim=1))
+    return o.to(device), d.to(device), pw.to(device), target.to(device)
+
+
+def build_model(device):
+    from nerf_amd import FourierFeatures, NerfInterpolation, NerfModel
+    torch.manual_seed(0)
+    model = NerfModel(4, 256, True, True, 2, FourierFeatures(10, 2 * math.pi), FourierFeatures(4, 1.0),
+                      learning_rate_start=5e-4, learning_rate_stop=5e-5)
+    ren = NerfInterpolation(NEAR, FAR, model, SAMPLES, "stratified_uniform", 0.0, "middle",
+                            density_factor=(3.0, 7.0)).to(device)
+    return ren
+
+
+def flops_per_sample(ren) -> float:
+    """Algorithmic MLP FLOPs per sample for fwd + bwd (dX and dW): 2*MACs * 3."""
+    macs = sum(m.in_features * m.out_features for m in ren.model_radiance.modules()
+               if isinstance(m, torch.nn.Linear))
+    return 2.0 * macs * 3.0
+
+
+def cpu_baseline(seconds: float = 15.0):
+    """The CPU oracle (oracle/nerf_oracle.py, PyTorch CPU fp32 — a restatement of the
+    reference's CPU path) running the same training step on a bounded sample."""
+    from oracle import nerf_oracle as O
+    threads = len(os.sched_getaffinity(0))
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    torch.set_num_threads(threads)
+    ren = build_model("cpu")
+    sd = {k: v.clone().requires_grad_(True) for k, v in ren.model_radiance.state_dict().items()}
+    opt = torch.optim.Adam(list(sd.values()), lr=5e-4, eps=1e-5)
+    B = 512
+    o, d, pw, target = synthetic_batch(B, 123, "cpu")
+
+    def step():
+        interval = (FAR - NEAR) / SAMPLES
+        t = O.linspace_t(NEAR, FAR, SAMPLES).unsqueeze(0).repeat(B, 1) + torch.rand(B, SAMPLES) * interval
+        t0, t1 = O.intervals(t, FAR)
+        pos, dirs = O.compute_positions(o, d, t0, t1, "middle")
+        pos_pe = O.fourier_features(pos.view(-1, 3), 10, 2 * math.pi)
+        dir_pe = O.fourier_features(dirs.reshape(-1, 3), 4, 1.0)
+        dens, rgb = O.nerf_model_forward(sd, pos_pe, dir_pe, 2, 4, True, True)
+        out, _ = O.render_rays(dens.view(B, SAMPLES), rgb.view(B, SAMPLES, 3), t1 - t0, 3.0, 7.0)
+        loss = torch.nn.functional.mse_loss(out, target)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+
+    step()  # warm-up
+    n, t_start = 0, time.perf_counter()
+    while True:
+        step()
+        n += 1
+        el = time.perf_counter() - t_start
+        if el >= seconds or n >= 50:
+            break
+    cpu_model = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": n * B * SAMPLES / el, "unit": "ray-samples/s", "cores": threads, "kind": "port",
+            "sample": f"{n} training steps of {B} rays x {SAMPLES} samples (same model/config, torch CPU fp32, "
+                      f"{el:.1f} s) on {cpu_model}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+
+    import nerf_amd
+    from nerf_amd import kernels as K
+    nerf_amd._lib.load()
+
+    ren = build_model(device)
+    opt = ren.configure_optimizers()["optimizer"]
+    params = [p for p in ren.parameters() if p.requires_grad]
+    o, d, pw, target = synthetic_batch(RAYS, 1000 + rank, device)
+    torch.manual_seed(1234 + rank)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss, _ = ren.training_loss(o, d, pw, target)
+        loss.backward()
+        if dist is not None:
+            grads = [p.grad for p in params]
+            flat = torch._utils._flatten_dense_tensors(grads)
+            dist.all_reduce(flat)
+            flat.div_(world)
+            for g, s in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
+                g.copy_(s)
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    K.TIMER = K.KernelTimer()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    timer, K.TIMER = K.TIMER, None
+    if dist is not None:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    final_loss = float(loss.item())
+
+    samples_total = RAYS * SAMPLES * world * args.steps
+    value = samples_total / elapsed
+    ks = timer.summary()
+    nt = ks.get("linear_nt", {"launches": 0, "flops": 0.0, "ms": 0.0})
+    nt_avg_ms = nt["ms"] / max(nt["launches"], 1)
+    nt_avg_flops = nt["flops"] / max(nt["launches"], 1)
+    achieved = (nt_avg_flops / (nt_avg_ms * 1e-3)) / 1e12 if nt_avg_ms > 0 else 0.0
+
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "traffic_linear_nt.json")
+    if os.path.exists(tfile):
+        with open(tfile) as f:
+            traffic = json.load(f).get("bytes_per_launch")
+
+    if rank == 0:
+        out = {
+            "metric": "ray-samples/sec (coarse+fine), training step",
+            "value": value,
+            "unit": "ray-samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic Lego-shaped rays/targets, random-init weights (torch.manual_seed(0))",
+            "config": {"workload": "naive-to-vanilla NeRF training step, Lego 400x400, 4096 rays x 64 samples "
+                                   "per GPU (BASELINE.json configs[1])",
+                       "rays_per_gpu": RAYS, "samples_per_ray": SAMPLES, "global_rays": RAYS * world,
+                       "parallelism": f"ray-batch dp{world}" + (" (RCCL all-reduce)" if world > 1 else "")},
+            "roofline": {"kernel": "linear_nt (fp32 MFMA 32x32x2: forward + input-gradient GEMMs)",
+                         "bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                         "avg_launch_us": nt_avg_ms * 1e3, "avg_flops_per_launch": nt_avg_flops,
+                         "launches_per_step": nt["launches"] / args.steps},
+            "kernels": {k: {"launches_per_step": v["launches"] / args.steps, "ms_per_step": v["ms"] / args.steps,
+                            "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["ms"] > 0 else 0.0}
+                        for k, v in ks.items()},
+            "mlp_tflops_per_step": flops_per_sample(ren) * RAYS * SAMPLES / (elapsed / args.steps) / 1e12,
+            "final_loss": final_loss,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

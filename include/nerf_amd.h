@@ -1,0 +1,222 @@
+/*
+ * nerf_amd.h — C-ABI of the MI355X (gfx950) NeRF ray-marching hot path.
+ *
+ * Every entry point is stateless, works on caller-owned device pointers and
+ * enqueues its kernels on the caller's HIP stream (passed as `void*`, i.e. a
+ * hipStream_t; NULL = the default stream).  Nothing here allocates device
+ * memory, synchronises the stream, or keeps global mutable state, so every
+ * call can be captured in a hipGraph.  All tensors are fp32 unless stated.
+ *
+ * Return value: NERF_OK (0) or a negative status (see nerf_status_string).
+ *
+ * Reference interfaces replaced (sarphiv/nerf-experiments, read-only copy):
+ *   - composite  : NerfInterpolation._render_rays        barf/model_interpolation.py:316-353
+ *                  (copies: naive-to-vanilla/model_interpolation.py:198-235,
+ *                   mip_NeRF/model_interpolation.py:192-229, 3d-ingp/model.py:347-380)
+ *   - resample   : NerfInterpolation._sample_t_pdf_weighted barf/model_interpolation.py:193-277
+ *                  (round/argmax variant: naive-to-vanilla/model_interpolation.py:128-169)
+ *   - sampling   : _sample_t_stratified_uniform + _get_intervals
+ *                                                        barf/model_interpolation.py:114-180
+ *   - encoding   : FourierFeatures / BarfPositionalEncoding / IntegratedFourierFeatures
+ *                  (+ IntegratedBarfFourierFeatures)     barf/positional_encodings.py:28-282
+ *                  fused with _compute_positions         barf/model_interpolation.py:288-312
+ *   - linear     : the nn.Linear (addmm) chain of NerfModel.forward
+ *                                                        barf/model_interpolation_architecture.py:96-141
+ *                  and its autograd backward (dX, dW, db)
+ *
+ * The reference has no FFI for this path (it is pure PyTorch); INTEGRATION.md
+ * shows the ctypes binding a maintainer would add, which is exactly what
+ * nerf-experiments_amd/nerf_amd/_lib.py does.
+ */
+#ifndef NERF_AMD_H
+#define NERF_AMD_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NERF_OK 0
+#define NERF_ERR_INVALID_ARG (-1)
+#define NERF_ERR_UNSUPPORTED (-2)
+#define NERF_ERR_LAUNCH (-3)
+#define NERF_ERR_WORKSPACE (-4)
+
+/* Library / ABI version (bumped on any signature change). */
+int nerf_abi_version(void);
+const char* nerf_status_string(int status);
+
+/* ---------------------------------------------------------------------------
+ * Alpha compositing (a4).  One wavefront per ray, exclusive prefix sum of
+ * b_s = ((-sigma_s * delta_s) * scale_a) * scale_b accumulated in fp64 (the
+ * reference's CPU cumsum accumulates fp32 input in double).
+ *   T_s = exp(sum_{j<s} b_j),  alpha_s = 1 - exp(b_s),  w_s = T_s * alpha_s,
+ *   rgb = sum_s w_s * c_s.
+ * Reference factor: scale_a = 3, scale_b = MAGIC_NUMBER (barf: 1/3, n2v/mip: 7);
+ * 3d-ingp uses scale_a = scale_b = 1.
+ * act = 0: density/color are already activated (the _render_rays contract).
+ * act = 1: density is raw, sigma = softplus(raw - density_shift, beta=1,
+ *          threshold=8) and color is raw, c = sigmoid(raw)  (NerfModel heads
+ *          fused in; model_interpolation_architecture.py:137-138).
+ * Addressing: sample n = ray*S + s; density[n*density_stride],
+ * color[n*color_stride + 0..2], dist[n], rgb_out[ray*3 + c], weights_out[n]
+ * (weights_out may be NULL).  S <= 1024.
+ * ------------------------------------------------------------------------- */
+int nerf_composite_fwd(const float* density, int64_t density_stride,
+                       const float* color, int64_t color_stride,
+                       const float* dist, int64_t n_rays, int32_t samples_per_ray,
+                       float scale_a, float scale_b, int32_t act, float density_shift,
+                       float* rgb_out, float* weights_out, void* stream);
+
+/* Backward of nerf_composite_fwd.  grad_rgb [n_rays,3]; grad_weights [n] or
+ * NULL.  Writes grad_density[n*gd_stride] and grad_color[n*gc_stride+0..2]
+ * (w.r.t. the raw inputs when act = 1).  Either output may be NULL. */
+int nerf_composite_bwd(const float* density, int64_t density_stride,
+                       const float* color, int64_t color_stride,
+                       const float* dist, int64_t n_rays, int32_t samples_per_ray,
+                       float scale_a, float scale_b, int32_t act, float density_shift,
+                       const float* grad_rgb, const float* grad_weights,
+                       float* grad_density, int64_t gd_stride,
+                       float* grad_color, int64_t gc_stride, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Stratified / equidistant t sampling (a6) + _get_intervals.
+ *   t_s = linspace(near, far - D, S)[s]  (D = (far-near)/S)
+ *         + (stratified ? U_{r,s} * D : 0) + (offset != 0 ? U_r * D * offset : 0)
+ *   t_start = t; t_end[s] = t[s+1], t_end[S-1] = far.
+ * U are Philox-4x32-10 uniforms in [0,1) keyed by (seed, offset_counter).
+ * ------------------------------------------------------------------------- */
+int nerf_sample_uniform(int64_t n_rays, int32_t samples_per_ray, float near_, float far_,
+                        int32_t stratified, float offset_size,
+                        uint64_t seed, uint64_t counter,
+                        float* t_start, float* t_end, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * PDF-weighted fine resampling (a5).  One wavefront per ray, n_bins <= 64.
+ * mode 0 (barf): largest-remainder integer allocation of n_samples - n_bins
+ *   fine samples (ties by index, as argsort().argsort() on CPU), +1 per bin,
+ *   exclusive scan, t_j = t_coarse_i + ((j - c_i) * dist_i) / n_i.
+ * mode 1 (naive-to-vanilla / 3d-ingp): round(w * (n_samples - n_bins)) with the
+ *   remainder added to the first argmax bin.
+ * If any ray's allocation is invalid (non-finite weights, wrong total) the
+ * whole batch falls back — as the reference does after its retry loop — to
+ * equidistant sampling with a per-ray offset of -U_r * D (model_interpolation.py:274-275),
+ * using (seed, counter) for U_r.  status (device int32, caller-zeroed) gets
+ * bit 0 set in that case.
+ * ------------------------------------------------------------------------- */
+int nerf_resample_pdf(const float* t_coarse, const float* weights, const float* dist_coarse,
+                      int64_t n_rays, int32_t n_bins, int32_t n_samples, int32_t mode,
+                      float near_, float far_, uint64_t seed, uint64_t counter,
+                      float* t_start, float* t_end, int32_t* status, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Positional encodings (a1-a3), fused with sample-position generation.
+ *
+ * Sample n (= ray*S + s).  Position source:
+ *   - x != NULL : position = x[n*3 .. n*3+2]   (S is ignored for positions)
+ *   - x == NULL : position = o[ray] + tq * d[ray], tq = t_start[n] (query=0,
+ *                 "left") or (t_start[n]+t_end[n])/2 (query=1, "middle").
+ * kind 0 = Fourier / BARF: args = p_d * (scale * 2^k) (fp32), out =
+ *   [p (if identity) | mask_k*cos(args) (d-major, k-minor) | mask_k*sin(args)].
+ *   use_mask == 0 means all ones (plain FourierFeatures).  levels <= 16.
+ * kind 1 = integrated (mip-NeRF IPE, positional_encodings.py:170-240); needs
+ *   dir (per ray, or the direction itself when x != NULL via xdir),
+ *   pixel_width (pw_mode 0: pw[ray]; 1: pw[n % n_rays] — the reference's
+ *   (B,)-shaped .repeat quirk; 2: pw[n]), t_start, t_end; variance
+ *   distributed if distribute_variance.  Optional BARF mask (IntegratedBarf...).
+ * out row stride out_ld >= output_dim; columns [output_dim, out_ld) are zeroed.
+ * ------------------------------------------------------------------------- */
+typedef struct nerf_pe_params {
+    int32_t kind;               /* 0 fourier/barf, 1 integrated */
+    int32_t levels;             /* L */
+    int32_t include_identity;   /* 0/1 */
+    int32_t query;              /* 0 left, 1 middle (ray mode) */
+    float scale;                /* base scale (2*pi, 1.0, ...) */
+    float pixel_width_sigma;    /* IPE extra variance when > 0.25 */
+    int32_t distribute_variance;/* IPE */
+    int32_t pw_mode;            /* IPE pixel width addressing */
+    int32_t use_mask;           /* 0: plain Fourier features */
+    float mask[16];             /* BARF coarse-to-fine mask values (by value: no
+                                   device copy and no int(alpha) sync per step) */
+} nerf_pe_params;
+
+int nerf_encode_fwd(const nerf_pe_params* params,
+                    const float* x, const float* xdir,
+                    const float* ray_o, const float* ray_d,
+                    const float* t_start, const float* t_end, const float* pixel_width,
+                    int64_t n_samples, int32_t samples_per_ray, int64_t n_rays,
+                    float* out, int64_t out_ld, void* stream);
+
+/* Backward of kind-0 encodings w.r.t. an explicit position input x:
+ *   dx[n,d] = g_id + sum_k mask_k*scale*2^k*(-g_cos*sin(a) + g_sin*cos(a)).
+ * grad_out has row stride g_ld. If accumulate, dx += ... */
+int nerf_encode_bwd(const nerf_pe_params* params, const float* x,
+                    const float* grad_out, int64_t g_ld, int64_t n_samples,
+                    float* dx, int32_t accumulate, void* stream);
+
+/* Per-ray direction encoding (dir PE evaluated once per ray instead of once
+ * per sample; the MLP reads row n / samples_per_ray).  kind 0 only. */
+int nerf_encode_rays(const nerf_pe_params* params, const float* ray_d, int64_t n_rays,
+                     float* out, int64_t out_ld, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Linear layers on fp32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 FMA chains).
+ *
+ * An operand is a column-concatenation of up to 4 row-major segments; segment
+ * j contributes columns [koff_j, koff_j + k_j) with k_j % 32 == 0, ld % 4 == 0,
+ * 16-byte aligned ptr; row m of the operand is row m / row_div_j of segment j
+ * (row_div > 1 broadcasts a per-ray tensor over its samples).
+ * ------------------------------------------------------------------------- */
+typedef struct nerf_seg {
+    const float* ptr;
+    int64_t ld;
+    int32_t k;
+    int32_t row_div;
+} nerf_seg;
+
+#define NERF_EPI_BIAS  1   /* + bias[n] */
+#define NERF_EPI_RELU  2   /* max(., 0) */
+#define NERF_EPI_MASK  4   /* * (aux[m, n] > 0): ReLU backward */
+#define NERF_EPI_ACCUM 8   /* out += result */
+
+/* out[m, n] = epi( sum_k A[m, k] * W[n, k] ),  m < M, n < N.
+ * W: packed row-major [ceil(N/128)*128][ldw], ldw = sum_j k_j (zero padding
+ * rows/cols).  out row stride ldo. */
+int nerf_linear_fwd(const nerf_seg* segs, int32_t n_segs, int64_t M,
+                    const float* W, int32_t ldw, int32_t N, const float* bias,
+                    float* out, int64_t ldo, int32_t epilogue,
+                    const float* aux, int64_t ld_aux, void* stream);
+
+/* Weight-gradient partials: for a grid of split-M slices,
+ *   slab[s][n][k] = sum_{m in slice s} dY[m, n] * X[m, k],
+ *   db_slab[s][n] = sum_{m in slice s} dY[m, n].
+ * workspace must hold nerf_linear_wgrad_workspace(...) bytes.  Then
+ * nerf_linear_wgrad_reduce (same M, N, K) sums the slices in a fixed order
+ * (deterministic) and scatters rows n < n_valid into dW[n, col_map[k]]
+ * (row stride ld_dw; col_map[k] < 0 skips; col_map NULL = identity) and db[n]
+ * (db may be NULL).  dY needs N % 4 == 0 and ld_dy % 4 == 0: pass N rounded up
+ * to 4 over a zero-padded dY and the true row count as n_valid. */
+size_t nerf_linear_wgrad_workspace(int64_t M, int32_t N, int32_t K);
+int nerf_linear_wgrad(const float* dY, int64_t ld_dy, int32_t N,
+                      const nerf_seg* segs, int32_t n_segs, int64_t M,
+                      void* workspace, size_t workspace_bytes, void* stream);
+int nerf_linear_wgrad_reduce(int64_t M, int32_t N, int32_t K, int32_t n_valid,
+                             const void* workspace, const int32_t* col_map,
+                             float* dW, int64_t ld_dw, float* db, void* stream);
+
+/* Pack an nn.Linear weight W[N][K_orig] into the kernel layouts:
+ *   Wp [ceil(N/128)*128][Kp]         Wp[n][k] = W[n][col_map[k]] (0 if map < 0 or n >= N)
+ *   Wt [ceil(Kp/128)*128 + 128][ldwt] Wt[k][n] = Wp[n][k] for n < N, 0 otherwise,
+ *                                    ldwt = ceil(N/32)*32 (the extra 128 zero
+ *                                    rows let any 32-aligned row window of Wt
+ *                                    be used as a 128-row-tiled B operand).
+ * Either output may be NULL. */
+int nerf_pack_weight(const float* W, int32_t N, int32_t K_orig, const int32_t* col_map,
+                     int32_t Kp, float* Wp, float* Wt, int32_t ldwt, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NERF_AMD_H */

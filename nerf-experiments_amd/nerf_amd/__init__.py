@@ -1,0 +1,10 @@
+"""nerf_amd — MI355X (gfx950) NeRF ray-marching hot path behind the
+sarphiv/nerf-experiments module API (positional_encodings, NerfModel,
+NerfInterpolation).  See DESIGN.md at the repository root."""
+from . import _lib, kernels  # noqa: F401
+from .positional_encodings import (BarfPositionalEncoding, FourierFeatures, IdentityPositionalEncoding,  # noqa: F401
+                                   IntegratedBarfFourierFeatures, IntegratedFourierFeatures, PositionalEncoding)
+from .model_interpolation_architecture import NerfBaseModel, NerfModel  # noqa: F401
+from .model_interpolation import MAGIC_NUMBER, NerfInterpolation, SchedulerLeNice  # noqa: F401
+
+__version__ = "0.1.0"

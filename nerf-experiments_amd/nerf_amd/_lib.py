@@ -1,0 +1,105 @@
+"""ctypes binding of the C-ABI library ``libnerf_amd.so`` (include/nerf_amd.h).
+
+This is the binding a maintainer of the reference would add:
+plain pointers, sizes and a ``hipStream_t`` per call.  ``torch`` must be imported
+first so that the library binds to the same ``libamdhip64.so.7`` (same SONAME)
+that PyTorch-ROCm already loaded — device pointers and streams are then shared.
+
+There is no fallback: if the library is missing, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be loaded before the HIP library, see above)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("NERF_AMD_LIB", os.path.join(_HERE, "libnerf_amd.so"))
+
+c_f = ctypes.c_float
+c_i32 = ctypes.c_int32
+c_i64 = ctypes.c_int64
+c_u64 = ctypes.c_uint64
+c_vp = ctypes.c_void_p
+c_sz = ctypes.c_size_t
+
+NERF_EPI_BIAS = 1
+NERF_EPI_RELU = 2
+NERF_EPI_MASK = 4
+NERF_EPI_ACCUM = 8
+
+
+class NerfSeg(ctypes.Structure):
+    _fields_ = [("ptr", c_vp), ("ld", c_i64), ("k", c_i32), ("row_div", c_i32)]
+
+
+class NerfPEParams(ctypes.Structure):
+    _fields_ = [
+        ("kind", c_i32),
+        ("levels", c_i32),
+        ("include_identity", c_i32),
+        ("query", c_i32),
+        ("scale", c_f),
+        ("pixel_width_sigma", c_f),
+        ("distribute_variance", c_i32),
+        ("pw_mode", c_i32),
+        ("use_mask", c_i32),
+        ("mask", c_f * 16),
+    ]
+
+
+# name -> (restype, argtypes)
+_SIGNATURES = {
+    "nerf_abi_version": (c_i32, []),
+    "nerf_status_string": (ctypes.c_char_p, [c_i32]),
+    "nerf_composite_fwd": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i32, c_f, c_f, c_i32, c_f,
+                                   c_vp, c_vp, c_vp]),
+    "nerf_composite_bwd": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i32, c_f, c_f, c_i32, c_f,
+                                   c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "nerf_sample_uniform": (c_i32, [c_i64, c_i32, c_f, c_f, c_i32, c_f, c_u64, c_u64, c_vp, c_vp, c_vp]),
+    "nerf_resample_pdf": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_f, c_f, c_u64, c_u64,
+                                  c_vp, c_vp, c_vp, c_vp]),
+    "nerf_encode_fwd": (c_i32, [ctypes.POINTER(NerfPEParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                c_i64, c_i32, c_i64, c_vp, c_i64, c_vp]),
+    "nerf_encode_bwd": (c_i32, [ctypes.POINTER(NerfPEParams), c_vp, c_vp, c_i64, c_i64, c_vp, c_i32, c_vp]),
+    "nerf_encode_rays": (c_i32, [ctypes.POINTER(NerfPEParams), c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "nerf_linear_fwd": (c_i32, [ctypes.POINTER(NerfSeg), c_i32, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp, c_i64,
+                                c_i32, c_vp, c_i64, c_vp]),
+    "nerf_linear_wgrad_workspace": (c_sz, [c_i64, c_i32, c_i32]),
+    "nerf_linear_wgrad": (c_i32, [c_vp, c_i64, c_i32, ctypes.POINTER(NerfSeg), c_i32, c_i64, c_vp, c_sz, c_vp]),
+    "nerf_linear_wgrad_reduce": (c_i32, [c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "nerf_pack_weight": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGNATURES.keys())
+
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load (once) and return the ctypes handle.  Raises if the library is absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(
+            f"nerf_amd: HIP library not found at {p}. Build it with `make -C nerf-experiments_amd` "
+            "(or __graft_entry__.build()); there is no CPU fallback.")
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.nerf_abi_version() != 1:
+        raise RuntimeError("nerf_amd: ABI version mismatch between Python binding and libnerf_amd.so")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        msg = load().nerf_status_string(status).decode()
+        raise RuntimeError(f"{what} failed with status {status}: {msg}")

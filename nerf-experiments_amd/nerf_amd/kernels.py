@@ -1,0 +1,249 @@
+"""Validated Python entry points for every C-ABI kernel.
+
+Each function checks device, dtype, contiguity and shapes (raising ``ValueError``
+like the reference's own asserts, e.g. positional_encodings.py:52,183 and
+model_interpolation.py:175,285), allocates outputs with the PyTorch caching
+allocator and launches on ``torch.cuda.current_stream()``.  No host
+synchronisation happens anywhere in this module.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import torch
+
+from . import _lib
+from ._lib import NerfPEParams, NerfSeg
+
+
+class KernelTimer:
+    """Optional HIP-event bracketing of the MFMA linear launches (used by bench.py).
+
+    Events are recorded on the same stream the kernel is launched on (torch's
+    current stream, which is the stream passed to the C-ABI), so
+    elapsed_time() is the kernel's device duration.  Records (tag, flops, start, end)."""
+
+    def __init__(self):
+        self.records = []
+
+    def bracket(self, tag: str, flops: float):
+        start = torch.cuda.Event(enable_timing=True)
+        end = torch.cuda.Event(enable_timing=True)
+        start.record()
+        self.records.append((tag, flops, start, end))
+        return end
+
+    def summary(self):
+        out = {}
+        for tag, flops, s, e in self.records:
+            ms = s.elapsed_time(e)
+            d = out.setdefault(tag, {"launches": 0, "flops": 0.0, "ms": 0.0})
+            d["launches"] += 1
+            d["flops"] += flops
+            d["ms"] += ms
+        return out
+
+
+TIMER: KernelTimer | None = None
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _require_cuda_f32(name: str, t: torch.Tensor) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise ValueError(f"{name} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name} must live on a ROCm device (got {t.device}); nerf_amd has no CPU path")
+    if t.dtype != torch.float32:
+        raise ValueError(f"{name} must be float32 (got {t.dtype})")
+
+
+def pad32(n: int) -> int:
+    return (n + 31) // 32 * 32
+
+
+def pad128(n: int) -> int:
+    return (n + 127) // 128 * 128
+
+
+# ----------------------------------------------------------------------------- composite
+def composite_fwd(density: torch.Tensor, density_stride: int, color: torch.Tensor, color_stride: int,
+                  dist: torch.Tensor, n_rays: int, samples_per_ray: int, scale_a: float, scale_b: float,
+                  act: bool, density_shift: float = 0.0, want_weights: bool = True):
+    _require_cuda_f32("density", density)
+    _require_cuda_f32("color", color)
+    _require_cuda_f32("dist", dist)
+    if not dist.is_contiguous() or dist.numel() != n_rays * samples_per_ray:
+        raise ValueError("dist must be contiguous with n_rays*samples_per_ray elements")
+    dev = dist.device
+    rgb = torch.empty(n_rays, 3, device=dev, dtype=torch.float32)
+    w = torch.empty(n_rays, samples_per_ray, device=dev, dtype=torch.float32) if want_weights else None
+    st = _lib.load().nerf_composite_fwd(_ptr(density), density_stride, _ptr(color), color_stride, _ptr(dist),
+                                        n_rays, samples_per_ray, scale_a, scale_b, int(act), density_shift,
+                                        _ptr(rgb), _ptr(w), _stream(dev))
+    _lib.check(st, "nerf_composite_fwd")
+    return rgb, w
+
+
+def composite_bwd(density, density_stride, color, color_stride, dist, n_rays, samples_per_ray, scale_a, scale_b,
+                  act, density_shift, grad_rgb, grad_weights, grad_density, gd_stride, grad_color, gc_stride):
+    grad_rgb = grad_rgb.contiguous()
+    if grad_weights is not None:
+        grad_weights = grad_weights.contiguous()
+    st = _lib.load().nerf_composite_bwd(_ptr(density), density_stride, _ptr(color), color_stride, _ptr(dist),
+                                        n_rays, samples_per_ray, scale_a, scale_b, int(act), density_shift,
+                                        _ptr(grad_rgb), _ptr(grad_weights), _ptr(grad_density), gd_stride,
+                                        _ptr(grad_color), gc_stride, _stream(dist.device))
+    _lib.check(st, "nerf_composite_bwd")
+
+
+# ----------------------------------------------------------------------------- sampling
+def sample_uniform(n_rays: int, samples_per_ray: int, near: float, far: float, stratified: bool,
+                   offset_size: float, seed: int, counter: int, device: torch.device):
+    t0 = torch.empty(n_rays, samples_per_ray, device=device, dtype=torch.float32)
+    t1 = torch.empty_like(t0)
+    st = _lib.load().nerf_sample_uniform(n_rays, samples_per_ray, near, far, int(stratified), offset_size,
+                                         seed, counter, _ptr(t0), _ptr(t1), _stream(device))
+    _lib.check(st, "nerf_sample_uniform")
+    return t0, t1
+
+
+def resample_pdf(t_coarse: torch.Tensor, weights: torch.Tensor, dist_coarse: torch.Tensor, n_samples: int,
+                 mode: int, near: float, far: float, seed: int, counter: int, status: torch.Tensor | None = None):
+    for name, t in (("t_coarse", t_coarse), ("weights", weights), ("distances_coarse", dist_coarse)):
+        _require_cuda_f32(name, t)
+    if t_coarse.dim() != 2 or weights.shape != t_coarse.shape or dist_coarse.shape != t_coarse.shape:
+        raise ValueError("t_coarse, weights and distances_coarse must share shape (batch_size, n_bins)")
+    t_coarse, weights, dist_coarse = t_coarse.contiguous(), weights.contiguous(), dist_coarse.contiguous()
+    n_rays, n_bins = t_coarse.shape
+    if n_samples < n_bins:
+        raise ValueError("n_samples must be >= the number of coarse bins")
+    dev = t_coarse.device
+    t0 = torch.empty(n_rays, n_samples, device=dev, dtype=torch.float32)
+    t1 = torch.empty_like(t0)
+    if status is None:
+        status = torch.zeros(1, device=dev, dtype=torch.int32)
+    st = _lib.load().nerf_resample_pdf(_ptr(t_coarse), _ptr(weights), _ptr(dist_coarse), n_rays, n_bins,
+                                       n_samples, mode, near, far, seed, counter, _ptr(t0), _ptr(t1),
+                                       _ptr(status), _stream(dev))
+    _lib.check(st, "nerf_resample_pdf")
+    return t0, t1, status
+
+
+# ----------------------------------------------------------------------------- encodings
+def make_pe_params(kind: int, levels: int, include_identity: bool, scale: float, query: int = 1,
+                   pixel_width_sigma: float = 0.0, distribute_variance: bool = False, pw_mode: int = 2,
+                   mask: Sequence[float] | None = None) -> NerfPEParams:
+    if levels > 16:
+        raise ValueError("levels > 16 is not supported")
+    p = NerfPEParams()
+    p.kind = kind
+    p.levels = levels
+    p.include_identity = int(bool(include_identity))
+    p.query = query
+    p.scale = scale
+    p.pixel_width_sigma = pixel_width_sigma
+    p.distribute_variance = int(bool(distribute_variance))
+    p.pw_mode = pw_mode
+    if mask is not None:
+        p.use_mask = 1
+        for i, m in enumerate(mask):
+            p.mask[i] = float(m)
+    else:
+        p.use_mask = 0
+    return p
+
+
+def encode_fwd(params: NerfPEParams, out_dim: int, *, x=None, xdir=None, ray_o=None, ray_d=None, t_start=None,
+               t_end=None, pixel_width=None, n_samples: int, samples_per_ray: int = 1, n_rays: int = 0,
+               out_ld: int | None = None, device=None) -> torch.Tensor:
+    ld = out_ld if out_ld is not None else pad32(out_dim)
+    for name, t in (("x", x), ("dir", xdir), ("ray_origs", ray_o), ("ray_dirs", ray_d), ("t_start", t_start),
+                    ("t_end", t_end), ("pixel_width", pixel_width)):
+        if t is not None:
+            _require_cuda_f32(name, t)
+            if not t.is_contiguous():
+                raise ValueError(f"{name} must be contiguous")
+    out = torch.empty(n_samples, ld, device=device, dtype=torch.float32)
+    st = _lib.load().nerf_encode_fwd(ctypes.byref(params), _ptr(x), _ptr(xdir), _ptr(ray_o), _ptr(ray_d),
+                                     _ptr(t_start), _ptr(t_end), _ptr(pixel_width), n_samples, samples_per_ray,
+                                     n_rays, _ptr(out), ld, _stream(out.device))
+    _lib.check(st, "nerf_encode_fwd")
+    return out
+
+
+def encode_bwd(params: NerfPEParams, x: torch.Tensor, grad_out: torch.Tensor, dx: torch.Tensor | None = None,
+               accumulate: bool = False) -> torch.Tensor:
+    n = x.shape[0]
+    if dx is None:
+        dx = torch.empty(n, 3, device=x.device, dtype=torch.float32)
+    if grad_out.stride(1) != 1:
+        grad_out = grad_out.contiguous()
+    st = _lib.load().nerf_encode_bwd(ctypes.byref(params), _ptr(x), _ptr(grad_out), grad_out.stride(0), n,
+                                     _ptr(dx), int(accumulate), _stream(x.device))
+    _lib.check(st, "nerf_encode_bwd")
+    return dx
+
+
+# ----------------------------------------------------------------------------- linear layers
+def make_segs(segs: Sequence[tuple[torch.Tensor, int, int]]):
+    """segs: (tensor, k, row_div); the tensor's row stride is its ld."""
+    arr = (NerfSeg * len(segs))()
+    for i, (t, k, rd) in enumerate(segs):
+        if t.stride(1) != 1:
+            raise ValueError("linear operand segments must be row-major")
+        arr[i].ptr = t.data_ptr()
+        arr[i].ld = t.stride(0)
+        arr[i].k = k
+        arr[i].row_div = rd
+    return arr
+
+
+def linear_fwd(segs, M: int, W: torch.Tensor, ldw: int, N: int, bias: torch.Tensor | None, out: torch.Tensor,
+               epilogue: int, aux: torch.Tensor | None = None, w_row_offset: int = 0) -> None:
+    arr = make_segs(segs)
+    wptr = W.data_ptr() + w_row_offset * ldw * 4
+    end = TIMER.bracket("linear_nt", 2.0 * M * N * ldw) if TIMER is not None else None
+    st = _lib.load().nerf_linear_fwd(arr, len(segs), M, wptr, ldw, N, _ptr(bias), _ptr(out), out.stride(0),
+                                     epilogue, _ptr(aux), aux.stride(0) if aux is not None else 0,
+                                     _stream(out.device))
+    if end is not None:
+        end.record()
+    _lib.check(st, "nerf_linear_fwd")
+
+
+def linear_wgrad(dY: torch.Tensor, N4: int, segs, M: int, workspace: torch.Tensor) -> None:
+    arr = make_segs(segs)
+    kt = sum(k for _, k, _ in segs)
+    end = TIMER.bracket("linear_wgrad", 2.0 * M * N4 * kt) if TIMER is not None else None
+    st = _lib.load().nerf_linear_wgrad(_ptr(dY), dY.stride(0), N4, arr, len(segs), M, _ptr(workspace),
+                                       workspace.numel() * workspace.element_size(), _stream(dY.device))
+    if end is not None:
+        end.record()
+    _lib.check(st, "nerf_linear_wgrad")
+
+
+def linear_wgrad_workspace_bytes(M: int, N4: int, K: int) -> int:
+    return int(_lib.load().nerf_linear_wgrad_workspace(M, N4, K))
+
+
+def linear_wgrad_reduce(M: int, N4: int, K: int, n_valid: int, workspace: torch.Tensor, col_map: torch.Tensor,
+                        dW: torch.Tensor, db: torch.Tensor | None) -> None:
+    st = _lib.load().nerf_linear_wgrad_reduce(M, N4, K, n_valid, _ptr(workspace), _ptr(col_map), _ptr(dW),
+                                              dW.stride(0), _ptr(db), _stream(dW.device))
+    _lib.check(st, "nerf_linear_wgrad_reduce")
+
+
+def pack_weight(W: torch.Tensor, col_map: torch.Tensor, Kp: int, Wp: torch.Tensor | None,
+                Wt: torch.Tensor | None, ldwt: int) -> None:
+    N, K_orig = W.shape
+    st = _lib.load().nerf_pack_weight(_ptr(W), N, K_orig, _ptr(col_map), Kp, _ptr(Wp), _ptr(Wt), ldwt,
+                                      _stream(W.device))
+    _lib.check(st, "nerf_pack_weight")

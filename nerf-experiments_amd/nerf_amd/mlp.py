@@ -1,0 +1,269 @@
+"""Execution plan + autograd for NeRF field MLPs on the fp32 MFMA linear kernels.
+
+A field MLP (NerfModel, NerfModelINGP, ...) is lowered once into a list of
+``LayerPlan``s.  Each layer reads a column-concatenation of *sources* —
+the padded position encoding ("pos"), the (per-sample or per-ray) direction
+encoding ("dir") or an earlier layer's output ("act", j) — so the reference's
+``th.cat`` copies (model_interpolation_architecture.py:111-125) never exist.
+Weights are repacked into the kernels' K-padded layout (and its transpose for
+the input-gradient GEMMs) only when a parameter's version counter changed.
+
+``MLPFunction`` is one autograd node for the whole network:
+  forward : one ``nerf_linear_fwd`` launch per layer (bias + ReLU fused), all
+            layer outputs kept for backward;
+  backward: per layer (in reverse) one ``nerf_linear_wgrad`` + reduce for
+            (dW, db) and one ``nerf_linear_fwd`` per consumed source for dX,
+            with the ReLU mask of the producing layer fused into its epilogue.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+import torch.nn as nn
+
+from . import kernels as K
+from ._lib import NERF_EPI_ACCUM, NERF_EPI_BIAS, NERF_EPI_MASK, NERF_EPI_RELU
+
+
+@dataclass
+class Source:
+    kind: str          # "pos" | "dir" | "act"
+    k_valid: int       # columns of the source consumed (reference layout width)
+    k_pad: int         # columns in the padded buffer consumed by the kernel
+    layer: int = -1    # producing layer for "act"
+
+
+@dataclass
+class LayerPlan:
+    module: nn.Linear
+    sources: list[Source]
+    relu: bool
+    N: int = 0
+    out_ld: int = 0
+    Kp: int = 0
+    ldwt: int = 0
+    koffs: list[int] = field(default_factory=list)
+    col_map: torch.Tensor | None = None
+    Wp: torch.Tensor | None = None
+    Wt: torch.Tensor | None = None
+    packed_version: tuple = ()
+
+    def finalize(self, device):
+        self.N = self.module.out_features
+        self.out_ld = K.pad32(self.N)
+        self.ldwt = K.pad32(self.N)
+        cm = []
+        orig = 0
+        self.koffs = []
+        kp = 0
+        for s in self.sources:
+            self.koffs.append(kp)
+            for j in range(s.k_pad):
+                cm.append(orig + j if j < s.k_valid else -1)
+            orig += s.k_valid
+            kp += s.k_pad
+        if orig != self.module.in_features:
+            raise ValueError(f"layer input width mismatch: sources give {orig}, Linear expects "
+                             f"{self.module.in_features}")
+        self.Kp = kp
+        self.col_map = torch.tensor(cm, dtype=torch.int32, device=device)
+        self.Wp = torch.empty(K.pad128(self.N), self.Kp, device=device, dtype=torch.float32)
+        self.Wt = torch.empty(K.pad128(self.Kp) + 128, self.ldwt, device=device, dtype=torch.float32)
+        self.packed_version = ()
+
+    def pack(self):
+        w = self.module.weight
+        ver = (w._version, w.data_ptr())
+        if ver != self.packed_version:
+            K.pack_weight(w.detach().contiguous(), self.col_map, self.Kp, self.Wp, self.Wt, self.ldwt)
+            self.packed_version = ver
+
+
+class MLPPlan:
+    """Layers in execution order; ``outputs`` are layer indices exposed to autograd."""
+
+    def __init__(self, layers: list[LayerPlan], outputs: list[int]):
+        self.layers = layers
+        self.outputs = outputs
+        self.device = None
+        self.consumed = [False] * len(layers)
+        for lp in layers:
+            for s in lp.sources:
+                if s.kind == "act":
+                    self.consumed[s.layer] = True
+
+    def to_device(self, device):
+        if self.device != device:
+            for lp in self.layers:
+                lp.finalize(device)
+            self.device = device
+
+    def params(self):
+        ps = []
+        for lp in self.layers:
+            ps += [lp.module.weight, lp.module.bias]
+        return ps
+
+
+def _src_tensor(src: Source, pos, dirs, acts, dir_rd):
+    if src.kind == "pos":
+        return pos, 1
+    if src.kind == "dir":
+        return dirs, dir_rd
+    return acts[src.layer], 1
+
+
+class MLPFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, plan: MLPPlan, M: int, pos: torch.Tensor, dirs: torch.Tensor | None, dir_rd: int, *params):
+        plan.to_device(pos.device)
+        acts: list[torch.Tensor] = []
+        for lp in plan.layers:
+            lp.pack()
+            segs = []
+            for s in lp.sources:
+                t, rd = _src_tensor(s, pos, dirs, acts, dir_rd)
+                segs.append((t, s.k_pad, rd))
+            out = torch.empty(M, lp.out_ld, device=pos.device, dtype=torch.float32)
+            epi = NERF_EPI_BIAS | (NERF_EPI_RELU if lp.relu else 0)
+            K.linear_fwd(segs, M, lp.Wp, lp.Kp, lp.N, lp.module.bias, out, epi)
+            acts.append(out)
+        ctx.plan = plan
+        ctx.M = M
+        ctx.dir_rd = dir_rd
+        ctx.has_dirs = dirs is not None
+        ctx.save_for_backward(pos, dirs if dirs is not None else pos, *acts)
+        return tuple(acts[i] for i in plan.outputs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        plan: MLPPlan = ctx.plan
+        M = ctx.M
+        saved = ctx.saved_tensors
+        pos = saved[0]
+        dirs = saved[1] if ctx.has_dirs else None
+        acts = list(saved[2:])
+        dev = pos.device
+        L = len(plan.layers)
+        dY: list[torch.Tensor | None] = [None] * L
+        for idx, g in zip(plan.outputs, grads):
+            if g is None:
+                continue
+            if g.shape != (M, plan.layers[idx].out_ld):
+                raise RuntimeError(f"unexpected gradient shape {tuple(g.shape)} for MLP output {idx}")
+            # outputs that also feed a later layer are accumulated into: never write autograd's tensor
+            dY[idx] = g.contiguous().clone() if plan.consumed[idx] else g.contiguous()
+        need_pos = ctx.needs_input_grad[2]
+        need_dir = ctx.needs_input_grad[3]
+        dpos = None
+        ddir = None
+        param_grads: list[torch.Tensor | None] = [None] * (2 * L)
+
+        # one workspace sized for the largest weight-gradient launch
+        ws_bytes = 0
+        for lp in plan.layers:
+            ws_bytes = max(ws_bytes, K.linear_wgrad_workspace_bytes(M, (lp.N + 3) // 4 * 4, lp.Kp))
+        workspace = torch.empty((ws_bytes + 3) // 4, device=dev, dtype=torch.float32)
+
+        for li in range(L - 1, -1, -1):
+            lp = plan.layers[li]
+            dZ = dY[li]
+            w = lp.module.weight
+            if dZ is None:
+                param_grads[2 * li] = torch.zeros_like(w)
+                param_grads[2 * li + 1] = torch.zeros_like(lp.module.bias)
+                continue
+            segs = []
+            for s in lp.sources:
+                t, rd = _src_tensor(s, pos, dirs, acts, ctx.dir_rd)
+                segs.append((t, s.k_pad, rd))
+            # ---- weight and bias gradients
+            N4 = (lp.N + 3) // 4 * 4
+            gW = torch.empty_like(w)
+            gb = torch.empty_like(lp.module.bias)
+            K.linear_wgrad(dZ, N4, segs, M, workspace)
+            K.linear_wgrad_reduce(M, N4, lp.Kp, lp.N, workspace, lp.col_map, gW, gb)
+            param_grads[2 * li] = gW
+            param_grads[2 * li + 1] = gb
+            # ---- input gradients
+            a_seg = [(dZ, lp.ldwt, 1)]
+            for s, koff in zip(lp.sources, lp.koffs):
+                if s.kind == "act":
+                    j = s.layer
+                    prod = plan.layers[j]
+                    epi = 0
+                    aux = None
+                    if prod.relu:
+                        epi |= NERF_EPI_MASK
+                        aux = acts[j]
+                    if dY[j] is None:
+                        if prod.out_ld > s.k_valid:
+                            dY[j] = torch.zeros(M, prod.out_ld, device=dev, dtype=torch.float32)
+                        else:
+                            dY[j] = torch.empty(M, prod.out_ld, device=dev, dtype=torch.float32)
+                    else:
+                        epi |= NERF_EPI_ACCUM
+                    K.linear_fwd(a_seg, M, lp.Wt, lp.ldwt, s.k_valid, None, dY[j], epi, aux=aux,
+                                 w_row_offset=koff)
+                elif s.kind == "pos" and need_pos:
+                    if dpos is None:
+                        dpos = torch.empty(M, s.k_pad, device=dev, dtype=torch.float32)
+                        epi = 0
+                    else:
+                        epi = NERF_EPI_ACCUM
+                    K.linear_fwd(a_seg, M, lp.Wt, lp.ldwt, s.k_pad, None, dpos, epi, w_row_offset=koff)
+                elif s.kind == "dir" and need_dir:
+                    if ddir is None:
+                        ddir = torch.empty(M, s.k_pad, device=dev, dtype=torch.float32)
+                        epi = 0
+                    else:
+                        epi = NERF_EPI_ACCUM
+                    K.linear_fwd(a_seg, M, lp.Wt, lp.ldwt, s.k_pad, None, ddir, epi, w_row_offset=koff)
+        if ddir is not None and ctx.dir_rd > 1:
+            ddir = ddir.view(-1, ctx.dir_rd, ddir.shape[1]).sum(dim=1)
+        return (None, None, dpos, ddir, None, *param_grads)
+
+
+def nerf_model_plan(n_segments: int, model_segments: nn.ModuleList, model_color: nn.Sequential,
+                    hidden_dim: int, pos_dim: int, dir_dim: int, delayed_direction: bool,
+                    delayed_density: bool) -> tuple[MLPPlan, int, int]:
+    """Lower NerfModel (barf/model_interpolation_architecture.py:33-161).
+
+    Segment i input = [z_{i-1} | dir (if not delayed_direction) | pos]; inside a
+    segment every Linear but the last is followed by ReLU; the last one is
+    followed by ReLU only between segments.  Head input = [z_last[:, :D] | dir
+    (if delayed_direction)] -> Linear -> ReLU -> Linear.
+    Returns (plan, index of the last segment layer, index of the head output layer).
+    """
+    layers: list[LayerPlan] = []
+    pos_src = Source("pos", pos_dim, K.pad32(pos_dim))
+    dir_src = Source("dir", dir_dim, K.pad32(dir_dim))
+    prev = -1
+    for i in range(n_segments):
+        seg = model_segments[i]
+        linears = [m for m in seg.modules() if isinstance(m, nn.Linear)] if isinstance(seg, nn.Sequential) \
+            else [seg]
+        for j, lin in enumerate(linears):
+            srcs: list[Source] = []
+            if j == 0:
+                if prev >= 0:
+                    srcs.append(Source("act", hidden_dim, hidden_dim, prev))
+                if not delayed_direction:
+                    srcs.append(dir_src)
+                srcs.append(pos_src)
+            else:
+                srcs.append(Source("act", hidden_dim, hidden_dim, len(layers) - 1))
+            last_in_seg = j == len(linears) - 1
+            relu = (not last_in_seg) or (i < n_segments - 1)
+            layers.append(LayerPlan(lin, srcs, relu))
+        prev = len(layers) - 1
+    z_last = prev
+    head0, head1 = model_color[0], model_color[2]
+    srcs = [Source("act", hidden_dim, hidden_dim, z_last)]
+    if delayed_direction:
+        srcs.append(dir_src)
+    layers.append(LayerPlan(head0, srcs, True))
+    layers.append(LayerPlan(head1, [Source("act", head0.out_features, head0.out_features, len(layers) - 1)], False))
+    head_out = len(layers) - 1
+    return MLPPlan(layers, [z_last, head_out]), z_last, head_out

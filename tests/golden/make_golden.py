@@ -1,0 +1,272 @@
+"""Generate golden input/output vectors by running the REFERENCE implementation.
+
+Runs only in the build container, where the read-only reference checkout is at
+/root/reference (override with NERF_REFERENCE).  The reference source never
+leaves that directory: this script imports it (with two import stubs for the
+absent pytorch_lightning / data modules), evaluates it on seeded inputs and
+writes plain arrays (inputs and expected outputs) to tests/golden/*.npz.
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+Fixtures:
+  pe.npz         FourierFeatures / BarfPositionalEncoding (+ d/dx) / IntegratedFourierFeatures /
+                 IntegratedBarfFourierFeatures / mip_NeRF IntegratedFourierFeatures outputs
+  composite.npz  NerfInterpolation._render_rays outputs and input gradients
+  resample.npz   _sample_t_pdf_weighted (barf) and _sample_t_fine (naive-to-vanilla) outputs
+  model.npz      NerfModel (barf config and naive-to-vanilla config): weights, inputs, outputs, gradients
+  color.npz      _compute_color end to end with explicit t, and forward coarse+fine with injected t
+  cos_kat.npz    barf/cos_test_barf.pt (the reference's own fixture, loaded weights_only)
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import sys
+import types
+
+import numpy as np
+import torch as th
+
+REF = os.environ.get("NERF_REFERENCE", "/root/reference")
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _install_stubs():
+    pl = types.ModuleType("pytorch_lightning")
+
+    class LightningModule(th.nn.Module):
+        def save_hyperparameters(self, *a, **k):
+            pass
+
+        @property
+        def device(self):
+            return th.device("cpu")
+
+        def log_dict(self, *a, **k):
+            pass
+
+    pl.LightningModule = LightningModule
+    sys.modules["pytorch_lightning"] = pl
+    for name in ("data_module", "dataset"):
+        m = types.ModuleType(name)
+        m.DatasetOutput = tuple
+        m.ImagePoseDataModule = object
+        sys.modules[name] = m
+
+
+def _import_from(subdir: str, names: list[str]):
+    """Import reference modules from one experiment directory (bare-name imports)."""
+    for n in names + ["model_interpolation_architecture", "positional_encodings", "model_interpolation", "magic"]:
+        sys.modules.pop(n, None)
+    sys.path.insert(0, os.path.join(REF, subdir))
+    try:
+        return [importlib.import_module(n) for n in names]
+    finally:
+        sys.path.pop(0)
+
+
+def f32(t):
+    return t.detach().cpu().numpy().astype(np.float32)
+
+
+def gen_pe():
+    (pe,) = _import_from("barf", ["positional_encodings"])
+    g = th.Generator().manual_seed(1)
+    N = 257
+    x = (th.rand(N, 3, generator=g) * 16 - 8)
+    d = th.randn(N, 3, generator=g)
+    d = d / th.linalg.vector_norm(d, dim=1, keepdim=True)
+    t0 = 2 + th.rand(N, 1, generator=g) * 6
+    t1 = t0 + th.rand(N, 1, generator=g) * 0.1 + 1e-3
+    out = {"x": f32(x), "dir": f32(d), "t0": f32(t0), "t1": f32(t1)}
+    out["fourier_L10_2pi"] = f32(pe.FourierFeatures(10, 2 * th.pi).forward(x))
+    out["fourier_L4_1"] = f32(pe.FourierFeatures(4, 1.0).forward(d))
+    for alpha in (0.0, 3.4, 10.0):
+        for ident in (True, False):
+            for scale, sname in ((1.0, "1"), (2 * th.pi, "2pi")):
+                enc = pe.BarfPositionalEncoding(10, alpha, 0, 1, ident, scale)
+                xx = x.clone().requires_grad_(True)
+                y = enc.forward(xx)
+                gy = th.randn(y.shape, generator=g)
+                (y * gy).sum().backward()
+                key = f"barf_L10_a{alpha}_id{int(ident)}_s{sname}"
+                out[key] = f32(y)
+                out[key + "_gy"] = f32(gy)
+                out[key + "_dx"] = f32(xx.grad)
+    enc = pe.BarfPositionalEncoding(10, 0.0, 10.0, 20.0, True, 1.0)
+    enc.update_alpha(13.7)
+    out["barf_update_alpha_13.7"] = np.array([float(enc.alpha)], np.float32)
+    out["barf_mask_a3.4"] = f32(pe.BarfPositionalEncoding(10, 3.4, 0, 1, True, 1.0).compute_mask(th.tensor(3.4)))
+    for pw, pwname in ((1 / 555.56, "400"), (1 / 1111.1, "800")):
+        pwt = th.full((N, 1), pw)
+        out[f"pw_{pwname}"] = f32(pwt)
+        for dv in (True, False):
+            for pws in (0.0, 0.5):
+                enc = pe.IntegratedFourierFeatures(10, 2 * th.pi, True, dv)
+                enc.pixel_width_sigma = pws
+                out[f"ipe_{pwname}_dv{int(dv)}_pws{pws}"] = f32(enc.forward(x, d, pwt, t0, t1))
+        enc = pe.IntegratedBarfFourierFeatures(10, 3.4, 0, 1, True, 1.0, True)
+        enc.pixel_width_sigma = 0.0
+        out[f"ipebarf_{pwname}_a3.4"] = f32(enc.forward(x, d, pwt, t0, t1))
+    # older mip_NeRF variant: no identity, scale 2*pi, (pos, dir, t_start, t_end, pixel_width) order
+    (mm,) = _import_from("mip_NeRF", ["mip_model"])
+    enc = mm.IntegratedFourierFeatures(10, 2 * th.pi, True)
+    out["mipnerf_ipe_800"] = f32(enc.forward(x, d, t0, t1, 1 / 1111.1))
+    np.savez_compressed(os.path.join(OUT, "pe.npz"), **out)
+
+
+def gen_composite():
+    (mi,) = _import_from("barf", ["model_interpolation"])
+    g = th.Generator().manual_seed(2)
+    out = {}
+    for S in (64, 128, 192):
+        B = 48
+        sig = th.nn.functional.softplus(th.randn(B, S, generator=g) * 4)
+        col = th.rand(B, S, 3, generator=g)
+        t = th.sort(2 + th.rand(B, S, generator=g) * 6, dim=1).values
+        dist = th.diff(t, dim=1, append=th.full((B, 1), 8.0))
+        model = mi.NerfInterpolation.__new__(mi.NerfInterpolation)
+        th.nn.Module.__init__(model)
+        sig_ = sig.clone().requires_grad_(True)
+        col_ = col.clone().requires_grad_(True)
+        rgb, w = model._render_rays(sig_, col_, dist)
+        grgb = th.randn(B, 3, generator=g)
+        gw = th.randn(B, S, generator=g)
+        ((rgb * grgb).sum() + (w * gw).sum()).backward()
+        k = f"S{S}"
+        out.update({f"{k}_sigma": f32(sig), f"{k}_color": f32(col), f"{k}_dist": f32(dist), f"{k}_rgb": f32(rgb),
+                    f"{k}_w": f32(w), f"{k}_grgb": f32(grgb), f"{k}_gw": f32(gw), f"{k}_dsigma": f32(sig_.grad),
+                    f"{k}_dcolor": f32(col_.grad)})
+    np.savez_compressed(os.path.join(OUT, "composite.npz"), **out)
+
+
+def _weights_suite(g, B, K):
+    w = th.nn.functional.softplus(th.randn(B, K, generator=g) * 3) * (th.rand(B, K, generator=g) < 0.7)
+    w = w / (w.sum(1, keepdim=True) + 1e-3)
+    w[0] = 0
+    w[0, 5] = 1.0                      # one-hot
+    w[1] = 1.0 / K                     # uniform: every fractional part ties
+    w[2] = 0
+    w[2, :3] = th.tensor([0.25, 0.25, 0.5])  # exact zeros elsewhere
+    w[3] = th.linspace(0, 1, K)        # ramp
+    w[4] = 0
+    w[4, -1] = 1e-30                   # tiny but valid
+    return w
+
+
+def gen_resample():
+    (mi,) = _import_from("barf", ["model_interpolation"])
+    g = th.Generator().manual_seed(3)
+    out = {}
+    model = mi.NerfInterpolation.__new__(mi.NerfInterpolation)
+    th.nn.Module.__init__(model)
+    model.far_sphere_normalized = 8.0
+    B, K = 64, 64
+    for N in (128, 256):
+        tc = th.sort(2 + th.rand(B, K, generator=g) * 6, dim=1).values
+        dist = th.diff(tc, dim=1, append=th.full((B, 1), 8.0))
+        w = _weights_suite(g, B, K)
+        t0, t1 = model._sample_t_pdf_weighted(tc, w, dist, N)
+        out.update({f"barf_N{N}_tc": f32(tc), f"barf_N{N}_w": f32(w), f"barf_N{N}_dist": f32(dist),
+                    f"barf_N{N}_t0": f32(t0), f"barf_N{N}_t1": f32(t1)})
+    # naive-to-vanilla round/argmax variant (K = 64 coarse + 192 fine)
+    (n2v,) = _import_from("naive-to-vanilla", ["model_interpolation"])
+    m2 = n2v.NerfInterpolation.__new__(n2v.NerfInterpolation)
+    th.nn.Module.__init__(m2)
+    m2.samples_per_ray_coarse, m2.samples_per_ray_fine, m2.far_sphere_normalized = 64, 192, 1 / 3
+    tc = th.sort(0.1 + th.rand(B, K, generator=g) * (1 / 3 - 0.1), dim=1).values
+    dist = th.diff(tc, dim=1, append=th.full((B, 1), 1 / 3))
+    w = _weights_suite(g, B, K)
+    w = w * 0.9  # the reference variant does not renormalise
+    t0, t1 = m2._sample_t_fine(tc, w, dist)
+    out.update({"n2v_tc": f32(tc), "n2v_w": f32(w), "n2v_dist": f32(dist), "n2v_t0": f32(t0), "n2v_t1": f32(t1)})
+    np.savez_compressed(os.path.join(OUT, "resample.npz"), **out)
+
+
+def _barf_models(pe, mia):
+    th.manual_seed(0)
+    barf = mia.NerfModel(4, 256, True, False, 2, pe.BarfPositionalEncoding(10, 10.0, 0, 1, True, 1.0),
+                         pe.BarfPositionalEncoding(4, 4.0, 0, 1, True, 1.0))
+    th.manual_seed(0)
+    n2v = mia.NerfModel(4, 256, True, True, 2, pe.FourierFeatures(10, 2 * th.pi), pe.FourierFeatures(4, 1.0))
+    th.manual_seed(0)
+    small = mia.NerfModel(2, 64, False, False, 3, pe.BarfPositionalEncoding(6, 3.4, 0, 1, True, 1.0),
+                          pe.BarfPositionalEncoding(2, 1.5, 0, 1, False, 1.0))
+    return {"barf": barf, "n2v": n2v, "small": small}
+
+
+def gen_model():
+    pe, mia = _import_from("barf", ["positional_encodings", "model_interpolation_architecture"])
+    g = th.Generator().manual_seed(4)
+    out = {}
+    N = 300
+    pos = th.rand(N, 3, generator=g) * 4 - 2
+    d = th.randn(N, 3, generator=g)
+    d = d / th.linalg.vector_norm(d, dim=1, keepdim=True)
+    out["pos"], out["dir"] = f32(pos), f32(d)
+    for name, m in _barf_models(pe, mia).items():
+        # weights are not stored: the build re-creates them from th.manual_seed(0) (same construction
+        # order) and these per-tensor checksums prove the initial weights are identical
+        for k, v in m.state_dict().items():
+            out[f"{name}.sdsum.{k}"] = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+        p = pos.clone().requires_grad_(True)
+        dens, rgb = m.forward(p, d, None, None, None)
+        gd = th.randn(N, generator=g)
+        gc = th.randn(N, 3, generator=g)
+        ((dens * gd).sum() + (rgb * gc).sum()).backward()
+        out[f"{name}.density"], out[f"{name}.rgb"] = f32(dens), f32(rgb)
+        out[f"{name}.gd"], out[f"{name}.gc"] = f32(gd), f32(gc)
+        out[f"{name}.dpos"] = f32(p.grad)
+        for k, prm in m.named_parameters():
+            if k.endswith(".bias") or k in ("model_segments.0.0.weight", "model_color.2.weight",
+                                            "model_color.0.weight"):
+                out[f"{name}.grad.{k}"] = f32(prm.grad)
+            out[f"{name}.gradsum.{k}"] = np.array([prm.grad.double().sum().item(),
+                                                   prm.grad.double().abs().sum().item()])
+    np.savez_compressed(os.path.join(OUT, "model.npz"), **out)
+
+
+def gen_color():
+    pe, mia, mi = _import_from("barf", ["positional_encodings", "model_interpolation_architecture",
+                                        "model_interpolation"])
+    g = th.Generator().manual_seed(5)
+    out = {}
+    B, Kc, Nf = 24, 64, 128
+    o = th.randn(B, 3, generator=g)
+    o = o / th.linalg.vector_norm(o, dim=1, keepdim=True) * 4.03
+    tgt = th.randn(B, 3, generator=g) * 0.3
+    d = tgt - o
+    d = d / th.linalg.vector_norm(d, dim=1, keepdim=True)
+    pw = th.full((B,), 1 / 1111.1)
+    th.manual_seed(0)
+    model = mia.NerfModel(4, 256, True, False, 2, pe.BarfPositionalEncoding(10, 10.0, 0, 1, True, 1.0),
+                          pe.BarfPositionalEncoding(4, 4.0, 0, 1, True, 1.0))
+    ren = mi.NerfInterpolation(2.0, 8.0, model, Nf, "stratified_uniform", 0.0, "middle", model, Kc)
+    tc = th.sort(2 + th.rand(B, Kc, generator=g) * 6, dim=1).values
+    t0, t1 = ren._get_intervals(tc)
+    rgb, w, dist = ren._compute_color(model, t0, t1, o, d, pw, B, Kc)
+    out.update({"o": f32(o), "d": f32(d), "pw": f32(pw), "tc": f32(tc), "rgb": f32(rgb), "w": f32(w)})
+    # forward coarse+fine with the coarse t injected (RNG-free)
+    ren._sample_t_stratified_uniform = lambda *a, **k: ren._get_intervals(tc.clone())
+    rgb_f, rgb_c = ren.forward(o, d, pw)
+    out["fwd_rgb_fine"], out["fwd_rgb_coarse"] = f32(rgb_f), f32(rgb_c)
+    np.savez_compressed(os.path.join(OUT, "color.npz"), **out)
+
+
+def gen_cos_kat():
+    t = th.load(os.path.join(REF, "barf", "cos_test_barf.pt"), weights_only=True)
+    np.savez_compressed(os.path.join(OUT, "cos_kat.npz"), cos=f32(t))
+
+
+if __name__ == "__main__":
+    _install_stubs()
+    th.set_num_threads(8)
+    gen_pe()
+    gen_composite()
+    gen_resample()
+    gen_model()
+    gen_color()
+    gen_cos_kat()
+    for f in sorted(os.listdir(OUT)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(OUT, f)))

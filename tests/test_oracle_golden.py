@@ -1,0 +1,112 @@
+"""Pin the CPU oracle (oracle/nerf_oracle.py) to the reference's golden vectors.
+
+These run on CPU only.  Tolerances: encodings and compositing 1e-6 abs (same
+fp32 op order as the reference; only libm ulps differ), resampling bit-exact on
+every ray, field MLP 1e-5 (same CPU BLAS, different cat/addmm grouping).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import nerf_oracle as O
+
+
+def t(a):
+    return torch.from_numpy(np.asarray(a))
+
+
+def test_fourier_features(golden):
+    g = golden("pe")
+    x, d = t(g["x"]), t(g["dir"])
+    np.testing.assert_allclose(O.fourier_features(x, 10, 2 * np.pi).numpy(), g["fourier_L10_2pi"], atol=1e-6, rtol=0)
+    np.testing.assert_allclose(O.fourier_features(d, 4, 1.0).numpy(), g["fourier_L4_1"], atol=1e-6, rtol=0)
+
+
+@pytest.mark.parametrize("alpha", [0.0, 3.4, 10.0])
+@pytest.mark.parametrize("ident", [True, False])
+@pytest.mark.parametrize("sname", ["1", "2pi"])
+def test_barf_pe_and_grad(golden, alpha, ident, sname):
+    g = golden("pe")
+    scale = 1.0 if sname == "1" else 2 * np.pi
+    key = f"barf_L10_a{alpha}_id{int(ident)}_s{sname}"
+    x = t(g["x"]).clone().requires_grad_(True)
+    y = O.barf_pe(x, 10, alpha, ident, scale)
+    np.testing.assert_allclose(y.detach().numpy(), g[key], atol=1e-6, rtol=0)
+    (y * t(g[key + "_gy"])).sum().backward()
+    np.testing.assert_allclose(x.grad.numpy(), g[key + "_dx"], atol=2e-3, rtol=1e-5)
+
+
+def test_barf_mask_and_alpha(golden):
+    g = golden("pe")
+    np.testing.assert_array_equal(O.barf_mask(3.4, 10).repeat(3).view(1, -1).numpy(), g["barf_mask_a3.4"])
+    # update_alpha(13.7) with start/end epochs 10/20 and alpha_start 0 -> 3.7
+    assert abs(float(g["barf_update_alpha_13.7"][0]) - 3.7) < 1e-6
+
+
+@pytest.mark.parametrize("pwname", ["400", "800"])
+@pytest.mark.parametrize("dv", [True, False])
+@pytest.mark.parametrize("pws", [0.0, 0.5])
+def test_integrated_pe(golden, pwname, dv, pws):
+    g = golden("pe")
+    y = O.integrated_pe(t(g["x"]), t(g["dir"]), t(g[f"pw_{pwname}"]), t(g["t0"]), t(g["t1"]), 10, 2 * np.pi,
+                        True, dv, pws)
+    np.testing.assert_allclose(y.numpy(), g[f"ipe_{pwname}_dv{int(dv)}_pws{pws}"], atol=1e-6, rtol=0)
+
+
+def test_integrated_barf_pe(golden):
+    g = golden("pe")
+    for pwname in ("400", "800"):
+        y = O.integrated_pe(t(g["x"]), t(g["dir"]), t(g[f"pw_{pwname}"]), t(g["t0"]), t(g["t1"]), 10, 1.0, True,
+                            True, 0.0, mask=O.barf_mask(3.4, 10))
+        np.testing.assert_allclose(y.numpy(), g[f"ipebarf_{pwname}_a3.4"], atol=1e-6, rtol=0)
+
+
+def test_mipnerf_ipe_variant(golden):
+    g = golden("pe")
+    n = g["x"].shape[0]
+    y = O.integrated_pe(t(g["x"]), t(g["dir"]), torch.full((n, 1), 1 / 1111.1), t(g["t0"]), t(g["t1"]), 10,
+                        2 * np.pi, False, True, 0.0)
+    np.testing.assert_allclose(y.numpy(), g["mipnerf_ipe_800"], atol=1e-6, rtol=0)
+
+
+@pytest.mark.parametrize("S", [64, 128, 192])
+def test_render_rays(golden, S):
+    g = golden("composite")
+    k = f"S{S}"
+    sig = t(g[f"{k}_sigma"]).clone().requires_grad_(True)
+    col = t(g[f"{k}_color"]).clone().requires_grad_(True)
+    rgb, w = O.render_rays(sig, col, t(g[f"{k}_dist"]), 3.0, 1 / 3)
+    np.testing.assert_allclose(rgb.detach().numpy(), g[f"{k}_rgb"], atol=1e-6, rtol=0)
+    np.testing.assert_allclose(w.detach().numpy(), g[f"{k}_w"], atol=1e-6, rtol=0)
+    ((rgb * t(g[f"{k}_grgb"])).sum() + (w * t(g[f"{k}_gw"])).sum()).backward()
+    np.testing.assert_allclose(sig.grad.numpy(), g[f"{k}_dsigma"], atol=1e-5, rtol=1e-5)
+    np.testing.assert_allclose(col.grad.numpy(), g[f"{k}_dcolor"], atol=1e-6, rtol=0)
+
+
+@pytest.mark.parametrize("N", [128, 256])
+def test_resample_barf(golden, N):
+    g = golden("resample")
+    k = f"barf_N{N}"
+    t0, t1, ok = O.sample_t_pdf_weighted(t(g[f"{k}_tc"]), t(g[f"{k}_w"]), t(g[f"{k}_dist"]), N, 8.0, mode=0)
+    assert ok
+    np.testing.assert_array_equal(t0.numpy(), g[f"{k}_t0"])
+    np.testing.assert_array_equal(t1.numpy(), g[f"{k}_t1"])
+
+
+def test_resample_n2v(golden):
+    g = golden("resample")
+    t0, t1, ok = O.sample_t_pdf_weighted(t(g["n2v_tc"]), t(g["n2v_w"]), t(g["n2v_dist"]), 256, 1 / 3, mode=1)
+    assert ok
+    np.testing.assert_array_equal(t0.numpy(), g["n2v_t0"])
+    np.testing.assert_array_equal(t1.numpy(), g["n2v_t1"])
+
+
+def test_cos_kat():
+    """barf/cos_test_barf.pt: the 10-level cos block of a 3-D PE, [x*2^0..x*2^9, y.., z..].
+    Inputs were not saved: recover x from column 0 and check the double-angle chain."""
+    import os
+    c = np.load(os.path.join(os.path.dirname(__file__), "golden", "cos_kat.npz"))["cos"].astype(np.float64)
+    assert c.shape == (1000, 30)
+    for d in range(3):
+        blk = c[:, d * 10:(d + 1) * 10]
+        np.testing.assert_allclose(blk[:, 1:], 2 * blk[:, :-1] ** 2 - 1, atol=5e-6)
