@@ -164,10 +164,12 @@ int nerf_encode_rays(const nerf_pe_params* params, const float* ray_d, int64_t n
 /* ---------------------------------------------------------------------------
  * Linear layers on fp32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 FMA chains).
  *
- * An operand is a column-concatenation of up to 4 row-major segments; segment
- * j contributes columns [koff_j, koff_j + k_j) with k_j % 32 == 0, ld % 4 == 0,
- * 16-byte aligned ptr; row m of the operand is row m / row_div_j of segment j
- * (row_div > 1 broadcasts a per-ray tensor over its samples).
+ * An operand is a column-concatenation of up to 4 row-major segments.  Segment
+ * j has k_j valid columns (k_j % 4 == 0, ld % 4 == 0, 16-byte aligned ptr) and
+ * occupies kp_j = roundup(k_j, 32) columns [koff_j, koff_j + kp_j) of the packed
+ * K dimension (columns past k_j read as zero); row m of the operand is row
+ * m / row_div_j of segment j (row_div > 1 broadcasts a per-ray tensor over its
+ * samples).  M < 2^31.
  * ------------------------------------------------------------------------- */
 typedef struct nerf_seg {
     const float* ptr;
@@ -182,8 +184,8 @@ typedef struct nerf_seg {
 #define NERF_EPI_ACCUM 8   /* out += result */
 
 /* out[m, n] = epi( sum_k A[m, k] * W[n, k] ),  m < M, n < N.
- * W: packed row-major [ceil(N/128)*128][ldw], ldw = sum_j k_j (zero padding
- * rows/cols).  out row stride ldo. */
+ * W: packed row-major [ceil(N/128)*128][ldw], ldw = sum_j kp_j (zero padding
+ * rows/cols).  out row stride ldo.  N <= 32 uses a 128 x 32 tile. */
 int nerf_linear_fwd(const nerf_seg* segs, int32_t n_segs, int64_t M,
                     const float* W, int32_t ldw, int32_t N, const float* bias,
                     float* out, int64_t ldo, int32_t epilogue,

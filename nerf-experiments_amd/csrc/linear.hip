@@ -6,49 +6,60 @@
 // gfx950), so results differ from CPU BLAS only by summation order.
 //
 // Forward / input-gradient ("NT"): out[M,N] = epi(A[M,K] . W[N,K]^T)
-//   tile 128 x 128, 256 threads = 4 waves in a 2x2 grid, each wave 64 x 64 =
-//   2 x 2 MFMA blocks of 32 x 32.  K streamed in 32-wide chunks through a
-//   double-buffered LDS tile (rows padded to 36 floats: the 16 distinct rows
-//   a ds_read_b128 lane group touches land on 16 distinct 16-byte bank slots).
-//   In a chunk, MFMA k-step s (0..15) pairs columns s and 16+s: lane half h
-//   reads columns h*16 + 4g .. +3 with one ds_read_b128 per operand block,
-//   which feeds four k-steps.  A is a concatenation of up to 4 segments
-//   (activations | positional encoding | per-ray direction encoding), so the
-//   reference's torch.cat copies are never materialised.
+//   256 threads = 4 waves.  BN = 128: 128 x 128 tile, waves 2 x 2, each 64 x 64
+//   (2 x 2 MFMA blocks of 32 x 32).  BN = 32 (narrow layers, N <= 32): 128 x 32
+//   tile, 4 waves stacked in M, each 32 x 32.
+//   K streams in 32-wide chunks through a double-buffered LDS tile (rows
+//   padded to 36 floats: the 16 distinct rows of a ds_read_b128 lane group hit
+//   16 distinct 16-byte bank slots).  In a chunk, MFMA k-step s (0..15) pairs
+//   columns s and 16 + s: lane half h reads columns h*16 + 4g .. +3 with one
+//   ds_read_b128 per operand block, which feeds four k-steps.
+//   A is a column-concatenation of up to 4 segments (activations | position
+//   encoding | per-ray direction encoding), so the reference's th.cat copies
+//   never exist; per-thread row pointers are recomputed only at segment
+//   boundaries (row_div broadcasts per-ray rows over their samples).
+//   The epilogue stages the accumulator tile through LDS so bias, ReLU, the
+//   ReLU-backward mask (aux) and accumulation run on coalesced 16-byte rows.
 //
 // Weight gradient ("TN"): slab[s][n][k] = sum_{m in slice s} dY[m,n] X[m,k]
 //   tile 128(n) x 128(k), split over M; 32-row M chunks staged in LDS; the
-//   MFMA reduction index is the sample index.  A second kernel sums the slices
-//   (fixed order, deterministic) and scatters into the nn.Linear grad layout.
+//   MFMA reduction index is the sample index.  A second kernel sums the
+//   slices in a fixed order (deterministic) and scatters into the nn.Linear
+//   gradient layout through a column map.
 #include "common.h"
 
 using namespace nerf;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+// native 4-wide vector (HIP's f4 is a struct: copies of it become memcpys that
+// defeat register promotion of the staging arrays)
+typedef float f4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 32, LDP = BK + 4;  // padded LDS row (floats)
+constexpr int BK = 32, LDP = BK + 4;  // chunk width and padded LDS row (floats)
 constexpr int MAX_SEGS = 4;
 
 struct SegList {
     const float* ptr[MAX_SEGS];
     int64_t ld[MAX_SEGS];
-    int k[MAX_SEGS];
+    int k[MAX_SEGS];        // valid columns (multiple of 4)
+    int kp[MAX_SEGS];       // padded width in the packed weight layout (multiple of 32)
     int row_div[MAX_SEGS];
-    int koff[MAX_SEGS];
+    int koff[MAX_SEGS];     // first packed column of the segment
     int n;
-    int ktot;
+    int ktot;               // sum of kp
 };
 
 struct NTArgs {
     SegList A;
-    int64_t M;
+    int M;
     const float* W; int ldw; int N;
     const float* bias;
     float* out; int64_t ldo;
     int epi;
     const float* aux; int64_t ldaux;
+    int vec_ok;             // out/aux/bias 16-byte aligned with ld % 4 == 0
 };
 
 // Runtime segment selection without dynamic indexing of the by-value kernel
@@ -66,158 +77,229 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
-// Loads one 128 x 32 A chunk (segment `sg`, column offset kc) and the matching
-// 128 x 32 W chunk into registers (4 float4 each per thread).
-__device__ __forceinline__ void load_chunk(const NTArgs& a, int sg, int kc, int64_t m0, int n0, float4 ra[4],
-                                           float4 rb[4]) {
-    const int t = threadIdx.x;
-    const int c4 = t & 7;
-    const float* sp = pick4(a.A.ptr, sg);
-    const int64_t ld = pick4(a.A.ld, sg);
-    const int rd = pick4(a.A.row_div, sg);
-    const int koff = pick4(a.A.koff, sg);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = i * 32 + (t >> 3);
-        const int64_t m = m0 + r;
-        const bool ok = m < a.M;
-        const int64_t mc = ok ? m : a.M - 1;  // clamp: branch-free load, zeroed below
-        const int64_t src = (rd == 1 ? mc : mc / rd);
-        float4 v = *reinterpret_cast<const float4*>(sp + src * ld + kc + c4 * 4);
-        ra[i] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-        const int n = n0 + r;
-        rb[i] = *reinterpret_cast<const float4*>(a.W + (int64_t)n * a.ldw + koff + kc + c4 * 4);
-    }
-}
+template <int BN>
+struct TileCfg;
+template <>
+struct TileCfg<128> {
+    static constexpr int WAVES_N = 2, WM = 64, WN = 64, BM = 128;
+};
+template <>
+struct TileCfg<32> {
+    static constexpr int WAVES_N = 1, WM = 32, WN = 32, BM = 128;
+};
 
-__device__ __forceinline__ void store_chunk(float* As, float* Bs, const float4 ra[4], const float4 rb[4]) {
-    const int t = threadIdx.x;
-    const int c4 = t & 7;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = i * 32 + (t >> 3);
-        *reinterpret_cast<float4*>(As + r * LDP + c4 * 4) = ra[i];
-        *reinterpret_cast<float4*>(Bs + r * LDP + c4 * 4) = rb[i];
-    }
-}
-
+template <int BN>
 __global__ __launch_bounds__(256, 2) void linear_nt_kernel(NTArgs a) {
-    __shared__ __attribute__((aligned(16))) float smem[2 * 2 * BM * LDP];
-    // buffer b: A tile at smem + b*2*BM*LDP, W tile right after it
+    using Cfg = TileCfg<BN>;
+    constexpr int BM = Cfg::BM, WM = Cfg::WM, WN = Cfg::WN;
+    constexpr int MB = WM / 32, NB = WN / 32;   // MFMA blocks per wave
+    constexpr int NA = BM / 32, NW = BN / 32;   // f4 staging loads per thread per chunk
+    constexpr int LDC = BN + 4;
+    constexpr int LDS_AB = 2 * (BM + BN) * LDP;
+    constexpr int LDS_C = BM * LDC;
+    constexpr int LDS_FLOATS = LDS_AB > LDS_C ? LDS_AB : LDS_C;
+    constexpr int BUF = (BM + BN) * LDP;
+    __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
 
     const int ntn = (a.N + BN - 1) / BN;
     const int bid = blockIdx.x;
     const int tn = bid % ntn;
-    const int64_t tm = bid / ntn;
-    const int64_t m0 = tm * BM;
+    const int m0 = (bid / ntn) * BM;
     const int n0 = tn * BN;
 
     const int t = threadIdx.x;
     const int wave = t >> 6, lane = t & 63;
-    const int wr = wave >> 1, wc = wave & 1;
+    const int wr = wave / Cfg::WAVES_N, wc = wave % Cfg::WAVES_N;
     const int li = lane & 31, lh = lane >> 5;
+    const int c4 = t & 7, rbase = t >> 3;
 
-    f32x16 acc[2][2];
+    f32x16 acc[MB][NB];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MB; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NB; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    // chunk iteration over (segment, kc)
-    int sg = 0, kc = 0;
-    float4 ra[4], rb[4];
-    load_chunk(a, sg, kc, m0, n0, ra, rb);
-    store_chunk(smem, smem + BM * LDP, ra, rb);
+    // ---- segment state: scalar parameters + per-thread row offsets
+    int seg = 0;
+    const float* sp = nullptr;
+    int sk = 0, skp = 0, skoff = 0;
+    int64_t aoff[NA];
+    unsigned aok = 0;
+    auto set_seg = [&](int s) __attribute__((always_inline)) {
+        sp = pick4(a.A.ptr, s);
+        const int64_t ld = pick4(a.A.ld, s);
+        const unsigned rd = (unsigned)pick4(a.A.row_div, s);
+        sk = pick4(a.A.k, s);
+        skp = pick4(a.A.kp, s);
+        skoff = pick4(a.A.koff, s);
+        aok = 0;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const int m = m0 + i * 32 + rbase;
+            const bool ok = m < a.M;
+            const unsigned mc = (unsigned)(ok ? m : a.M - 1);
+            const unsigned src = (rd == 1u) ? mc : mc / rd;
+            aoff[i] = (int64_t)src * ld + c4 * 4;
+            aok |= (ok ? 1u : 0u) << i;
+        }
+    };
+    int64_t woff[NW];
+#pragma unroll
+    for (int j = 0; j < NW; ++j) woff[j] = (int64_t)(n0 + j * 32 + rbase) * a.ldw + c4 * 4;
+
+    f4 ra[NA], rw[NW];
+    auto load_chunk = [&](int kc) __attribute__((always_inline)) {
+        const int col = kc + c4 * 4;
+        const bool cok = col < sk;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const f4 v = *reinterpret_cast<const f4*>(sp + aoff[i] + (cok ? kc : 0));
+            ra[i] = (cok && ((aok >> i) & 1u)) ? v : f4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int j = 0; j < NW; ++j) rw[j] = *reinterpret_cast<const f4*>(a.W + woff[j] + skoff + kc);
+    };
+    auto store_chunk = [&](int buf) __attribute__((always_inline)) {
+        float* As = smem + buf * BUF;
+        float* Ws = As + BM * LDP;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) *reinterpret_cast<f4*>(As + (i * 32 + rbase) * LDP + c4 * 4) = ra[i];
+#pragma unroll
+        for (int j = 0; j < NW; ++j) *reinterpret_cast<f4*>(Ws + (j * 32 + rbase) * LDP + c4 * 4) = rw[j];
+    };
+
+    set_seg(0);
+    int kc = 0;
+    load_chunk(0);
+    store_chunk(0);
     __syncthreads();
     const int nchunks = a.A.ktot / BK;
     int cur = 0;
     for (int c = 0; c < nchunks; ++c) {
-        // advance to next chunk coordinates
-        int nsg = sg, nkc = kc + BK;
-        if (nkc >= pick4(a.A.k, nsg)) { nsg++; nkc = 0; }
-        const bool has_next = (c + 1 < nchunks);
-        // the last iteration re-stages chunk 0 into the idle buffer (never read):
-        // keeps the staging registers branch-free
-        load_chunk(a, has_next ? nsg : 0, has_next ? nkc : 0, m0, n0, ra, rb);
+        // stage chunk c+1 (the last iteration re-stages the current chunk into the
+        // idle buffer, which is never read: keeps the staging registers branch-free)
+        const bool has_next = c + 1 < nchunks;
+        if (has_next) {
+            kc += BK;
+            if (kc >= skp) {
+                ++seg;
+                set_seg(seg);
+                kc = 0;
+            }
+        }
+        load_chunk(kc);
 
-        const float* Ab = smem + cur * 2 * BM * LDP + (wr * 64 + li) * LDP + lh * 16;
-        const float* Bb = smem + cur * 2 * BM * LDP + BM * LDP + (wc * 64 + li) * LDP + lh * 16;
+        const float* Ab = smem + cur * BUF + (wr * WM + li) * LDP + lh * 16;
+        const float* Bb = smem + cur * BUF + BM * LDP + (wc * WN + li) * LDP + lh * 16;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-            float4 av[2], bv[2];
-            av[0] = *reinterpret_cast<const float4*>(Ab + g * 4);
-            av[1] = *reinterpret_cast<const float4*>(Ab + 32 * LDP + g * 4);
-            bv[0] = *reinterpret_cast<const float4*>(Bb + g * 4);
-            bv[1] = *reinterpret_cast<const float4*>(Bb + 32 * LDP + g * 4);
+            f4 av[MB], bv[NB];
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < MB; ++i) av[i] = *reinterpret_cast<const f4*>(Ab + i * 32 * LDP + g * 4);
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
+            for (int j = 0; j < NB; ++j) bv[j] = *reinterpret_cast<const f4*>(Bb + j * 32 * LDP + g * 4);
+#pragma unroll
+            for (int i = 0; i < MB; ++i)
+#pragma unroll
+                for (int j = 0; j < NB; ++j) {
                     acc[i][j] = mfma32(av[i].x, bv[j].x, acc[i][j]);
                     acc[i][j] = mfma32(av[i].y, bv[j].y, acc[i][j]);
                     acc[i][j] = mfma32(av[i].z, bv[j].z, acc[i][j]);
                     acc[i][j] = mfma32(av[i].w, bv[j].w, acc[i][j]);
                 }
         }
-        store_chunk(smem + (cur ^ 1) * 2 * BM * LDP, smem + (cur ^ 1) * 2 * BM * LDP + BM * LDP, ra, rb);
+        store_chunk(cur ^ 1);
         __syncthreads();
         cur ^= 1;
-        sg = nsg; kc = nkc;
     }
 
-    // epilogue: C/D map of 32x32 MFMA: col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+    // ---- epilogue: accumulators -> LDS tile -> coalesced 16-byte rows
+    // C/D map of the 32x32 MFMA: col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+    float* Cs = smem;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int n = n0 + wc * 64 + j * 32 + li;
-        if (n >= a.N) continue;
-        const float bv = (a.epi & NERF_EPI_BIAS) ? a.bias[n] : 0.f;
+    for (int i = 0; i < MB; ++i)
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int j = 0; j < NB; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int64_t m = m0 + wr * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                if (m >= a.M) continue;
-                float v = acc[i][j][r];
-                if (a.epi & NERF_EPI_BIAS) v = v + bv;
-                if (a.epi & NERF_EPI_RELU) v = fmaxf(v, 0.f);
-                if (a.epi & NERF_EPI_MASK) v = (a.aux[m * a.ldaux + n] > 0.f) ? v : 0.f;
-                float* o = a.out + m * a.ldo + n;
-                if (a.epi & NERF_EPI_ACCUM) v = *o + v;
-                *o = v;
+                const int row = wr * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                Cs[row * LDC + wc * WN + j * 32 + li] = acc[i][j][r];
+            }
+    __syncthreads();
+    constexpr int Q = BN / 4;               // f4 per tile row
+    constexpr int ITER = BM * Q / 256;
+#pragma unroll 4
+    for (int it = 0; it < ITER; ++it) {
+        const int q = it * 256 + t;
+        const int row = q / Q, cq = q - (q / Q) * Q;
+        const int m = m0 + row;
+        const int n = n0 + cq * 4;
+        if (m >= a.M || n >= a.N) continue;
+        f4 v = *reinterpret_cast<const f4*>(Cs + row * LDC + cq * 4);
+        float* o = a.out + (int64_t)m * a.ldo + n;
+        if (a.vec_ok && n + 4 <= a.N) {
+            if (a.epi & NERF_EPI_BIAS) {
+                const f4 b = *reinterpret_cast<const f4*>(a.bias + n);
+                v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+            }
+            if (a.epi & NERF_EPI_RELU) {
+                v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+            }
+            if (a.epi & NERF_EPI_MASK) {
+                const f4 x = *reinterpret_cast<const f4*>(a.aux + (int64_t)m * a.ldaux + n);
+                v.x = x.x > 0.f ? v.x : 0.f; v.y = x.y > 0.f ? v.y : 0.f;
+                v.z = x.z > 0.f ? v.z : 0.f; v.w = x.w > 0.f ? v.w : 0.f;
+            }
+            if (a.epi & NERF_EPI_ACCUM) {
+                const f4 p = *reinterpret_cast<const f4*>(o);
+                v.x = p.x + v.x; v.y = p.y + v.y; v.z = p.z + v.z; v.w = p.w + v.w;
+            }
+            *reinterpret_cast<f4*>(o) = v;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (n + e >= a.N) break;
+                float x = e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
+                if (a.epi & NERF_EPI_BIAS) x = x + a.bias[n + e];
+                if (a.epi & NERF_EPI_RELU) x = fmaxf(x, 0.f);
+                if (a.epi & NERF_EPI_MASK) x = (a.aux[(int64_t)m * a.ldaux + n + e] > 0.f) ? x : 0.f;
+                if (a.epi & NERF_EPI_ACCUM) x = o[e] + x;
+                o[e] = x;
             }
         }
     }
 }
 
 // ------------------------------- weight gradient ---------------------------
+constexpr int TB = 128;  // n and k tile of the weight-gradient kernel
 constexpr int TBM = 32;  // samples per LDS stage
 
 struct TNArgs {
     const float* dY; int64_t lddy; int N;
     SegList X;
-    int64_t M;
-    int64_t m_per_split;
+    int M;
+    int m_per_split;
     int splits;
     float* slab;      // [splits][ntn*128][ntk*128]
     float* db_slab;   // [splits][ntn*128]
 };
 
 __global__ __launch_bounds__(256, 2) void linear_wgrad_kernel(TNArgs a) {
-    __shared__ __attribute__((aligned(16))) float sY[2][TBM][BN];
-    __shared__ __attribute__((aligned(16))) float sX[2][TBM][BN];
+    __shared__ __attribute__((aligned(16))) float sY[2][TBM][TB];
+    __shared__ __attribute__((aligned(16))) float sX[2][TBM][TB];
 
-    const int ntn = (a.N + BN - 1) / BN;
-    const int ntk = (a.X.ktot + BN - 1) / BN;
+    const int ntn = (a.N + TB - 1) / TB;
+    const int ntk = (a.X.ktot + TB - 1) / TB;
     const int tiles = ntn * ntk;
     const int bid = blockIdx.x;
     const int split = bid / tiles;
     const int tile = bid - split * tiles;
     const int tn = tile / ntk, tk = tile - (tile / ntk) * ntk;
-    const int n0 = tn * BN, k0 = tk * BN;
-    const int64_t mbeg = (int64_t)split * a.m_per_split;
-    int64_t mend = mbeg + a.m_per_split;
+    const int n0 = tn * TB, k0 = tk * TB;
+    const int mbeg = split * a.m_per_split;
+    int mend = mbeg + a.m_per_split;
     if (mend > a.M) mend = a.M;
 
     const int t = threadIdx.x;
@@ -225,19 +307,20 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_kernel(TNArgs a) {
     const int wr = wave >> 1, wc = wave & 1;   // wr: n half, wc: k half
     const int li = lane & 31, lh = lane >> 5;
 
-    // this thread's fixed load column (float4 granule) for both tiles
+    // this thread's fixed load column (f4 granule) for both tiles
     const int c4 = t & 31;
-    const int rr = t >> 5;  // 0..7, rows rr, rr+8, rr+16, rr+24
+    const int rr = t >> 5;  // 0..7: rows rr, rr+8, rr+16, rr+24 of each stage
     const int ny = n0 + c4 * 4;
     const bool ny_ok = ny < a.N;
     const int kx = k0 + c4 * 4;
     int xs = -1, xoff = 0;
 #pragma unroll
     for (int s = 0; s < MAX_SEGS; ++s)
-        if (s < a.X.n && kx >= a.X.koff[s] && kx < a.X.koff[s] + a.X.k[s]) { xs = s; xoff = kx - a.X.koff[s]; }
-    const float* xptr = xs >= 0 ? pick4(a.X.ptr, xs) : nullptr;
-    const int64_t xld = xs >= 0 ? pick4(a.X.ld, xs) : 0;
-    const int xrd = xs >= 0 ? pick4(a.X.row_div, xs) : 1;
+        if (s < a.X.n && kx >= a.X.koff[s] && kx < a.X.koff[s] + a.X.kp[s]) { xs = s; xoff = kx - a.X.koff[s]; }
+    const bool x_ok = xs >= 0 && xoff < (xs >= 0 ? pick4(a.X.k, xs) : 0);
+    const float* xptr = x_ok ? pick4(a.X.ptr, xs) : a.dY;
+    const int64_t xld = x_ok ? pick4(a.X.ld, xs) : 0;
+    const unsigned xrd = x_ok ? (unsigned)pick4(a.X.row_div, xs) : 1u;
 
     f32x16 acc[2][2];
 #pragma unroll
@@ -248,23 +331,25 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_kernel(TNArgs a) {
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     float dbacc = 0.f;
 
-    float4 ry[4], rx[4];
-    auto gload = [&](int64_t mc) {
+    f4 ry[4], rx[4];
+    auto gload = [&](int mc) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int64_t m = mc + rr + 8 * i;
+            const int m = mc + rr + 8 * i;
             const bool mok = m < mend;
-            ry[i] = (mok && ny_ok) ? *reinterpret_cast<const float4*>(a.dY + m * a.lddy + ny)
-                                   : make_float4(0.f, 0.f, 0.f, 0.f);
-            rx[i] = (mok && xptr) ? *reinterpret_cast<const float4*>(xptr + (xrd == 1 ? m : m / xrd) * xld + xoff)
-                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+            const unsigned mm = (unsigned)(mok ? m : mbeg);
+            const f4 vy = *reinterpret_cast<const f4*>(a.dY + (int64_t)mm * a.lddy + (ny_ok ? ny : 0));
+            const f4 vx =
+                *reinterpret_cast<const f4*>(xptr + (int64_t)(xrd == 1u ? mm : mm / xrd) * xld + (x_ok ? xoff : 0));
+            ry[i] = (mok && ny_ok) ? vy : f4{0.f, 0.f, 0.f, 0.f};
+            rx[i] = (mok && x_ok) ? vx : f4{0.f, 0.f, 0.f, 0.f};
         }
     };
-    auto sstore = [&](int buf) {
+    auto sstore = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            *reinterpret_cast<float4*>(&sY[buf][rr + 8 * i][c4 * 4]) = ry[i];
-            *reinterpret_cast<float4*>(&sX[buf][rr + 8 * i][c4 * 4]) = rx[i];
+            *reinterpret_cast<f4*>(&sY[buf][rr + 8 * i][c4 * 4]) = ry[i];
+            *reinterpret_cast<f4*>(&sX[buf][rr + 8 * i][c4 * 4]) = rx[i];
         }
     };
 
@@ -273,9 +358,9 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_kernel(TNArgs a) {
         sstore(0);
         __syncthreads();
         int cur = 0;
-        for (int64_t mc = mbeg; mc < mend; mc += TBM) {
+        for (int mc = mbeg; mc < mend; mc += TBM) {
             const bool has_next = mc + TBM < mend;
-            if (has_next) gload(mc + TBM);
+            gload(has_next ? mc + TBM : mc);
 #pragma unroll
             for (int s = 0; s < 16; ++s) {
                 const int mr = lh * 16 + s;
@@ -289,17 +374,17 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_kernel(TNArgs a) {
 #pragma unroll
                     for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
             }
-            if (tk == 0 && t < BN) {
+            if (tk == 0 && t < TB) {
 #pragma unroll
                 for (int r = 0; r < TBM; ++r) dbacc += sY[cur][r][t];
             }
-            if (has_next) sstore(cur ^ 1);
+            sstore(cur ^ 1);
             __syncthreads();
             cur ^= 1;
         }
     }
 
-    const int npad = ntn * BN, kpad = ntk * BN;
+    const int npad = ntn * TB, kpad = ntk * TB;
     float* slab = a.slab + (size_t)split * npad * kpad;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -311,39 +396,65 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_kernel(TNArgs a) {
                 const int k = k0 + wc * 64 + j * 32 + li;
                 slab[(size_t)n * kpad + k] = acc[i][j][r];
             }
-    if (tk == 0 && t < BN) a.db_slab[(size_t)split * npad + n0 + t] = dbacc;
+    if (tk == 0 && t < TB) a.db_slab[(size_t)split * npad + n0 + t] = dbacc;
 }
 
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(int splits, int N, int K, int npad, int kpad,
+// Sum the split slabs.  Block = 64 consecutive outputs x 4 split groups; each
+// thread sums splits g, g+4, ... (independent loads in flight), then the 4
+// partial sums are added in a fixed order through LDS: deterministic.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(int splits, int n_valid, int K, int npad, int kpad,
                                                            const float* __restrict__ slab,
                                                            const float* __restrict__ db_slab,
                                                            const int32_t* __restrict__ col_map,
                                                            float* __restrict__ dW, int64_t ld_dw,
                                                            float* __restrict__ db) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t total = (int64_t)N * K;
-    if (idx < total) {
-        const int n = (int)(idx / K), k = (int)(idx - (idx / K) * K);
-        const int dst = col_map ? col_map[k] : k;
-        if (dst >= 0) {
-            double s = 0.0;
-            for (int sp = 0; sp < splits; ++sp) s += (double)slab[((size_t)sp * npad + n) * kpad + k];
-            dW[(int64_t)n * ld_dw + dst] = (float)s;
+    __shared__ double part[4][64];
+    const int t = threadIdx.x;
+    const int o = t & 63, g = t >> 6;
+    const int64_t total = (int64_t)n_valid * K;
+    const int64_t nblk_w = (total + 63) / 64;
+    const bool is_db = (int64_t)blockIdx.x >= nblk_w;
+    const int64_t idx = is_db ? ((int64_t)blockIdx.x - nblk_w) * 64 + o : (int64_t)blockIdx.x * 64 + o;
+    const int64_t lim = is_db ? n_valid : total;
+    double s0 = 0.0, s1 = 0.0;
+    if (idx < lim) {
+        size_t off, stride;
+        if (is_db) {
+            off = (size_t)idx;
+            stride = (size_t)npad;
+        } else {
+            const int n = (int)(idx / K), k = (int)(idx - (idx / K) * K);
+            off = (size_t)n * kpad + k;
+            stride = (size_t)npad * kpad;
         }
+        const float* base = is_db ? db_slab : slab;
+        int sp = g;
+        for (; sp + 4 < splits; sp += 8) {
+            s0 += (double)base[(size_t)sp * stride + off];
+            s1 += (double)base[(size_t)(sp + 4) * stride + off];
+        }
+        if (sp < splits) s0 += (double)base[(size_t)sp * stride + off];
     }
-    if (db && idx < N) {
-        double s = 0.0;
-        for (int sp = 0; sp < splits; ++sp) s += (double)db_slab[(size_t)sp * npad + idx];
-        db[idx] = (float)s;
+    part[g][o] = s0 + s1;
+    __syncthreads();
+    if (g == 0 && idx < lim) {
+        const double s = ((part[0][o] + part[1][o]) + part[2][o]) + part[3][o];
+        if (is_db) {
+            db[idx] = (float)s;
+        } else {
+            const int n = (int)(idx / K), k = (int)(idx - (idx / K) * K);
+            const int dst = col_map ? col_map[k] : k;
+            if (dst >= 0) dW[(int64_t)n * ld_dw + dst] = (float)s;
+        }
     }
 }
 
 int choose_splits(int64_t M, int tiles) {
-    int64_t target = 1024 / (tiles > 0 ? tiles : 1);
+    int64_t target = 512 / (tiles > 0 ? tiles : 1);
+    if (target > 128) target = 128;
     if (target < 1) target = 1;
     const int64_t max_splits = (M + TBM - 1) / TBM;
     if (target > max_splits) target = max_splits;
-    if (target > 4096) target = 4096;
     return (int)target;
 }
 
@@ -352,12 +463,15 @@ bool build_segs(const nerf_seg* segs, int n, SegList& L) {
     int koff = 0;
     for (int i = 0; i < n; ++i) {
         const nerf_seg& s = segs[i];
-        if (!s.ptr || s.k <= 0 || (s.k % BK) != 0 || s.ld < s.k || (s.ld % 4) != 0 || s.row_div < 1) return false;
+        if (!s.ptr || s.k <= 0 || (s.k % 4) != 0 || s.ld < s.k || (s.ld % 4) != 0 || s.row_div < 1) return false;
         if (!aligned16(s.ptr)) return false;
-        L.ptr[i] = s.ptr; L.ld[i] = s.ld; L.k[i] = s.k; L.row_div[i] = s.row_div; L.koff[i] = koff;
-        koff += s.k;
+        const int kp = (s.k + BK - 1) / BK * BK;
+        L.ptr[i] = s.ptr; L.ld[i] = s.ld; L.k[i] = s.k; L.kp[i] = kp; L.row_div[i] = s.row_div; L.koff[i] = koff;
+        koff += kp;
     }
-    for (int i = n; i < MAX_SEGS; ++i) { L.ptr[i] = nullptr; L.ld[i] = 0; L.k[i] = 0; L.row_div[i] = 1; L.koff[i] = koff; }
+    for (int i = n; i < MAX_SEGS; ++i) {
+        L.ptr[i] = nullptr; L.ld[i] = 0; L.k[i] = 0; L.kp[i] = 0; L.row_div[i] = 1; L.koff[i] = koff;
+    }
     L.n = n;
     L.ktot = koff;
     return true;
@@ -387,43 +501,49 @@ __global__ void pack_weight_kernel(const float* __restrict__ W, int N, int K_ori
 extern "C" int nerf_linear_fwd(const nerf_seg* segs, int32_t n_segs, int64_t M, const float* W, int32_t ldw, int32_t N,
                                const float* bias, float* out, int64_t ldo, int32_t epilogue, const float* aux,
                                int64_t ld_aux, void* stream) {
-    NERF_REQUIRE(M >= 0 && N >= 1);
+    NERF_REQUIRE(M >= 0 && M < (1ll << 31) && N >= 1);
     if (M == 0) return NERF_OK;
     SegList L;
     NERF_REQUIRE(build_segs(segs, n_segs, L));
-    NERF_REQUIRE(W && out && aligned16(W) && ldw == L.ktot && ldo >= N);
+    NERF_REQUIRE(W && out && aligned16(W) && ldw == L.ktot && (ldw % 4) == 0 && ldo >= N);
     if (epilogue & NERF_EPI_BIAS) NERF_REQUIRE(bias != nullptr);
     if (epilogue & NERF_EPI_MASK) NERF_REQUIRE(aux != nullptr && ld_aux >= N);
-    NTArgs a{L, M, W, ldw, N, bias, out, ldo, epilogue, aux, ld_aux};
-    const int64_t ntm = (M + BM - 1) / BM;
-    const int64_t ntn = (N + BN - 1) / BN;
-    const int64_t blocks = ntm * ntn;
-    NERF_REQUIRE(blocks < (1ll << 31));
-    hipLaunchKernelGGL(linear_nt_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
+    const int vec_ok = aligned16(out) && (ldo % 4) == 0 && (!(epilogue & NERF_EPI_BIAS) || aligned16(bias)) &&
+                       (!(epilogue & NERF_EPI_MASK) || (aligned16(aux) && (ld_aux % 4) == 0));
+    NTArgs a{L, (int)M, W, ldw, N, bias, out, ldo, epilogue, aux, ld_aux, vec_ok};
+    const int64_t ntm = (M + 127) / 128;
+    hipStream_t st = as_stream(stream);
+    if (N <= 32) {
+        hipLaunchKernelGGL(linear_nt_kernel<32>, dim3((unsigned)ntm), dim3(256), 0, st, a);
+    } else {
+        const int64_t ntn = (N + 127) / 128;
+        hipLaunchKernelGGL(linear_nt_kernel<128>, dim3((unsigned)(ntm * ntn)), dim3(256), 0, st, a);
+    }
     NERF_CHECK_LAUNCH();
     return NERF_OK;
 }
 
 extern "C" size_t nerf_linear_wgrad_workspace(int64_t M, int32_t N, int32_t K) {
-    const int ntn = (N + BN - 1) / BN, ntk = (K + BN - 1) / BN;
+    const int ntn = (N + TB - 1) / TB, ntk = (K + TB - 1) / TB;
     const int splits = choose_splits(M, ntn * ntk);
-    return (size_t)splits * ntn * BN * (size_t)ntk * BN * sizeof(float) + (size_t)splits * ntn * BN * sizeof(float);
+    return (size_t)splits * ntn * TB * (size_t)ntk * TB * sizeof(float) + (size_t)splits * ntn * TB * sizeof(float);
 }
 
 extern "C" int nerf_linear_wgrad(const float* dY, int64_t ld_dy, int32_t N, const nerf_seg* segs, int32_t n_segs,
                                  int64_t M, void* workspace, size_t workspace_bytes, void* stream) {
-    NERF_REQUIRE(dY && N >= 1 && M >= 0 && aligned16(dY) && (ld_dy % 4) == 0 && (N % 4) == 0 && ld_dy >= N);
+    NERF_REQUIRE(dY && N >= 1 && M >= 0 && M < (1ll << 31) && aligned16(dY) && (ld_dy % 4) == 0 && (N % 4) == 0 &&
+                 ld_dy >= N);
     SegList L;
     NERF_REQUIRE(build_segs(segs, n_segs, L));
-    const int ntn = (N + BN - 1) / BN, ntk = (L.ktot + BN - 1) / BN;
+    const int ntn = (N + TB - 1) / TB, ntk = (L.ktot + TB - 1) / TB;
     const int splits = choose_splits(M, ntn * ntk);
     const size_t need = nerf_linear_wgrad_workspace(M, N, L.ktot);
-    if (!workspace || workspace_bytes < need) return NERF_ERR_WORKSPACE;
+    if (!workspace || workspace_bytes < need || !aligned16(workspace)) return NERF_ERR_WORKSPACE;
     float* slab = reinterpret_cast<float*>(workspace);
-    float* db_slab = slab + (size_t)splits * ntn * BN * (size_t)ntk * BN;
+    float* db_slab = slab + (size_t)splits * ntn * TB * (size_t)ntk * TB;
     int64_t mps = (M + splits - 1) / splits;
     mps = ((mps + TBM - 1) / TBM) * TBM;
-    TNArgs a{dY, ld_dy, N, L, M, mps, splits, slab, db_slab};
+    TNArgs a{dY, ld_dy, N, L, (int)M, (int)mps, splits, slab, db_slab};
     const int64_t blocks = (int64_t)splits * ntn * ntk;
     hipLaunchKernelGGL(linear_wgrad_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
     NERF_CHECK_LAUNCH();
@@ -433,14 +553,14 @@ extern "C" int nerf_linear_wgrad(const float* dY, int64_t ld_dy, int32_t N, cons
 extern "C" int nerf_linear_wgrad_reduce(int64_t M, int32_t N, int32_t K, int32_t n_valid, const void* workspace,
                                         const int32_t* col_map, float* dW, int64_t ld_dw, float* db, void* stream) {
     NERF_REQUIRE(workspace && dW && N >= 1 && K >= 1 && n_valid >= 1 && n_valid <= N);
-    const int ntn = (N + BN - 1) / BN, ntk = (K + BN - 1) / BN;
+    const int ntn = (N + TB - 1) / TB, ntk = (K + TB - 1) / TB;
     const int splits = choose_splits(M, ntn * ntk);
     const float* slab = reinterpret_cast<const float*>(workspace);
-    const float* db_slab = slab + (size_t)splits * ntn * BN * (size_t)ntk * BN;
+    const float* db_slab = slab + (size_t)splits * ntn * TB * (size_t)ntk * TB;
     const int64_t total = (int64_t)n_valid * K;
-    const int64_t blocks = (total + 255) / 256;
+    const int64_t blocks = (total + 63) / 64 + (db ? (n_valid + 63) / 64 : 0);
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), splits, n_valid, K,
-                       ntn * BN, ntk * BN, slab, db_slab, col_map, dW, ld_dw, db);
+                       ntn * TB, ntk * TB, slab, db_slab, col_map, dW, ld_dw, db);
     NERF_CHECK_LAUNCH();
     return NERF_OK;
 }
@@ -448,9 +568,9 @@ extern "C" int nerf_linear_wgrad_reduce(int64_t M, int32_t N, int32_t K, int32_t
 extern "C" int nerf_pack_weight(const float* W, int32_t N, int32_t K_orig, const int32_t* col_map, int32_t Kp,
                                 float* Wp, float* Wt, int32_t ldwt, void* stream) {
     NERF_REQUIRE(W && col_map && N >= 1 && K_orig >= 1 && Kp >= 1 && (Kp % BK) == 0);
-    const int npad = ((N + BN - 1) / BN) * BN;
+    const int npad = ((N + 127) / 128) * 128;
     if (Wt) NERF_REQUIRE(ldwt >= ((N + 31) / 32) * 32);
-    const int kpad_rows = ((Kp + BN - 1) / BN) * BN + BN;
+    const int kpad_rows = ((Kp + 127) / 128) * 128 + 128;
     int64_t total = (int64_t)npad * Kp;
     const int64_t pad_total = (int64_t)(kpad_rows - Kp) * (Wt ? ldwt : 0);
     if (pad_total > total) total = pad_total;

@@ -194,7 +194,9 @@ def encode_bwd(params: NerfPEParams, x: torch.Tensor, grad_out: torch.Tensor, dx
 
 # ----------------------------------------------------------------------------- linear layers
 def make_segs(segs: Sequence[tuple[torch.Tensor, int, int]]):
-    """segs: (tensor, k, row_div); the tensor's row stride is its ld."""
+    """segs: (tensor, k, row_div) with k % 4 == 0 valid columns; the tensor's row
+    stride is its ld.  In the packed weight layout each segment occupies
+    pad32(k) columns."""
     arr = (NerfSeg * len(segs))()
     for i, (t, k, rd) in enumerate(segs):
         if t.stride(1) != 1:

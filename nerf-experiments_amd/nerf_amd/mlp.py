@@ -51,7 +51,9 @@ class LayerPlan:
 
     def finalize(self, device):
         self.N = self.module.out_features
-        self.out_ld = K.pad32(self.N)
+        # outputs are stored with 16-byte rows (N rounded up to 4); the kernels zero-fill
+        # the remaining columns of a 32-wide K chunk when such a buffer is an operand
+        self.out_ld = (self.N + 3) // 4 * 4
         self.ldwt = K.pad32(self.N)
         cm = []
         orig = 0
@@ -187,7 +189,7 @@ class MLPFunction(torch.autograd.Function):
             param_grads[2 * li] = gW
             param_grads[2 * li + 1] = gb
             # ---- input gradients
-            a_seg = [(dZ, lp.ldwt, 1)]
+            a_seg = [(dZ, lp.out_ld, 1)]
             for s, koff in zip(lp.sources, lp.koffs):
                 if s.kind == "act":
                     j = s.layer

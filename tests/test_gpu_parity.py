@@ -351,13 +351,13 @@ def test_training_steps_reduce_loss():
     o = (torch.nn.functional.normalize(torch.randn(B, 3), dim=1) * 0.168).to(DEV)
     d = torch.nn.functional.normalize(-o.cpu() + torch.randn(B, 3) * 0.1, dim=1).to(DEV)
     pw = torch.full((B,), 1 / 555.56, device=DEV)
-    target = torch.rand(B, 3, device=DEV)
+    target = torch.full((B, 3), 0.3, device=DEV)   # learnable: a constant colour
     losses = []
     for _ in range(30):
         opt.zero_grad()
         loss, _ = ren.training_loss(o, d, pw, target)
         loss.backward()
         opt.step()
-        losses.append(float(loss))
+        losses.append(float(loss.detach()))
     assert all(math.isfinite(x) for x in losses)
-    assert losses[-1] < 0.8 * losses[0]
+    assert losses[-1] < 0.3 * losses[0]
