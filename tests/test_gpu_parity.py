@@ -225,33 +225,50 @@ def test_sample_uniform():
 # ----------------------------------------------------------------------------- linear layers
 @pytest.mark.parametrize("M,N,ks,rd", [(1000, 256, (256, 64), (1, 1)), (777, 257, (256,), (1,)),
                                        (4096, 128, (256, 32), (1, 64)), (300, 4, (128,), (1,)),
-                                       (129, 300, (32, 32, 64), (1, 3, 1))])
+                                       (129, 300, (32, 32, 64), (1, 3, 1)), (1000, 128, (4,), (1,)),
+                                       (333, 20, (260, 12), (1, 7))])
 def test_linear_fwd_wgrad(M, N, ks, rd):
+    """Packed layout: segment j occupies pad32(k_j) weight columns; columns past k_j are zero."""
     from nerf_amd import kernels as K
-    from nerf_amd._lib import NERF_EPI_BIAS, NERF_EPI_RELU
+    from nerf_amd._lib import NERF_EPI_ACCUM, NERF_EPI_BIAS, NERF_EPI_MASK, NERF_EPI_RELU
     torch.manual_seed(M + N)
     segs_cpu = [torch.randn((M + r - 1) // r, k) for k, r in zip(ks, rd)]
-    Kt = sum(ks)
-    W = torch.randn(N, Kt) / math.sqrt(Kt)
+    Kv = sum(ks)
+    Kp = sum(K.pad32(k) for k in ks)
+    W = torch.randn(N, Kv) / math.sqrt(Kv)
     b = torch.randn(N)
     X = torch.cat([s.repeat_interleave(r, dim=0)[:M] for s, r in zip(segs_cpu, rd)], dim=1)
-    ref = torch.relu(X @ W.T + b)
+    cm = []
+    off = 0
+    for k in ks:
+        cm += [off + j for j in range(k)] + [-1] * (K.pad32(k) - k)
+        off += k
+    Wp = torch.zeros(K.pad128(N), Kp)
+    for j, c in enumerate(cm):
+        if c >= 0:
+            Wp[:N, j] = W[:, c]
     segs = [(s.to(DEV), k, r) for s, k, r in zip(segs_cpu, ks, rd)]
-    Wp = torch.zeros(K.pad128(N), Kt)
-    Wp[:N] = W
-    out = torch.empty(M, K.pad32(N), device=DEV)
-    K.linear_fwd(segs, M, Wp.to(DEV), Kt, N, b.to(DEV), out, NERF_EPI_BIAS | NERF_EPI_RELU)
+    ldo = (N + 3) // 4 * 4
+    out = torch.empty(M, ldo, device=DEV)
+    K.linear_fwd(segs, M, Wp.to(DEV), Kp, N, b.to(DEV), out, NERF_EPI_BIAS | NERF_EPI_RELU)
+    ref = torch.relu(X @ W.T + b)
     np.testing.assert_allclose(out[:, :N].cpu().numpy(), ref.numpy(), atol=1e-4, rtol=1e-4)
-    # weight gradient
-    dY = torch.randn(M, K.pad32(N))
+    # ReLU-mask + accumulate epilogue
+    aux = torch.randn(M, ldo)
+    out2 = torch.randn(M, ldo)
+    o2 = out2.clone().to(DEV)
+    K.linear_fwd(segs, M, Wp.to(DEV), Kp, N, None, o2, NERF_EPI_MASK | NERF_EPI_ACCUM, aux=aux.to(DEV))
+    ref2 = out2[:, :N] + (X @ W.T) * (aux[:, :N] > 0)
+    np.testing.assert_allclose(o2[:, :N].cpu().numpy(), ref2.numpy(), atol=1e-4, rtol=1e-4)
+    # weight gradient, scattered through the column map
+    dY = torch.randn(M, ldo)
     dY[:, N:] = 0
-    N4 = (N + 3) // 4 * 4
-    ws = torch.empty((K.linear_wgrad_workspace_bytes(M, N4, Kt) + 3) // 4, device=DEV)
+    N4 = ldo
+    ws = torch.empty((K.linear_wgrad_workspace_bytes(M, N4, Kp) + 3) // 4, device=DEV)
     K.linear_wgrad(dY.to(DEV), N4, segs, M, ws)
-    dW = torch.empty(N, Kt, device=DEV)
+    dW = torch.empty(N, Kv, device=DEV)
     db = torch.empty(N, device=DEV)
-    cm = torch.arange(Kt, dtype=torch.int32, device=DEV)
-    K.linear_wgrad_reduce(M, N4, Kt, N, ws, cm, dW, db)
+    K.linear_wgrad_reduce(M, N4, Kp, N, ws, torch.tensor(cm, dtype=torch.int32, device=DEV), dW, db)
     np.testing.assert_allclose(dW.cpu().numpy(), (dY[:, :N].T.double() @ X.double()).float().numpy(), atol=2e-4,
                                rtol=1e-4)
     np.testing.assert_allclose(db.cpu().numpy(), dY[:, :N].sum(0).numpy(), atol=2e-4, rtol=1e-4)

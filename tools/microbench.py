@@ -42,41 +42,42 @@ def time_it(fn, reps=20, warm=3):
 
 def bench_linear(M, N, ks, rd, epi=NERF_EPI_BIAS | NERF_EPI_RELU):
     segs = [(torch.randn((M + r - 1) // r, k, device=DEV), k, r) for k, r in zip(ks, rd)]
-    Kt = sum(ks)
+    Kt = sum(K.pad32(k) for k in ks)
     W = torch.randn(K.pad128(N), Kt, device=DEV) * 0.05
     b = torch.randn(N, device=DEV)
-    out = torch.empty(M, K.pad32(N), device=DEV)
-    aux = torch.randn(M, K.pad32(N), device=DEV) if epi & NERF_EPI_MASK else None
+    ldo = (N + 3) // 4 * 4
+    out = torch.empty(M, ldo, device=DEV)
+    aux = torch.randn(M, ldo, device=DEV) if epi & NERF_EPI_MASK else None
     ms = time_it(lambda: K.linear_fwd(segs, M, W, Kt, N, b, out, epi, aux=aux))
-    fl = 2.0 * M * N * Kt
+    fl = 2.0 * M * N * sum(ks)
     return {"kernel": "linear_nt", "M": M, "N": N, "K": ks, "ms": ms, "tflops": fl / ms / 1e9}
 
 
 def bench_wgrad(M, N, ks, rd):
     segs = [(torch.randn((M + r - 1) // r, k, device=DEV), k, r) for k, r in zip(ks, rd)]
-    Kt = sum(ks)
+    Kt = sum(K.pad32(k) for k in ks)
     N4 = (N + 3) // 4 * 4
-    dY = torch.randn(M, K.pad32(N), device=DEV)
+    dY = torch.randn(M, N4, device=DEV)
     ws = torch.empty((K.linear_wgrad_workspace_bytes(M, N4, Kt) + 3) // 4, device=DEV)
     dW = torch.empty(N, Kt, device=DEV)
     db = torch.empty(N, device=DEV)
     cm = torch.arange(Kt, dtype=torch.int32, device=DEV)
     ms1 = time_it(lambda: K.linear_wgrad(dY, N4, segs, M, ws))
     ms2 = time_it(lambda: K.linear_wgrad_reduce(M, N4, Kt, N, ws, cm, dW, db))
-    fl = 2.0 * M * N * Kt
+    fl = 2.0 * M * N * sum(ks)
     return {"kernel": "linear_wgrad", "M": M, "N": N, "K": ks, "ms": ms1, "reduce_ms": ms2,
             "tflops": fl / ms1 / 1e9}
 
 
 def bench_composite(B, S):
-    head = torch.randn(B * S, 32, device=DEV)
+    head = torch.randn(B * S, 4, device=DEV)
     dist = torch.rand(B, S, device=DEV) * 0.01
-    ms = time_it(lambda: K.composite_fwd(head[:, 3:], 32, head, 32, dist, B, S, 3.0, 7.0, True))
+    ms = time_it(lambda: K.composite_fwd(head[:, 3:], 4, head, 4, dist, B, S, 3.0, 7.0, True))
     algo = B * S * (16 + 4 + 4) + B * 12
     g = torch.randn(B, 3, device=DEV)
     gh = torch.zeros_like(head)
-    ms_b = time_it(lambda: K.composite_bwd(head[:, 3:], 32, head, 32, dist, B, S, 3.0, 7.0, True, 0.0, g, None,
-                                           gh[:, 3:], 32, gh, 32))
+    ms_b = time_it(lambda: K.composite_bwd(head[:, 3:], 4, head, 4, dist, B, S, 3.0, 7.0, True, 0.0, g, None,
+                                           gh[:, 3:], 4, gh, 4))
     return {"kernel": "composite", "B": B, "S": S, "fwd_ms": ms, "fwd_GBs_algo": algo / ms / 1e6,
             "bwd_ms": ms_b}
 
@@ -117,7 +118,7 @@ def main():
     res.append(bench_linear(M, 4, (128,), (1,), NERF_EPI_BIAS))
     # input-gradient layers
     res.append(bench_linear(M, 256, (256,), (1,), NERF_EPI_MASK))
-    res.append(bench_linear(M, 128, (32,), (1,), NERF_EPI_MASK))
+    res.append(bench_linear(M, 128, (4,), (1,), NERF_EPI_MASK))
     res.append(bench_linear(M, 256, (128,), (1,), 0))
     # weight gradients
     res.append(bench_wgrad(M, 256, (256,), (1,)))
