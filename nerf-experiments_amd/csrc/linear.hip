@@ -141,7 +141,7 @@ __global__ __launch_bounds__(256, 2) void linear_nt_kernel(NTArgs a) {
             const bool ok = m < a.M;
             const unsigned mc = (unsigned)(ok ? m : a.M - 1);
             const unsigned src = (rd == 1u) ? mc : mc / rd;
-            aoff[i] = (int64_t)src * ld + c4 * 4;
+            aoff[i] = (int64_t)src * ld;  // row start; the column is added per chunk
             aok |= (ok ? 1u : 0u) << i;
         }
     };
@@ -153,9 +153,10 @@ __global__ __launch_bounds__(256, 2) void linear_nt_kernel(NTArgs a) {
     auto load_chunk = [&](int kc) __attribute__((always_inline)) {
         const int col = kc + c4 * 4;
         const bool cok = col < sk;
+        const int acol = cok ? col : 0;  // columns past k are never addressed (zero-filled)
 #pragma unroll
         for (int i = 0; i < NA; ++i) {
-            const f4 v = *reinterpret_cast<const f4*>(sp + aoff[i] + (cok ? kc : 0));
+            const f4 v = *reinterpret_cast<const f4*>(sp + aoff[i] + acol);
             ra[i] = (cok && ((aok >> i) & 1u)) ? v : f4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
