@@ -30,8 +30,18 @@ from ._lib import NERF_EPI_ACCUM, NERF_EPI_BIAS, NERF_EPI_MASK, NERF_EPI_RELU
 class Source:
     kind: str          # "pos" | "dir" | "act"
     k_valid: int       # columns of the source consumed (reference layout width)
-    k_pad: int         # columns in the padded buffer consumed by the kernel
+    k_pad: int         # columns the source occupies in the packed weight layout (multiple of 32)
     layer: int = -1    # producing layer for "act"
+
+    @property
+    def k_seg(self) -> int:
+        """Columns the kernel reads from the buffer (multiple of 4; the rest of the
+        32-wide chunk is zero-filled)."""
+        return (self.k_valid + 3) // 4 * 4
+
+    def __post_init__(self):
+        if self.kind == "act" and self.k_valid % 4:
+            raise NotImplementedError("nerf_amd needs hidden widths that are multiples of 4")
 
 
 @dataclass
@@ -126,7 +136,7 @@ class MLPFunction(torch.autograd.Function):
             segs = []
             for s in lp.sources:
                 t, rd = _src_tensor(s, pos, dirs, acts, dir_rd)
-                segs.append((t, s.k_pad, rd))
+                segs.append((t, s.k_seg, rd))
             out = torch.empty(M, lp.out_ld, device=pos.device, dtype=torch.float32)
             epi = NERF_EPI_BIAS | (NERF_EPI_RELU if lp.relu else 0)
             K.linear_fwd(segs, M, lp.Wp, lp.Kp, lp.N, lp.module.bias, out, epi)
@@ -179,7 +189,7 @@ class MLPFunction(torch.autograd.Function):
             segs = []
             for s in lp.sources:
                 t, rd = _src_tensor(s, pos, dirs, acts, ctx.dir_rd)
-                segs.append((t, s.k_pad, rd))
+                segs.append((t, s.k_seg, rd))
             # ---- weight and bias gradients
             N4 = (lp.N + 3) // 4 * 4
             gW = torch.empty_like(w)
@@ -250,22 +260,23 @@ def nerf_model_plan(n_segments: int, model_segments: nn.ModuleList, model_color:
             srcs: list[Source] = []
             if j == 0:
                 if prev >= 0:
-                    srcs.append(Source("act", hidden_dim, hidden_dim, prev))
+                    srcs.append(Source("act", hidden_dim, K.pad32(hidden_dim), prev))
                 if not delayed_direction:
                     srcs.append(dir_src)
                 srcs.append(pos_src)
             else:
-                srcs.append(Source("act", hidden_dim, hidden_dim, len(layers) - 1))
+                srcs.append(Source("act", hidden_dim, K.pad32(hidden_dim), len(layers) - 1))
             last_in_seg = j == len(linears) - 1
             relu = (not last_in_seg) or (i < n_segments - 1)
             layers.append(LayerPlan(lin, srcs, relu))
         prev = len(layers) - 1
     z_last = prev
     head0, head1 = model_color[0], model_color[2]
-    srcs = [Source("act", hidden_dim, hidden_dim, z_last)]
+    srcs = [Source("act", hidden_dim, K.pad32(hidden_dim), z_last)]
     if delayed_direction:
         srcs.append(dir_src)
     layers.append(LayerPlan(head0, srcs, True))
-    layers.append(LayerPlan(head1, [Source("act", head0.out_features, head0.out_features, len(layers) - 1)], False))
+    layers.append(LayerPlan(head1, [Source("act", head0.out_features, K.pad32(head0.out_features), len(layers) - 1)],
+                            False))
     head_out = len(layers) - 1
     return MLPPlan(layers, [z_last, head_out]), z_last, head_out

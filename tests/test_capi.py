@@ -1,0 +1,84 @@
+"""C-ABI library: loads without a GPU, exports exactly what include/nerf_amd.h
+declares, and rejects bad arguments with a status (no compute launched)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "nerf_amd.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(nerf_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_entry_points():
+    fns = header_functions()
+    for name in ("nerf_composite_fwd", "nerf_composite_bwd", "nerf_resample_pdf", "nerf_sample_uniform",
+                 "nerf_encode_fwd", "nerf_encode_bwd", "nerf_linear_fwd", "nerf_linear_wgrad",
+                 "nerf_linear_wgrad_reduce", "nerf_pack_weight"):
+        assert name in fns
+
+
+def test_library_exports_every_header_symbol():
+    from nerf_amd import _lib
+    lib = _lib.load()
+    for name in header_functions():
+        assert hasattr(lib, name), name
+    assert sorted(_lib.EXPORTED_SYMBOLS) == header_functions()
+
+
+def test_exported_dynamic_symbols_with_nm():
+    import subprocess
+    from nerf_amd import _lib
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    syms = set(re.findall(r"\b(nerf_[a-z0-9_]+)\b", out))
+    assert set(header_functions()) <= syms
+
+
+def test_abi_version_and_status_strings():
+    from nerf_amd import _lib
+    lib = _lib.load()
+    assert lib.nerf_abi_version() == 1
+    assert lib.nerf_status_string(0) == b"ok"
+    assert b"invalid" in lib.nerf_status_string(-1)
+    assert b"workspace" in lib.nerf_status_string(-4)
+
+
+def test_argument_validation_returns_status_without_launch():
+    from nerf_amd import _lib
+    lib = _lib.load()
+    # null pointers / bad sizes are rejected before anything touches the device
+    assert lib.nerf_composite_fwd(None, 1, None, 3, None, 5, 64, 3.0, 1.0, 0, 0.0, None, None, None) == -1
+    assert lib.nerf_composite_fwd(None, 1, None, 3, None, 0, 64, 3.0, 1.0, 0, 0.0, None, None, None) == 0
+    assert lib.nerf_resample_pdf(None, None, None, 4, 64, 128, 0, 0.0, 1.0, 0, 0, None, None, None, None) == -1
+    seg = (_lib.NerfSeg * 1)()
+    seg[0].ptr = None
+    assert lib.nerf_linear_fwd(seg, 1, 10, None, 32, 4, None, None, 4, 0, None, 0, None) == -1
+    seg[0].ptr = 16
+    seg[0].ld = 32
+    seg[0].k = 6          # not a multiple of 4
+    seg[0].row_div = 1
+    assert lib.nerf_linear_fwd(seg, 1, 10, 16, 32, 4, None, 16, 4, 0, None, 0, None) == -1
+    assert lib.nerf_linear_wgrad(16, 8, 6, seg, 1, 10, None, 0, None) == -1   # N % 4 != 0
+    p = _lib.NerfPEParams()
+    p.levels = 20
+    assert lib.nerf_encode_fwd(ctypes.byref(p), None, None, None, None, None, None, None, 10, 1, 10, 16, 64,
+                               None) == -1
+
+
+def test_check_raises_with_message():
+    from nerf_amd import _lib
+    with pytest.raises(RuntimeError, match="invalid argument"):
+        _lib.check(-1, "nerf_test")
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    from nerf_amd import _lib
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        _lib.load(str(tmp_path / "absent.so"))

@@ -1,0 +1,64 @@
+"""Ray-batch DP on CPU with the gloo backend, world size 2: the gradient
+all-reduce produces the mean gradient on every rank, and DP over two shards
+equals the full-batch gradient of a shared model (the multi-GPU bench path)."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                        "nerf-experiments_amd"))
+        from nerf_amd.ddp import GradAllReduce, shard_rays
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Linear(6, 16), torch.nn.ReLU(), torch.nn.Linear(16, 3))
+        g = torch.Generator().manual_seed(42)
+        x = torch.randn(64, 6, generator=g)
+        y = torch.randn(64, 3, generator=g)
+        sl = shard_rays(64, rank, world)
+        loss = torch.nn.functional.mse_loss(model(x[sl]), y[sl], reduction="sum") / 64 * world
+        loss.backward()
+        GradAllReduce(model.parameters())()
+        flat = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
+        q.put((rank, flat))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # reference: full-batch gradient on one process
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(6, 16), torch.nn.ReLU(), torch.nn.Linear(16, 3))
+    g = torch.Generator().manual_seed(42)
+    x = torch.randn(64, 6, generator=g)
+    y = torch.randn(64, 3, generator=g)
+    torch.nn.functional.mse_loss(model(x), y, reduction="sum").div(64).backward()
+    ref = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
+    assert torch.allclose(res[0], res[1])
+    assert torch.allclose(res[0], ref, atol=1e-6)

@@ -1,0 +1,170 @@
+"""Host-side logic that needs no GPU: MLP lowering, packing maps, encoder
+bookkeeping, schedules, state_dict layout, and that the product path refuses
+CPU tensors (no silent fallback)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import nerf_oracle as O
+
+
+def _models():
+    from nerf_amd import BarfPositionalEncoding, FourierFeatures, NerfModel
+    torch.manual_seed(0)
+    barf = NerfModel(4, 256, True, False, 2, BarfPositionalEncoding(10, 10.0, 0, 1, True, 1.0),
+                     BarfPositionalEncoding(4, 4.0, 0, 1, True, 1.0))
+    torch.manual_seed(0)
+    n2v = NerfModel(4, 256, True, True, 2, FourierFeatures(10, 2 * math.pi), FourierFeatures(4, 1.0))
+    torch.manual_seed(0)
+    small = NerfModel(2, 64, False, False, 3, BarfPositionalEncoding(6, 3.4, 0, 1, True, 1.0),
+                      BarfPositionalEncoding(2, 1.5, 0, 1, False, 1.0))
+    torch.manual_seed(0)
+    flat = NerfModel(0, 32, False, True, 2, FourierFeatures(2, 1.0), FourierFeatures(1, 1.0))
+    return {"barf": barf, "n2v": n2v, "small": small, "flat": flat}
+
+
+@pytest.mark.parametrize("name", ["barf", "n2v", "small", "flat"])
+def test_state_dict_layout_and_init_match_reference(golden, name):
+    m = _models()[name]
+    if name == "flat":
+        assert [k for k in m.state_dict()] == ["model_segments.0.weight", "model_segments.0.bias",
+                                              "model_segments.1.weight", "model_segments.1.bias",
+                                              "model_color.0.weight", "model_color.0.bias",
+                                              "model_color.2.weight", "model_color.2.bias"]
+        return
+    g = golden("model")
+    keys = sorted(k.split(".sdsum.", 1)[1] for k in g if k.startswith(f"{name}.sdsum."))
+    assert sorted(m.state_dict().keys()) == keys
+    for k, v in m.state_dict().items():
+        ref = g[f"{name}.sdsum.{k}"]
+        assert abs(v.double().sum().item() - ref[0]) <= 1e-9 * max(1.0, abs(ref[1])), k
+
+
+@pytest.mark.parametrize("name", ["barf", "n2v", "small", "flat"])
+def test_mlp_lowering(name):
+    from nerf_amd.mlp import nerf_model_plan
+    m = _models()[name]
+    plan, z_last, head = nerf_model_plan(m.n_segments, m.model_segments, m.model_color, m.hidden_dim,
+                                         m.position_encoder.output_dim, m.direction_encoder.output_dim,
+                                         m.delayed_direction, m.delayed_density)
+    linears = [mod for mod in m.modules() if isinstance(mod, torch.nn.Linear)]
+    assert len(plan.layers) == len(linears)
+    assert {id(lp.module) for lp in plan.layers} == {id(x) for x in linears}
+    assert plan.outputs == [z_last, head] and head == len(plan.layers) - 1
+    for i, lp in enumerate(plan.layers):
+        lp.finalize("cpu")
+        # the column map is a bijection onto the Linear's input columns
+        cm = lp.col_map.tolist()
+        assert sorted(c for c in cm if c >= 0) == list(range(lp.module.in_features))
+        assert lp.Kp % 32 == 0 and lp.Kp == len(cm)
+        # relu everywhere except the last layer of the last segment and the colour output
+        assert lp.relu == (i not in (z_last, head))
+    # the head reads z_last without its density column and the direction encoding (if delayed)
+    srcs = plan.layers[head - 1].sources
+    assert srcs[0].kind == "act" and srcs[0].layer == z_last and srcs[0].k_valid == m.hidden_dim
+    assert (len(srcs) == 2) == m.delayed_direction
+    # segment inputs follow the reference order [z, dir, pos]
+    first = [lp for lp in plan.layers if any(s.kind == "pos" for s in lp.sources)]
+    assert len(first) == m.n_segments
+    for i, lp in enumerate(first):
+        kinds = [s.kind for s in lp.sources]
+        expect = (["act"] if i > 0 else []) + ([] if m.delayed_direction else ["dir"]) + ["pos"]
+        assert kinds == expect
+
+
+def test_col_map_follows_reference_concatenation():
+    """Packed column j of a segment maps to the Linear input column of the same feature."""
+    from nerf_amd.mlp import LayerPlan, Source
+    lin = torch.nn.Linear(256 + 63, 256)
+    lp = LayerPlan(lin, [Source("act", 256, 256, 0), Source("pos", 63, 64)], True)
+    lp.finalize("cpu")
+    cm = lp.col_map.tolist()
+    assert cm[:256] == list(range(256)) and cm[256:319] == list(range(256, 319)) and cm[319] == -1
+
+
+@pytest.mark.parametrize("alpha", [0.0, 0.5, 3.4, 9.99, 10.0, 12.0])
+def test_barf_mask_values(alpha):
+    from nerf_amd.positional_encodings import barf_mask_values
+    assert barf_mask_values(alpha, 10) == O.barf_mask(alpha, 10).tolist()
+
+
+def test_barf_alpha_schedule_and_state_dict():
+    from nerf_amd import BarfPositionalEncoding
+    enc = BarfPositionalEncoding(10, 1.0, 2.0, 6.0, True, 1.0)
+    for epoch, want in ((0.0, 1.0), (2.0, 1.0), (4.0, 5.5), (6.0, 10.0), (100.0, 10.0)):
+        enc.update_alpha(epoch)
+        assert abs(enc._alpha_host - want) < 1e-6 and abs(float(enc.alpha) - want) < 1e-6
+    enc2 = BarfPositionalEncoding(10, 0.0, 2.0, 6.0, True, 1.0)
+    enc2.load_state_dict(enc.state_dict())
+    assert enc2._alpha_host == enc._alpha_host
+    assert enc.output_dim == 63 and enc.padded_dim == 64
+
+
+def test_encoder_dims_and_errors():
+    from nerf_amd import (FourierFeatures, IdentityPositionalEncoding, IntegratedBarfFourierFeatures,
+                          IntegratedFourierFeatures)
+    assert FourierFeatures(10).output_dim == 60 and FourierFeatures(4, 1.0).padded_dim == 32
+    assert IdentityPositionalEncoding().output_dim == 3
+    ipe = IntegratedFourierFeatures(10, 2 * math.pi, True, True)
+    assert ipe.output_dim == 63
+    with pytest.raises(TypeError):
+        ipe._pe_params()          # pixel_width_sigma unset: the reference raises TypeError too
+    ib = IntegratedBarfFourierFeatures(10, 0, 0, 1, False, 1.0, True)
+    assert ib.output_dim == 60
+    with pytest.raises(ValueError):
+        FourierFeatures(4).encode_padded(torch.zeros(5, 2))
+
+
+def test_product_path_refuses_cpu_tensors():
+    from nerf_amd import FourierFeatures
+    with pytest.raises(ValueError, match="ROCm device"):
+        FourierFeatures(4)(torch.zeros(8, 3))
+
+
+def test_scheduler_le_nice():
+    from nerf_amd import SchedulerLeNice
+    p = torch.nn.Parameter(torch.zeros(1))
+    q = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.Adam([{"params": [p], "lr": 1e-3}, {"params": [q], "lr": 5e-4}], eps=1e-5)
+    sch = SchedulerLeNice(opt, [1e-3, 5e-4], [1e-5, 5e-5], [100, 0])
+    for _ in range(100):
+        opt.step()
+        sch.step()
+    assert abs(opt.param_groups[0]["lr"] - 1e-5) < 1e-9
+    assert abs(opt.param_groups[1]["lr"] - 5e-4) < 1e-12
+    for _ in range(10):
+        opt.step()
+        sch.step()
+    assert abs(opt.param_groups[0]["lr"] - 1e-5) < 1e-9
+
+
+def test_renderer_param_groups_and_optimizer():
+    from nerf_amd import NerfInterpolation
+    m = _models()["barf"]
+    ren = NerfInterpolation(2.0, 8.0, m, 128, "equidistant", -1.0, "middle", m, 64)
+    assert len(ren.param_groups) == 2 and ren.proposal
+    cfg = ren.configure_optimizers()
+    assert isinstance(cfg["optimizer"], torch.optim.Adam) and cfg["optimizer"].defaults["eps"] == 1e-5
+    assert cfg["lr_scheduler"]["interval"] == "step"
+    with pytest.raises(ValueError):
+        ren._get_t_query(torch.zeros(1), torch.zeros(1), "bogus")
+
+
+def test_oracle_resample_fallback_flag():
+    w = torch.rand(3, 64)
+    w[1] = 0
+    tc = torch.sort(torch.rand(3, 64), dim=1).values
+    _, _, ok = O.sample_t_pdf_weighted(tc, w, torch.full((3, 64), 0.01), 128, 1.0, 0)
+    assert not ok
+
+
+def test_shard_rays_partition():
+    from nerf_amd.ddp import shard_rays
+    for n, w in ((4096, 8), (1000, 3), (5, 8)):
+        idx = []
+        for r in range(w):
+            sl = shard_rays(n, r, w)
+            idx += list(range(n))[sl]
+        assert idx == list(range(n))
