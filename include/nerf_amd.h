@@ -182,6 +182,7 @@ typedef struct nerf_seg {
 #define NERF_EPI_RELU  2   /* max(., 0) */
 #define NERF_EPI_MASK  4   /* * (aux[m, n] > 0): ReLU backward */
 #define NERF_EPI_ACCUM 8   /* out += result */
+#define NERF_EPI_NO_PERSIST 256  /* tuning: one tile per workgroup instead of a persistent grid */
 
 /* out[m, n] = epi( sum_k A[m, k] * W[n, k] ),  m < M, n < N.
  * W: packed row-major [ceil(N/128)*128][ldw], ldw = sum_j kp_j (zero padding

@@ -88,38 +88,45 @@ struct TileCfg<32> {
     static constexpr int WAVES_N = 1, WM = 32, WN = 32, BM = 128;
 };
 
+// XCD-aware tile order: blocks b and b + 8 are dealt to the same XCD, so the ntn
+// column tiles of one row tile (which share the A rows) are placed 8 apart and
+// read A once from HBM into that XCD's L2.  Returns false for padding tiles.
+__device__ __forceinline__ bool tile_coords(int tile, int ntm, int ntn, int& tm, int& tn) {
+    const int grp = 8 * ntn;
+    const int g = tile / grp, r = tile - g * grp;
+    tn = r / 8;
+    tm = g * 8 + (r - tn * 8);
+    return tm < ntm;
+}
+
+// Persistent over output tiles: a workgroup walks tiles blockIdx.x, +gridDim.x, ...
+// and stages the NEXT tile's first K chunk during the current tile's last chunk,
+// so the HBM latency of a tile start is hidden behind MFMA work.  The epilogue
+// stages the accumulators through the idle LDS buffer, 64 rows at a time.
 template <int BN>
-__global__ __launch_bounds__(256, 2) void linear_nt_kernel(NTArgs a) {
+__global__ __launch_bounds__(256, 2) void linear_nt_kernel(NTArgs a, int ntm, int ntiles) {
     using Cfg = TileCfg<BN>;
     constexpr int BM = Cfg::BM, WM = Cfg::WM, WN = Cfg::WN;
     constexpr int MB = WM / 32, NB = WN / 32;   // MFMA blocks per wave
     constexpr int NA = BM / 32, NW = BN / 32;   // f4 staging loads per thread per chunk
     constexpr int LDC = BN + 4;
-    constexpr int LDS_AB = 2 * (BM + BN) * LDP;
-    constexpr int LDS_C = BM * LDC;
-    constexpr int LDS_FLOATS = LDS_AB > LDS_C ? LDS_AB : LDS_C;
     constexpr int BUF = (BM + BN) * LDP;
-    __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
+    constexpr int HR = BM / 2;                  // epilogue rows per half
+    static_assert(HR * LDC <= BUF, "epilogue half-tile must fit one staging buffer");
+    __shared__ __attribute__((aligned(16))) float smem[2 * BUF];
 
     const int ntn = (a.N + BN - 1) / BN;
-    const int bid = blockIdx.x;
-    const int tn = bid % ntn;
-    const int m0 = (bid / ntn) * BM;
-    const int n0 = tn * BN;
-
     const int t = threadIdx.x;
     const int wave = t >> 6, lane = t & 63;
     const int wr = wave / Cfg::WAVES_N, wc = wave % Cfg::WAVES_N;
     const int li = lane & 31, lh = lane >> 5;
     const int c4 = t & 7, rbase = t >> 3;
 
-    f32x16 acc[MB][NB];
-#pragma unroll
-    for (int i = 0; i < MB; ++i)
-#pragma unroll
-        for (int j = 0; j < NB; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    // find this workgroup's first real tile
+    int tile = blockIdx.x, tm = 0, tn = 0;
+    while (tile < ntiles && !tile_coords(tile, ntm, ntn, tm, tn)) tile += gridDim.x;
+    if (tile >= ntiles) return;
+    int m0 = tm * BM, n0 = tn * BN;
 
     // ---- segment state: scalar parameters + per-thread row offsets
     int seg = 0;
@@ -127,7 +134,7 @@ __global__ __launch_bounds__(256, 2) void linear_nt_kernel(NTArgs a) {
     int sk = 0, skp = 0, skoff = 0;
     int64_t aoff[NA];
     unsigned aok = 0;
-    auto set_seg = [&](int s) __attribute__((always_inline)) {
+    auto set_seg = [&](int s, int mbase) __attribute__((always_inline)) {
         sp = pick4(a.A.ptr, s);
         const int64_t ld = pick4(a.A.ld, s);
         const unsigned rd = (unsigned)pick4(a.A.row_div, s);
@@ -137,7 +144,7 @@ __global__ __launch_bounds__(256, 2) void linear_nt_kernel(NTArgs a) {
         aok = 0;
 #pragma unroll
         for (int i = 0; i < NA; ++i) {
-            const int m = m0 + i * 32 + rbase;
+            const int m = mbase + i * 32 + rbase;
             const bool ok = m < a.M;
             const unsigned mc = (unsigned)(ok ? m : a.M - 1);
             const unsigned src = (rd == 1u) ? mc : mc / rd;
@@ -146,8 +153,10 @@ __global__ __launch_bounds__(256, 2) void linear_nt_kernel(NTArgs a) {
         }
     };
     int64_t woff[NW];
+    auto set_w = [&](int nbase) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < NW; ++j) woff[j] = (int64_t)(n0 + j * 32 + rbase) * a.ldw + c4 * 4;
+        for (int j = 0; j < NW; ++j) woff[j] = (int64_t)(nbase + j * 32 + rbase) * a.ldw + c4 * 4;
+    };
 
     f4 ra[NA], rw[NW];
     auto load_chunk = [&](int kc) __attribute__((always_inline)) {
@@ -171,105 +180,132 @@ __global__ __launch_bounds__(256, 2) void linear_nt_kernel(NTArgs a) {
         for (int j = 0; j < NW; ++j) *reinterpret_cast<f4*>(Ws + (j * 32 + rbase) * LDP + c4 * 4) = rw[j];
     };
 
-    set_seg(0);
+    set_seg(0, m0);
+    set_w(n0);
     int kc = 0;
     load_chunk(0);
     store_chunk(0);
     __syncthreads();
     const int nchunks = a.A.ktot / BK;
     int cur = 0;
-    for (int c = 0; c < nchunks; ++c) {
-        // stage chunk c+1 (the last iteration re-stages the current chunk into the
-        // idle buffer, which is never read: keeps the staging registers branch-free)
-        const bool has_next = c + 1 < nchunks;
-        if (has_next) {
-            kc += BK;
-            if (kc >= skp) {
-                ++seg;
-                set_seg(seg);
-                kc = 0;
-            }
-        }
-        load_chunk(kc);
 
-        const float* Ab = smem + cur * BUF + (wr * WM + li) * LDP + lh * 16;
-        const float* Bb = smem + cur * BUF + BM * LDP + (wc * WN + li) * LDP + lh * 16;
+    while (true) {
+        // next tile of this workgroup (if any)
+        int ntile = tile + gridDim.x, ntm_ = 0, ntn_ = 0;
+        while (ntile < ntiles && !tile_coords(ntile, ntm, ntn, ntm_, ntn_)) ntile += gridDim.x;
+        const bool has_next_tile = ntile < ntiles;
+
+        f32x16 acc[MB][NB];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            f4 av[MB], bv[NB];
+        for (int i = 0; i < MB; ++i)
 #pragma unroll
-            for (int i = 0; i < MB; ++i) av[i] = *reinterpret_cast<const f4*>(Ab + i * 32 * LDP + g * 4);
+            for (int j = 0; j < NB; ++j)
 #pragma unroll
-            for (int j = 0; j < NB; ++j) bv[j] = *reinterpret_cast<const f4*>(Bb + j * 32 * LDP + g * 4);
-#pragma unroll
-            for (int i = 0; i < MB; ++i)
-#pragma unroll
-                for (int j = 0; j < NB; ++j) {
-                    acc[i][j] = mfma32(av[i].x, bv[j].x, acc[i][j]);
-                    acc[i][j] = mfma32(av[i].y, bv[j].y, acc[i][j]);
-                    acc[i][j] = mfma32(av[i].z, bv[j].z, acc[i][j]);
-                    acc[i][j] = mfma32(av[i].w, bv[j].w, acc[i][j]);
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+        for (int c = 0; c < nchunks; ++c) {
+            // stage the next chunk: of this tile, else the first chunk of the next tile
+            // (else re-stage chunk 0 into the idle buffer, never read: branch-free registers)
+            if (c + 1 < nchunks) {
+                kc += BK;
+                if (kc >= skp) {
+                    ++seg;
+                    set_seg(seg, m0);
+                    kc = 0;
                 }
-        }
-        store_chunk(cur ^ 1);
-        __syncthreads();
-        cur ^= 1;
-    }
+            } else {
+                seg = 0;
+                kc = 0;
+                set_seg(0, has_next_tile ? ntm_ * BM : m0);
+                set_w(has_next_tile ? ntn_ * BN : n0);
+            }
+            load_chunk(kc);
 
-    // ---- epilogue: accumulators -> LDS tile -> coalesced 16-byte rows
-    // C/D map of the 32x32 MFMA: col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-    float* Cs = smem;
+            const float* Ab = smem + cur * BUF + (wr * WM + li) * LDP + lh * 16;
+            const float* Bb = smem + cur * BUF + BM * LDP + (wc * WN + li) * LDP + lh * 16;
 #pragma unroll
-    for (int i = 0; i < MB; ++i)
+            for (int g = 0; g < 4; ++g) {
+                f4 av[MB], bv[NB];
 #pragma unroll
-        for (int j = 0; j < NB; ++j)
+                for (int i = 0; i < MB; ++i) av[i] = *reinterpret_cast<const f4*>(Ab + i * 32 * LDP + g * 4);
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = wr * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                Cs[row * LDC + wc * WN + j * 32 + li] = acc[i][j][r];
-            }
-    __syncthreads();
-    constexpr int Q = BN / 4;               // f4 per tile row
-    constexpr int ITER = BM * Q / 256;
-#pragma unroll 4
-    for (int it = 0; it < ITER; ++it) {
-        const int q = it * 256 + t;
-        const int row = q / Q, cq = q - (q / Q) * Q;
-        const int m = m0 + row;
-        const int n = n0 + cq * 4;
-        if (m >= a.M || n >= a.N) continue;
-        f4 v = *reinterpret_cast<const f4*>(Cs + row * LDC + cq * 4);
-        float* o = a.out + (int64_t)m * a.ldo + n;
-        if (a.vec_ok && n + 4 <= a.N) {
-            if (a.epi & NERF_EPI_BIAS) {
-                const f4 b = *reinterpret_cast<const f4*>(a.bias + n);
-                v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
-            }
-            if (a.epi & NERF_EPI_RELU) {
-                v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
-            }
-            if (a.epi & NERF_EPI_MASK) {
-                const f4 x = *reinterpret_cast<const f4*>(a.aux + (int64_t)m * a.ldaux + n);
-                v.x = x.x > 0.f ? v.x : 0.f; v.y = x.y > 0.f ? v.y : 0.f;
-                v.z = x.z > 0.f ? v.z : 0.f; v.w = x.w > 0.f ? v.w : 0.f;
-            }
-            if (a.epi & NERF_EPI_ACCUM) {
-                const f4 p = *reinterpret_cast<const f4*>(o);
-                v.x = p.x + v.x; v.y = p.y + v.y; v.z = p.z + v.z; v.w = p.w + v.w;
-            }
-            *reinterpret_cast<f4*>(o) = v;
-        } else {
+                for (int j = 0; j < NB; ++j) bv[j] = *reinterpret_cast<const f4*>(Bb + j * 32 * LDP + g * 4);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                if (n + e >= a.N) break;
-                float x = e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
-                if (a.epi & NERF_EPI_BIAS) x = x + a.bias[n + e];
-                if (a.epi & NERF_EPI_RELU) x = fmaxf(x, 0.f);
-                if (a.epi & NERF_EPI_MASK) x = (a.aux[(int64_t)m * a.ldaux + n + e] > 0.f) ? x : 0.f;
-                if (a.epi & NERF_EPI_ACCUM) x = o[e] + x;
-                o[e] = x;
+                for (int i = 0; i < MB; ++i)
+#pragma unroll
+                    for (int j = 0; j < NB; ++j) {
+                        acc[i][j] = mfma32(av[i].x, bv[j].x, acc[i][j]);
+                        acc[i][j] = mfma32(av[i].y, bv[j].y, acc[i][j]);
+                        acc[i][j] = mfma32(av[i].z, bv[j].z, acc[i][j]);
+                        acc[i][j] = mfma32(av[i].w, bv[j].w, acc[i][j]);
+                    }
             }
+            store_chunk(cur ^ 1);
+            __syncthreads();
+            cur ^= 1;
         }
+        // now `cur` holds the next tile's first chunk; buffer cur ^ 1 is idle
+
+        // ---- epilogue: accumulators -> idle LDS buffer (64 rows at a time) -> 16-byte rows
+        // C/D map of the 32x32 MFMA: col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+        float* Cs = smem + (cur ^ 1) * BUF;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if ((wr * WM) / HR == h) {
+#pragma unroll
+                for (int i = 0; i < MB; ++i)
+#pragma unroll
+                    for (int j = 0; j < NB; ++j)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int row = wr * WM - h * HR + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                            Cs[row * LDC + wc * WN + j * 32 + li] = acc[i][j][r];
+                        }
+            }
+            __syncthreads();
+            constexpr int Q = BN / 4;               // f4 per tile row
+            constexpr int ITER = HR * Q / 256;
+#pragma unroll 4
+            for (int it = 0; it < ITER; ++it) {
+                const int q = it * 256 + t;
+                const int row = q / Q, cq = q - (q / Q) * Q;
+                const int m = m0 + h * HR + row;
+                const int n = n0 + cq * 4;
+                if (m >= a.M || n >= a.N) continue;
+                f4 v = *reinterpret_cast<const f4*>(Cs + row * LDC + cq * 4);
+                float* o = a.out + (int64_t)m * a.ldo + n;
+                if (a.vec_ok && n + 4 <= a.N) {
+                    if (a.epi & NERF_EPI_BIAS) v += *reinterpret_cast<const f4*>(a.bias + n);
+                    if (a.epi & NERF_EPI_RELU) {
+                        v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+                    }
+                    if (a.epi & NERF_EPI_MASK) {
+                        const f4 x = *reinterpret_cast<const f4*>(a.aux + (int64_t)m * a.ldaux + n);
+                        v.x = x.x > 0.f ? v.x : 0.f; v.y = x.y > 0.f ? v.y : 0.f;
+                        v.z = x.z > 0.f ? v.z : 0.f; v.w = x.w > 0.f ? v.w : 0.f;
+                    }
+                    if (a.epi & NERF_EPI_ACCUM) v = *reinterpret_cast<const f4*>(o) + v;
+                    *reinterpret_cast<f4*>(o) = v;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        if (n + e >= a.N) break;
+                        float x = e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
+                        if (a.epi & NERF_EPI_BIAS) x = x + a.bias[n + e];
+                        if (a.epi & NERF_EPI_RELU) x = fmaxf(x, 0.f);
+                        if (a.epi & NERF_EPI_MASK) x = (a.aux[(int64_t)m * a.ldaux + n + e] > 0.f) ? x : 0.f;
+                        if (a.epi & NERF_EPI_ACCUM) x = o[e] + x;
+                        o[e] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+
+        if (!has_next_tile) break;
+        tile = ntile;
+        m0 = ntm_ * BM;
+        n0 = ntn_ * BN;
     }
 }
 
@@ -450,6 +486,19 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(int splits, int n_val
     }
 }
 
+// compute units of the current device (cached per device id)
+int cu_count() {
+    static int cached[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cached[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cached[dev] = n;
+    }
+    return cached[dev];
+}
+
 int choose_splits(int64_t M, int tiles) {
     int64_t target = 512 / (tiles > 0 ? tiles : 1);
     if (target > 128) target = 128;
@@ -512,13 +561,19 @@ extern "C" int nerf_linear_fwd(const nerf_seg* segs, int32_t n_segs, int64_t M, 
     const int vec_ok = aligned16(out) && (ldo % 4) == 0 && (!(epilogue & NERF_EPI_BIAS) || aligned16(bias)) &&
                        (!(epilogue & NERF_EPI_MASK) || (aligned16(aux) && (ld_aux % 4) == 0));
     NTArgs a{L, (int)M, W, ldw, N, bias, out, ldo, epilogue, aux, ld_aux, vec_ok};
-    const int64_t ntm = (M + 127) / 128;
+    const int ntm = (int)((M + 127) / 128);
+    const int ntn = N <= 32 ? 1 : (N + 127) / 128;
+    const int ntiles = (ntm + 7) / 8 * 8 * ntn;        // XCD-aware order pads to groups of 8 row tiles
+    int grid = ntiles;
+    if (!(epilogue & NERF_EPI_NO_PERSIST)) {
+        const int cap = 2 * cu_count();                 // two resident workgroups per CU
+        if (grid > cap) grid = cap;
+    }
     hipStream_t st = as_stream(stream);
     if (N <= 32) {
-        hipLaunchKernelGGL(linear_nt_kernel<32>, dim3((unsigned)ntm), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(linear_nt_kernel<32>, dim3((unsigned)grid), dim3(256), 0, st, a, ntm, ntiles);
     } else {
-        const int64_t ntn = (N + 127) / 128;
-        hipLaunchKernelGGL(linear_nt_kernel<128>, dim3((unsigned)(ntm * ntn)), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(linear_nt_kernel<128>, dim3((unsigned)grid), dim3(256), 0, st, a, ntm, ntiles);
     }
     NERF_CHECK_LAUNCH();
     return NERF_OK;

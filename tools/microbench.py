@@ -21,6 +21,8 @@ sys.path.insert(0, os.path.join(ROOT, "nerf-experiments_amd"))
 from nerf_amd import kernels as K  # noqa: E402
 from nerf_amd._lib import NERF_EPI_BIAS, NERF_EPI_MASK, NERF_EPI_RELU  # noqa: E402
 
+NERF_EPI_NO_PERSIST = 256
+
 DEV = torch.device("cuda", 0)
 
 
@@ -50,7 +52,11 @@ def bench_linear(M, N, ks, rd, epi=NERF_EPI_BIAS | NERF_EPI_RELU):
     aux = torch.randn(M, ldo, device=DEV) if epi & NERF_EPI_MASK else None
     ms = time_it(lambda: K.linear_fwd(segs, M, W, Kt, N, b, out, epi, aux=aux))
     fl = 2.0 * M * N * sum(ks)
-    return {"kernel": "linear_nt", "M": M, "N": N, "K": ks, "ms": ms, "tflops": fl / ms / 1e9}
+    r = {"kernel": "linear_nt", "M": M, "N": N, "K": ks, "ms": ms, "tflops": fl / ms / 1e9}
+    # A/B in the same process: one tile per workgroup (no persistence)
+    ms_np = time_it(lambda: K.linear_fwd(segs, M, W, Kt, N, b, out, epi | NERF_EPI_NO_PERSIST, aux=aux))
+    r["tflops_no_persist"] = fl / ms_np / 1e9
+    return r
 
 
 def bench_wgrad(M, N, ks, rd):
@@ -107,9 +113,16 @@ def bench_resample(B, Kb, N):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json")
+    ap.add_argument("--only", help="run one shape repeatedly for counter collection: nt256 | nt256mask | wgrad256")
     args = ap.parse_args()
     M = 4096 * 64
     res = []
+    if args.only:
+        fn = {"nt256": lambda: bench_linear(M, 256, (256,), (1,)),
+              "nt256mask": lambda: bench_linear(M, 256, (256,), (1,), NERF_EPI_MASK),
+              "wgrad256": lambda: bench_wgrad(M, 256, (256,), (1,))}[args.only]
+        print(json.dumps(fn()))
+        return
     # forward layers of the bench model
     res.append(bench_linear(M, 256, (64,), (1,)))
     res.append(bench_linear(M, 256, (256,), (1,)))
