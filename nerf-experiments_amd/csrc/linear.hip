@@ -159,15 +159,15 @@ __global__ __launch_bounds__(256, 2) void linear_nt_kernel(NTArgs a, int ntm, in
     };
 
     f4 ra[NA], rw[NW];
+    unsigned rmask = 0;  // rows/columns of the staged chunk to zero-fill (applied at the LDS write,
+                         // so the loads stay in flight under the MFMAs)
     auto load_chunk = [&](int kc) __attribute__((always_inline)) {
         const int col = kc + c4 * 4;
         const bool cok = col < sk;
         const int acol = cok ? col : 0;  // columns past k are never addressed (zero-filled)
+        rmask = cok ? aok : 0u;
 #pragma unroll
-        for (int i = 0; i < NA; ++i) {
-            const f4 v = *reinterpret_cast<const f4*>(sp + aoff[i] + acol);
-            ra[i] = (cok && ((aok >> i) & 1u)) ? v : f4{0.f, 0.f, 0.f, 0.f};
-        }
+        for (int i = 0; i < NA; ++i) ra[i] = *reinterpret_cast<const f4*>(sp + aoff[i] + acol);
 #pragma unroll
         for (int j = 0; j < NW; ++j) rw[j] = *reinterpret_cast<const f4*>(a.W + woff[j] + skoff + kc);
     };
@@ -175,7 +175,9 @@ __global__ __launch_bounds__(256, 2) void linear_nt_kernel(NTArgs a, int ntm, in
         float* As = smem + buf * BUF;
         float* Ws = As + BM * LDP;
 #pragma unroll
-        for (int i = 0; i < NA; ++i) *reinterpret_cast<f4*>(As + (i * 32 + rbase) * LDP + c4 * 4) = ra[i];
+        for (int i = 0; i < NA; ++i)
+            *reinterpret_cast<f4*>(As + (i * 32 + rbase) * LDP + c4 * 4) =
+                ((rmask >> i) & 1u) ? ra[i] : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < NW; ++j) *reinterpret_cast<f4*>(Ws + (j * 32 + rbase) * LDP + c4 * 4) = rw[j];
     };
@@ -220,6 +222,10 @@ __global__ __launch_bounds__(256, 2) void linear_nt_kernel(NTArgs a, int ntm, in
                 set_w(has_next_tile ? ntn_ * BN : n0);
             }
             load_chunk(kc);
+            // keep the staging loads here, ahead of the MFMAs: left alone, the scheduler
+            // sinks them to the end of the block (register reuse) and the chunk then
+            // waits on a full HBM round trip before its ds_write
+            __builtin_amdgcn_sched_barrier(0);
 
             const float* Ab = smem + cur * BUF + (wr * WM + li) * LDP + lh * 16;
             const float* Bb = smem + cur * BUF + BM * LDP + (wc * WN + li) * LDP + lh * 16;
@@ -369,24 +375,26 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_kernel(TNArgs a) {
     float dbacc = 0.f;
 
     f4 ry[4], rx[4];
+    unsigned mmask = 0;  // staged rows inside the slice (zero-fill applied at the LDS write)
     auto gload = [&](int mc) __attribute__((always_inline)) {
+        mmask = 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int m = mc + rr + 8 * i;
             const bool mok = m < mend;
+            mmask |= (mok ? 1u : 0u) << i;
             const unsigned mm = (unsigned)(mok ? m : mbeg);
-            const f4 vy = *reinterpret_cast<const f4*>(a.dY + (int64_t)mm * a.lddy + (ny_ok ? ny : 0));
-            const f4 vx =
-                *reinterpret_cast<const f4*>(xptr + (int64_t)(xrd == 1u ? mm : mm / xrd) * xld + (x_ok ? xoff : 0));
-            ry[i] = (mok && ny_ok) ? vy : f4{0.f, 0.f, 0.f, 0.f};
-            rx[i] = (mok && x_ok) ? vx : f4{0.f, 0.f, 0.f, 0.f};
+            ry[i] = *reinterpret_cast<const f4*>(a.dY + (int64_t)mm * a.lddy + (ny_ok ? ny : 0));
+            rx[i] = *reinterpret_cast<const f4*>(xptr + (int64_t)(xrd == 1u ? mm : mm / xrd) * xld + (x_ok ? xoff : 0));
         }
     };
     auto sstore = [&](int buf) __attribute__((always_inline)) {
+        const f4 z = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            *reinterpret_cast<f4*>(&sY[buf][rr + 8 * i][c4 * 4]) = ry[i];
-            *reinterpret_cast<f4*>(&sX[buf][rr + 8 * i][c4 * 4]) = rx[i];
+            const bool mok = (mmask >> i) & 1u;
+            *reinterpret_cast<f4*>(&sY[buf][rr + 8 * i][c4 * 4]) = (mok && ny_ok) ? ry[i] : z;
+            *reinterpret_cast<f4*>(&sX[buf][rr + 8 * i][c4 * 4]) = (mok && x_ok) ? rx[i] : z;
         }
     };
 
@@ -398,6 +406,7 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_kernel(TNArgs a) {
         for (int mc = mbeg; mc < mend; mc += TBM) {
             const bool has_next = mc + TBM < mend;
             gload(has_next ? mc + TBM : mc);
+            __builtin_amdgcn_sched_barrier(0);  // issue the next stage's loads before the MFMAs
 #pragma unroll
             for (int s = 0; s < 16; ++s) {
                 const int mr = lh * 16 + s;
