@@ -143,11 +143,12 @@ def main():
 
     import nerf_amd
     from nerf_amd import kernels as K
+    from nerf_amd.ddp import GradAllReduce
     nerf_amd._lib.load()
 
     ren = build_model(device)
     opt = ren.configure_optimizers()["optimizer"]
-    params = [p for p in ren.parameters() if p.requires_grad]
+    allreduce = GradAllReduce(ren.parameters())
     o, d, pw, target = synthetic_batch(RAYS, 1000 + rank, device)
     torch.manual_seed(1234 + rank)
 
@@ -156,12 +157,7 @@ def main():
         loss, _ = ren.training_loss(o, d, pw, target)
         loss.backward()
         if dist is not None:
-            grads = [p.grad for p in params]
-            flat = torch._utils._flatten_dense_tensors(grads)
-            dist.all_reduce(flat)
-            flat.div_(world)
-            for g, s in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
-                g.copy_(s)
+            allreduce()          # one RCCL all-reduce of the flat gradient bucket
         opt.step()
         return loss
 
