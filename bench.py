@@ -32,6 +32,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "nerf-experiments_amd"))
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+BF16_MFMA_PEAK_TFLOPS = 2516.6  # MI355X_MICROARCH.md: ~2.5 PF dense (32x32x16 bf16, 32 cycles, 2.4 GHz)
+X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3.0   # 3 bf16 MFMAs per fp32-accurate product
 HBM_PEAK_GBS = 8000.0
 
 RAYS = 4096
@@ -128,7 +130,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--matmul-precision", default="high", choices=("highest", "high", "medium"),
+                    help="torch.set_float32_matmul_precision for the MLP GEMMs: highest = fp32 MFMA, "
+                         "high/medium = 3 x bf16 split MFMA (fp32-accurate to ~2^-16); the reference's "
+                         "naive-to-vanilla run uses medium + 16-mixed (main.py:53)")
     args = ap.parse_args()
+    torch.set_float32_matmul_precision(args.matmul_precision)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -187,13 +194,17 @@ def main():
     samples_total = RAYS * SAMPLES * world * args.steps
     value = samples_total / elapsed
     ks = timer.summary()
-    nt = ks.get("linear_nt", {"launches": 0, "flops": 0.0, "ms": 0.0})
+    from nerf_amd.mlp import matmul_precision
+    x3 = matmul_precision() == "x3"
+    nt_name = "linear_nt_x3" if x3 else "linear_nt"
+    peak = X3_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
+    nt = ks.get(nt_name, {"launches": 0, "flops": 0.0, "ms": 0.0})
     nt_avg_ms = nt["ms"] / max(nt["launches"], 1)
     nt_avg_flops = nt["flops"] / max(nt["launches"], 1)
     achieved = (nt_avg_flops / (nt_avg_ms * 1e-3)) / 1e12 if nt_avg_ms > 0 else 0.0
 
     traffic = None
-    tfile = os.path.join(ROOT, "profiles", "traffic_linear_nt.json")
+    tfile = os.path.join(ROOT, "profiles", f"traffic_{nt_name}.json")
     if os.path.exists(tfile):
         with open(tfile) as f:
             traffic = json.load(f).get("bytes_per_launch")
@@ -211,14 +222,18 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
+            "matmul": ("3xbf16 split MFMA (hi*hi+hi*lo+lo*hi, fp32 accumulate)" if x3 else "fp32 MFMA"),
+            "matmul_precision": args.matmul_precision,
             "data": "synthetic Lego-shaped rays/targets, random-init weights (torch.manual_seed(0))",
             "config": {"workload": "naive-to-vanilla NeRF training step, Lego 400x400, 4096 rays x 64 samples "
                                    "per GPU (BASELINE.json configs[1])",
                        "rays_per_gpu": RAYS, "samples_per_ray": SAMPLES, "global_rays": RAYS * world,
                        "parallelism": f"ray-batch dp{world}" + (" (RCCL all-reduce)" if world > 1 else "")},
-            "roofline": {"kernel": "linear_nt (fp32 MFMA 32x32x2: forward + input-gradient GEMMs)",
-                         "bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,
+            "roofline": {"kernel": (f"{nt_name} (" + ("3 x bf16 MFMA 32x32x16; peak = bf16 dense / 3"
+                                                       if x3 else "fp32 MFMA 32x32x2")
+                                    + ": forward + input-gradient GEMMs; achieved in algorithmic fp32 GEMM flops)"),
+                         "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak, "traffic": traffic,
                          "avg_launch_us": nt_avg_ms * 1e3, "avg_flops_per_launch": nt_avg_flops,
                          "launches_per_step": nt["launches"] / args.steps},
             "kernels": {k: {"launches_per_step": v["launches"] / args.steps, "ms_per_step": v["ms"] / args.steps,

@@ -219,6 +219,28 @@ int nerf_linear_wgrad_reduce(int64_t M, int32_t N, int32_t K, int32_t n_valid,
 int nerf_pack_weight(const float* W, int32_t N, int32_t K_orig, const int32_t* col_map,
                      int32_t Kp, float* Wp, float* Wt, int32_t ldwt, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Split-precision variants ("3 x bf16"): same contracts as the fp32 entry points,
+ * each product formed as lo*hi + hi*lo + hi*hi on bf16 MFMA with fp32
+ * accumulation (x = hi + lo, hi = bf16(x), lo = bf16(x - hi)): ~2^-17 relative
+ * error per product at 5.3x the fp32 MFMA rate.  Selected by the host when
+ * torch.get_float32_matmul_precision() != "highest" (the reference sets "high",
+ * barf/run_barf.py:101).  N >= 33 for nerf_linear_fwd_x3 (narrower layers use the
+ * fp32 kernel).  Weights are pre-split by nerf_pack_weight_x3 into bf16 planes of
+ * the fp32 packed layouts; ldw % 8 == 0.  nerf_linear_wgrad_x3 writes the same
+ * workspace as nerf_linear_wgrad (reduce with nerf_linear_wgrad_reduce).
+ * ------------------------------------------------------------------------- */
+int nerf_linear_fwd_x3(const nerf_seg* segs, int32_t n_segs, int64_t M,
+                       const void* W_hi, const void* W_lo, int32_t ldw, int32_t N, const float* bias,
+                       float* out, int64_t ldo, int32_t epilogue,
+                       const float* aux, int64_t ld_aux, void* stream);
+int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N,
+                         const nerf_seg* segs, int32_t n_segs, int64_t M,
+                         void* workspace, size_t workspace_bytes, void* stream);
+int nerf_pack_weight_x3(const float* W, int32_t N, int32_t K_orig, const int32_t* col_map,
+                        int32_t Kp, void* Wp_hi, void* Wp_lo, void* Wt_hi, void* Wt_lo,
+                        int32_t ldwt, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -557,6 +557,9 @@ __global__ void pack_weight_kernel(const float* __restrict__ W, int N, int K_ori
 
 }  // namespace
 
+// shared with linear_x3.hip (same slab layout and reduce)
+int nerf_wgrad_choose_splits(int64_t M, int tiles) { return choose_splits(M, tiles); }
+
 extern "C" int nerf_linear_fwd(const nerf_seg* segs, int32_t n_segs, int64_t M, const float* W, int32_t ldw, int32_t N,
                                const float* bias, float* out, int64_t ldo, int32_t epilogue, const float* aux,
                                int64_t ld_aux, void* stream) {

@@ -26,6 +26,21 @@ from . import kernels as K
 from ._lib import NERF_EPI_ACCUM, NERF_EPI_BIAS, NERF_EPI_MASK, NERF_EPI_RELU
 
 
+def matmul_precision() -> str:
+    """"fp32" (exact fp32 MFMA) or "x3" (3 x bf16 split MFMA, ~2^-17 per product).
+
+    Follows torch.get_float32_matmul_precision(), the knob the reference itself sets
+    (barf/run_barf.py:101 "high", naive-to-vanilla/main.py:53 "medium"): "highest" ->
+    exact fp32; "high"/"medium" -> split precision, which is ~64x more accurate than
+    the TF32/bf16 those settings select on the reference's hardware."""
+    if PRECISION_OVERRIDE is not None:
+        return PRECISION_OVERRIDE
+    return "fp32" if torch.get_float32_matmul_precision() == "highest" else "x3"
+
+
+PRECISION_OVERRIDE: str | None = None
+
+
 @dataclass
 class Source:
     kind: str          # "pos" | "dir" | "act"
@@ -58,6 +73,11 @@ class LayerPlan:
     Wp: torch.Tensor | None = None
     Wt: torch.Tensor | None = None
     packed_version: tuple = ()
+    Wph: torch.Tensor | None = None
+    Wpl: torch.Tensor | None = None
+    Wth: torch.Tensor | None = None
+    Wtl: torch.Tensor | None = None
+    packed_version_x3: tuple = ()
 
     def finalize(self, device):
         self.N = self.module.out_features
@@ -83,13 +103,37 @@ class LayerPlan:
         self.Wp = torch.empty(K.pad128(self.N), self.Kp, device=device, dtype=torch.float32)
         self.Wt = torch.empty(K.pad128(self.Kp) + 128, self.ldwt, device=device, dtype=torch.float32)
         self.packed_version = ()
+        self.Wph = self.Wpl = self.Wth = self.Wtl = None
+        self.packed_version_x3 = ()
 
-    def pack(self):
+    def pack(self, precision: str = "fp32"):
         w = self.module.weight
         ver = (w._version, w.data_ptr())
         if ver != self.packed_version:
             K.pack_weight(w.detach().contiguous(), self.col_map, self.Kp, self.Wp, self.Wt, self.ldwt)
             self.packed_version = ver
+        if precision == "x3" and ver != self.packed_version_x3:
+            if self.Wph is None:
+                dev = self.Wp.device
+                self.Wph = torch.empty(self.Wp.shape, device=dev, dtype=torch.bfloat16)
+                self.Wpl = torch.empty_like(self.Wph)
+                self.Wth = torch.empty(self.Wt.shape, device=dev, dtype=torch.bfloat16)
+                self.Wtl = torch.empty_like(self.Wth)
+            K.pack_weight_x3(w.detach().contiguous(), self.col_map, self.Kp, self.Wph, self.Wpl, self.Wth, self.Wtl,
+                             self.ldwt)
+            self.packed_version_x3 = ver
+
+    def gemm(self, precision: str, segs, M: int, transpose: bool, N: int, bias, out, epi, aux=None,
+             row_offset: int = 0):
+        """Forward (W) or input-gradient (W^T) GEMM in the requested precision; layers
+        narrower than 33 outputs always use the fp32 kernel (their 128 x 32 tile)."""
+        if precision == "x3" and N > 32:
+            wh, wl = (self.Wth, self.Wtl) if transpose else (self.Wph, self.Wpl)
+            K.linear_fwd_x3(segs, M, wh, wl, self.ldwt if transpose else self.Kp, N, bias, out, epi, aux=aux,
+                            w_row_offset=row_offset)
+        else:
+            K.linear_fwd(segs, M, self.Wt if transpose else self.Wp, self.ldwt if transpose else self.Kp, N, bias,
+                         out, epi, aux=aux, w_row_offset=row_offset)
 
 
 class MLPPlan:
@@ -130,17 +174,19 @@ class MLPFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, plan: MLPPlan, M: int, pos: torch.Tensor, dirs: torch.Tensor | None, dir_rd: int, *params):
         plan.to_device(pos.device)
+        prec = matmul_precision()
         acts: list[torch.Tensor] = []
         for lp in plan.layers:
-            lp.pack()
+            lp.pack(prec)
             segs = []
             for s in lp.sources:
                 t, rd = _src_tensor(s, pos, dirs, acts, dir_rd)
                 segs.append((t, s.k_seg, rd))
             out = torch.empty(M, lp.out_ld, device=pos.device, dtype=torch.float32)
             epi = NERF_EPI_BIAS | (NERF_EPI_RELU if lp.relu else 0)
-            K.linear_fwd(segs, M, lp.Wp, lp.Kp, lp.N, lp.module.bias, out, epi)
+            lp.gemm(prec, segs, M, False, lp.N, lp.module.bias, out, epi)
             acts.append(out)
+        ctx.prec = prec
         ctx.plan = plan
         ctx.M = M
         ctx.dir_rd = dir_rd
@@ -194,7 +240,10 @@ class MLPFunction(torch.autograd.Function):
             N4 = (lp.N + 3) // 4 * 4
             gW = torch.empty_like(w)
             gb = torch.empty_like(lp.module.bias)
-            K.linear_wgrad(dZ, N4, segs, M, workspace)
+            if ctx.prec == "x3":
+                K.linear_wgrad_x3(dZ, N4, segs, M, workspace)
+            else:
+                K.linear_wgrad(dZ, N4, segs, M, workspace)
             K.linear_wgrad_reduce(M, N4, lp.Kp, lp.N, workspace, lp.col_map, gW, gb)
             param_grads[2 * li] = gW
             param_grads[2 * li + 1] = gb
@@ -216,22 +265,21 @@ class MLPFunction(torch.autograd.Function):
                             dY[j] = torch.empty(M, prod.out_ld, device=dev, dtype=torch.float32)
                     else:
                         epi |= NERF_EPI_ACCUM
-                    K.linear_fwd(a_seg, M, lp.Wt, lp.ldwt, s.k_valid, None, dY[j], epi, aux=aux,
-                                 w_row_offset=koff)
+                    lp.gemm(ctx.prec, a_seg, M, True, s.k_valid, None, dY[j], epi, aux=aux, row_offset=koff)
                 elif s.kind == "pos" and need_pos:
                     if dpos is None:
                         dpos = torch.empty(M, s.k_pad, device=dev, dtype=torch.float32)
                         epi = 0
                     else:
                         epi = NERF_EPI_ACCUM
-                    K.linear_fwd(a_seg, M, lp.Wt, lp.ldwt, s.k_pad, None, dpos, epi, w_row_offset=koff)
+                    lp.gemm(ctx.prec, a_seg, M, True, s.k_pad, None, dpos, epi, row_offset=koff)
                 elif s.kind == "dir" and need_dir:
                     if ddir is None:
                         ddir = torch.empty(M, s.k_pad, device=dev, dtype=torch.float32)
                         epi = 0
                     else:
                         epi = NERF_EPI_ACCUM
-                    K.linear_fwd(a_seg, M, lp.Wt, lp.ldwt, s.k_pad, None, ddir, epi, w_row_offset=koff)
+                    lp.gemm(ctx.prec, a_seg, M, True, s.k_pad, None, ddir, epi, row_offset=koff)
         if ddir is not None and ctx.dir_rd > 1:
             ddir = ddir.view(-1, ctx.dir_rd, ddir.shape[1]).sum(dim=1)
         return (None, None, dpos, ddir, None, *param_grads)

@@ -274,6 +274,92 @@ def test_linear_fwd_wgrad(M, N, ks, rd):
     np.testing.assert_allclose(db.cpu().numpy(), dY[:, :N].sum(0).numpy(), atol=2e-4, rtol=1e-4)
 
 
+def _split_bf16(W):
+    hi = W.bfloat16()
+    return hi, (W - hi.float()).bfloat16()
+
+
+@pytest.mark.parametrize("M,N,ks,rd", [(1000, 256, (256, 64), (1, 1)), (777, 257, (256,), (1,)),
+                                       (4096, 128, (256, 32), (1, 64)), (300, 4, (128,), (1,)),
+                                       (129, 300, (32, 32, 64), (1, 3, 1)), (1000, 128, (4,), (1,)),
+                                       (333, 20, (260, 12), (1, 7)), (70000, 256, (256,), (1,))])
+def test_linear_x3_fwd_wgrad(M, N, ks, rd):
+    """3 x bf16 split-precision GEMMs (hi*hi + hi*lo + lo*hi, fp32 accumulate).
+
+    Tolerance: each product misses lo_x*lo_w and the residual rounding of lo, both
+    <= 2^-16 |x||w|, so |err| <= 2^-15 * (|X| @ |W|^T) bounds the result elementwise."""
+    from nerf_amd import kernels as K
+    from nerf_amd._lib import NERF_EPI_ACCUM, NERF_EPI_BIAS, NERF_EPI_MASK, NERF_EPI_RELU
+    torch.manual_seed(M + N + 1)
+    segs_cpu = [torch.randn((M + r - 1) // r, k) for k, r in zip(ks, rd)]
+    Kv = sum(ks)
+    Kp = sum(K.pad32(k) for k in ks)
+    W = torch.randn(N, Kv) / math.sqrt(Kv)
+    b = torch.randn(N)
+    X = torch.cat([s.repeat_interleave(r, dim=0)[:M] for s, r in zip(segs_cpu, rd)], dim=1)
+    cm = []
+    off = 0
+    for k in ks:
+        cm += [off + j for j in range(k)] + [-1] * (K.pad32(k) - k)
+        off += k
+    cmd = torch.tensor(cm, dtype=torch.int32, device=DEV)
+    ldwt = K.pad32(N)
+    Wph = torch.empty(K.pad128(N), Kp, dtype=torch.bfloat16, device=DEV)
+    Wpl = torch.empty_like(Wph)
+    Wth = torch.empty(K.pad128(Kp) + 128, ldwt, dtype=torch.bfloat16, device=DEV)
+    Wtl = torch.empty_like(Wth)
+    K.pack_weight_x3(W.to(DEV), cmd, Kp, Wph, Wpl, Wth, Wtl, ldwt)
+    # packing is bit-exact against torch's round-to-nearest-even split
+    Wp = torch.zeros(K.pad128(N), Kp)
+    for j, c in enumerate(cm):
+        if c >= 0:
+            Wp[:N, j] = W[:, c]
+    h, lo = _split_bf16(Wp)
+    assert torch.equal(Wph.cpu().view(torch.int16), h.view(torch.int16))
+    assert torch.equal(Wpl.cpu().view(torch.int16), lo.view(torch.int16))
+    ht, lt = _split_bf16(Wp.T.contiguous())
+    assert torch.equal(Wth.cpu()[:Kp, :N].view(torch.int16), ht[:, :N].view(torch.int16))
+    assert torch.equal(Wtl.cpu()[:Kp, :N].view(torch.int16), lt[:, :N].view(torch.int16))
+    assert not Wth.cpu()[Kp:].float().abs().any() and not Wth.cpu()[:, N:].float().abs().any()
+
+    segs = [(s.to(DEV), k, r) for s, k, r in zip(segs_cpu, ks, rd)]
+    ldo = (N + 3) // 4 * 4
+    Xd, Wd = X.double(), W.double()
+    bound = 2.0 ** -15 * (Xd.abs() @ Wd.abs().T) + 1e-6
+    out = torch.empty(M, ldo, device=DEV)
+    K.linear_fwd_x3(segs, M, Wph, Wpl, Kp, N, b.to(DEV), out, NERF_EPI_BIAS | NERF_EPI_RELU)
+    ref = torch.relu(Xd @ Wd.T + b.double())
+    err = (out[:, :N].cpu().double() - ref).abs()
+    assert (err <= bound + 1e-6).all(), float((err - bound).max())
+    # ReLU-mask + accumulate epilogue
+    aux = torch.randn(M, ldo)
+    out2 = torch.randn(M, ldo)
+    o2 = out2.clone().to(DEV)
+    K.linear_fwd_x3(segs, M, Wph, Wpl, Kp, N, None, o2, NERF_EPI_MASK | NERF_EPI_ACCUM, aux=aux.to(DEV))
+    ref2 = out2[:, :N].double() + (Xd @ Wd.T) * (aux[:, :N] > 0)
+    err = (o2[:, :N].cpu().double() - ref2).abs()
+    assert (err <= bound + 1e-6).all(), float((err - bound).max())
+    # transposed (input-gradient) direction through Wt planes: dX = dY @ W
+    dY = torch.randn(M, ldo)
+    dY[:, N:] = 0
+    dX = torch.empty(M, Kp, device=DEV)
+    K.linear_fwd_x3([(dY.to(DEV), ldo, 1)], M, Wth, Wtl, ldwt, Kp, None, dX, 0)
+    refx = dY[:, :N].double() @ Wp[:N].double()
+    bx = 2.0 ** -15 * (dY[:, :N].double().abs() @ Wp[:N].double().abs()) + 1e-6
+    assert ((dX.cpu().double() - refx).abs() <= bx).all()
+    # weight gradient, scattered through the column map (fp64 split reduction)
+    N4 = ldo
+    ws = torch.empty((K.linear_wgrad_workspace_bytes(M, N4, Kp) + 3) // 4, device=DEV)
+    K.linear_wgrad_x3(dY.to(DEV), N4, segs, M, ws)
+    dW = torch.empty(N, Kv, device=DEV)
+    db = torch.empty(N, device=DEV)
+    K.linear_wgrad_reduce(M, N4, Kp, N, ws, cmd, dW, db)
+    refw = dY[:, :N].T.double() @ Xd
+    bw = 2.0 ** -15 * (dY[:, :N].T.double().abs() @ Xd.abs()) + 1e-6
+    assert ((dW.cpu().double() - refw).abs() <= bw).all()
+    np.testing.assert_allclose(db.cpu().numpy(), dY[:, :N].sum(0).numpy(), atol=2e-4, rtol=1e-4)
+
+
 # ----------------------------------------------------------------------------- field MLP
 def _make_models():
     from nerf_amd import BarfPositionalEncoding, FourierFeatures, NerfModel
@@ -288,8 +374,17 @@ def _make_models():
     return {"barf": barf, "n2v": n2v, "small": small}
 
 
+@pytest.fixture(params=["highest", "high"])
+def matmul_precision(request):
+    """Both MLP GEMM precisions: "highest" -> fp32 MFMA, "high" -> 3 x bf16 split MFMA."""
+    old = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision(request.param)
+    yield request.param
+    torch.set_float32_matmul_precision(old)
+
+
 @pytest.mark.parametrize("name", ["barf", "n2v", "small"])
-def test_nerf_model_golden(golden, name):
+def test_nerf_model_golden(golden, name, matmul_precision):
     g = golden("model")
     m = _make_models()[name]
     # identical initial weights to the reference's th.manual_seed(0) construction
@@ -304,18 +399,23 @@ def test_nerf_model_golden(golden, name):
     np.testing.assert_allclose(dens.detach().cpu().numpy(), g[f"{name}.density"], atol=1e-4, rtol=1e-4)
     np.testing.assert_allclose(rgb.detach().cpu().numpy(), g[f"{name}.rgb"], atol=1e-4, rtol=1e-4)
     ((dens * g2d(g[f"{name}.gd"])).sum() + (rgb * g2d(g[f"{name}.gc"])).sum()).backward()
-    np.testing.assert_allclose(pos.grad.cpu().numpy(), g[f"{name}.dpos"], atol=1e-3, rtol=1e-3)
+    # Gradients of the deep first segment pass through ~10 ReLU masks whose pre-activations
+    # sit arbitrarily close to zero, so they are ill-conditioned: in fp64 a 1e-5 relative
+    # perturbation of the weights moves barf's model_segments.0.* gradients by up to 6e-3 of
+    # their max.  The 3 x bf16 GEMMs (~2^-16 per product) get a correspondingly looser bound.
+    tol = 1e-4 if matmul_precision == "highest" else 2e-3
+    np.testing.assert_allclose(pos.grad.cpu().numpy(), g[f"{name}.dpos"], atol=10 * tol, rtol=10 * tol)
     for k, prm in m.named_parameters():
         s = g[f"{name}.gradsum.{k}"]
         gs = prm.grad.double()
-        assert abs(gs.abs().sum().item() - s[1]) <= 1e-4 * s[1] + 1e-6, k
+        assert abs(gs.abs().sum().item() - s[1]) <= tol * s[1] + 1e-6, k
         key = f"{name}.grad.{k}"
         if key in g:
-            np.testing.assert_allclose(prm.grad.cpu().numpy(), g[key], atol=1e-4 * max(1.0, np.abs(g[key]).max()),
-                                       rtol=1e-3)
+            np.testing.assert_allclose(prm.grad.cpu().numpy(), g[key], atol=tol * max(1.0, np.abs(g[key]).max()),
+                                       rtol=10 * tol)
 
 
-def test_compute_color_and_forward_golden(golden):
+def test_compute_color_and_forward_golden(golden, matmul_precision):
     """_compute_color with explicit t and the coarse+fine forward with injected coarse t."""
     from nerf_amd import BarfPositionalEncoding, NerfInterpolation, NerfModel
     g = golden("color")

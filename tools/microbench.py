@@ -42,7 +42,7 @@ def time_it(fn, reps=20, warm=3):
     return ts[len(ts) // 2]
 
 
-def bench_linear(M, N, ks, rd, epi=NERF_EPI_BIAS | NERF_EPI_RELU):
+def bench_linear(M, N, ks, rd, epi=NERF_EPI_BIAS | NERF_EPI_RELU, x3=False):
     segs = [(torch.randn((M + r - 1) // r, k, device=DEV), k, r) for k, r in zip(ks, rd)]
     Kt = sum(K.pad32(k) for k in ks)
     W = torch.randn(K.pad128(N), Kt, device=DEV) * 0.05
@@ -50,8 +50,16 @@ def bench_linear(M, N, ks, rd, epi=NERF_EPI_BIAS | NERF_EPI_RELU):
     ldo = (N + 3) // 4 * 4
     out = torch.empty(M, ldo, device=DEV)
     aux = torch.randn(M, ldo, device=DEV) if epi & NERF_EPI_MASK else None
-    ms = time_it(lambda: K.linear_fwd(segs, M, W, Kt, N, b, out, epi, aux=aux))
     fl = 2.0 * M * N * sum(ks)
+    if x3:
+        Wh = W.bfloat16()
+        Wl = (W - Wh.float()).bfloat16()
+        ms = time_it(lambda: K.linear_fwd_x3(segs, M, Wh, Wl, Kt, N, b, out, epi, aux=aux))
+        r = {"kernel": "linear_nt_x3", "M": M, "N": N, "K": ks, "ms": ms, "tflops": fl / ms / 1e9}
+        ms_np = time_it(lambda: K.linear_fwd_x3(segs, M, Wh, Wl, Kt, N, b, out, epi | NERF_EPI_NO_PERSIST, aux=aux))
+        r["tflops_no_persist"] = fl / ms_np / 1e9
+        return r
+    ms = time_it(lambda: K.linear_fwd(segs, M, W, Kt, N, b, out, epi, aux=aux))
     r = {"kernel": "linear_nt", "M": M, "N": N, "K": ks, "ms": ms, "tflops": fl / ms / 1e9}
     # A/B in the same process: one tile per workgroup (no persistence)
     ms_np = time_it(lambda: K.linear_fwd(segs, M, W, Kt, N, b, out, epi | NERF_EPI_NO_PERSIST, aux=aux))
@@ -59,7 +67,7 @@ def bench_linear(M, N, ks, rd, epi=NERF_EPI_BIAS | NERF_EPI_RELU):
     return r
 
 
-def bench_wgrad(M, N, ks, rd):
+def bench_wgrad(M, N, ks, rd, x3=False):
     segs = [(torch.randn((M + r - 1) // r, k, device=DEV), k, r) for k, r in zip(ks, rd)]
     Kt = sum(K.pad32(k) for k in ks)
     N4 = (N + 3) // 4 * 4
@@ -68,10 +76,11 @@ def bench_wgrad(M, N, ks, rd):
     dW = torch.empty(N, Kt, device=DEV)
     db = torch.empty(N, device=DEV)
     cm = torch.arange(Kt, dtype=torch.int32, device=DEV)
-    ms1 = time_it(lambda: K.linear_wgrad(dY, N4, segs, M, ws))
+    wg = K.linear_wgrad_x3 if x3 else K.linear_wgrad
+    ms1 = time_it(lambda: wg(dY, N4, segs, M, ws))
     ms2 = time_it(lambda: K.linear_wgrad_reduce(M, N4, Kt, N, ws, cm, dW, db))
     fl = 2.0 * M * N * sum(ks)
-    return {"kernel": "linear_wgrad", "M": M, "N": N, "K": ks, "ms": ms1, "reduce_ms": ms2,
+    return {"kernel": "linear_wgrad_x3" if x3 else "linear_wgrad", "M": M, "N": N, "K": ks, "ms": ms1, "reduce_ms": ms2,
             "tflops": fl / ms1 / 1e9}
 
 
@@ -120,24 +129,28 @@ def main():
     if args.only:
         fn = {"nt256": lambda: bench_linear(M, 256, (256,), (1,)),
               "nt256mask": lambda: bench_linear(M, 256, (256,), (1,), NERF_EPI_MASK),
-              "wgrad256": lambda: bench_wgrad(M, 256, (256,), (1,))}[args.only]
+              "wgrad256": lambda: bench_wgrad(M, 256, (256,), (1,)),
+              "nt256x3": lambda: bench_linear(M, 256, (256,), (1,), x3=True),
+              "wgrad256x3": lambda: bench_wgrad(M, 256, (256,), (1,), x3=True)}[args.only]
         print(json.dumps(fn()))
         return
-    # forward layers of the bench model
-    res.append(bench_linear(M, 256, (64,), (1,)))
-    res.append(bench_linear(M, 256, (256,), (1,)))
-    res.append(bench_linear(M, 256, (256, 64), (1, 1)))
-    res.append(bench_linear(M, 128, (256, 32), (1, 64)))
-    res.append(bench_linear(M, 4, (128,), (1,), NERF_EPI_BIAS))
-    # input-gradient layers
-    res.append(bench_linear(M, 256, (256,), (1,), NERF_EPI_MASK))
-    res.append(bench_linear(M, 128, (4,), (1,), NERF_EPI_MASK))
-    res.append(bench_linear(M, 256, (128,), (1,), 0))
-    # weight gradients
-    res.append(bench_wgrad(M, 256, (256,), (1,)))
-    res.append(bench_wgrad(M, 256, (256, 64), (1, 1)))
-    res.append(bench_wgrad(M, 128, (256, 32), (1, 64)))
-    res.append(bench_wgrad(M, 4, (128,), (1,)))
+    for x3 in (False, True):
+        # forward layers of the bench model
+        res.append(bench_linear(M, 256, (64,), (1,), x3=x3))
+        res.append(bench_linear(M, 256, (256,), (1,), x3=x3))
+        res.append(bench_linear(M, 256, (256, 64), (1, 1), x3=x3))
+        res.append(bench_linear(M, 128, (256, 32), (1, 64), x3=x3))
+        if not x3:
+            res.append(bench_linear(M, 4, (128,), (1,), NERF_EPI_BIAS))
+        # input-gradient layers
+        res.append(bench_linear(M, 256, (256,), (1,), NERF_EPI_MASK, x3=x3))
+        res.append(bench_linear(M, 128, (4,), (1,), NERF_EPI_MASK, x3=x3))
+        res.append(bench_linear(M, 256, (128,), (1,), 0, x3=x3))
+        # weight gradients
+        res.append(bench_wgrad(M, 256, (256,), (1,), x3=x3))
+        res.append(bench_wgrad(M, 256, (256, 64), (1, 1), x3=x3))
+        res.append(bench_wgrad(M, 128, (256, 32), (1, 64), x3=x3))
+        res.append(bench_wgrad(M, 4, (128,), (1,), x3=x3))
     res.append(bench_composite(4096, 64))
     res.append(bench_composite(65536, 128))
     res.append(bench_encode(4096, 64))
