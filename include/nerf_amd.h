@@ -183,6 +183,7 @@ typedef struct nerf_seg {
 #define NERF_EPI_MASK  4   /* * (aux[m, n] > 0): ReLU backward */
 #define NERF_EPI_ACCUM 8   /* out += result */
 #define NERF_EPI_NO_PERSIST 256  /* tuning: one tile per workgroup instead of a persistent grid */
+#define NERF_EPI_NARROW_TILE 512 /* tuning: force the 128-column tile of the split-precision kernel for N > 128 */
 
 /* out[m, n] = epi( sum_k A[m, k] * W[n, k] ),  m < M, n < N.
  * W: packed row-major [ceil(N/128)*128][ldw], ldw = sum_j kp_j (zero padding
@@ -225,21 +226,24 @@ int nerf_pack_weight(const float* W, int32_t N, int32_t K_orig, const int32_t* c
  * accumulation (x = hi + lo, hi = bf16(x), lo = bf16(x - hi)): ~2^-17 relative
  * error per product at 5.3x the fp32 MFMA rate.  Selected by the host when
  * torch.get_float32_matmul_precision() != "highest" (the reference sets "high",
- * barf/run_barf.py:101).  N >= 33 for nerf_linear_fwd_x3 (narrower layers use the
- * fp32 kernel).  Weights are pre-split by nerf_pack_weight_x3 into bf16 planes of
- * the fp32 packed layouts; ldw % 8 == 0.  nerf_linear_wgrad_x3 writes the same
- * workspace as nerf_linear_wgrad (reduce with nerf_linear_wgrad_reduce).
+ * barf/run_barf.py:101).  Weights are pre-split by nerf_pack_weight_x3 into an
+ * interleaved layout of the fp32 packed matrices: element (r, c) of a [rows][ld]
+ * matrix is stored at Wx[r][c/32][c%32] (hi) and Wx[r][c/32][32 + c%32] (lo), so
+ * every 32-column chunk of a row is 128 contiguous bytes (ld % 32 == 0; Wp_x has
+ * ceil(N/128)*128 rows of ld = Kp, Wt_x has ceil(Kp/128)*128 + 128 rows of ld = ldwt).
+ * 32 < N <= 256 runs a 256-row tile staged by LDS-DMA; other N a 128 x 128 tile.
+ * nerf_linear_wgrad_x3 writes the same workspace as nerf_linear_wgrad (reduce with
+ * nerf_linear_wgrad_reduce).
  * ------------------------------------------------------------------------- */
 int nerf_linear_fwd_x3(const nerf_seg* segs, int32_t n_segs, int64_t M,
-                       const void* W_hi, const void* W_lo, int32_t ldw, int32_t N, const float* bias,
+                       const void* W_x, int32_t ldw, int32_t N, const float* bias,
                        float* out, int64_t ldo, int32_t epilogue,
                        const float* aux, int64_t ld_aux, void* stream);
 int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N,
                          const nerf_seg* segs, int32_t n_segs, int64_t M,
                          void* workspace, size_t workspace_bytes, void* stream);
 int nerf_pack_weight_x3(const float* W, int32_t N, int32_t K_orig, const int32_t* col_map,
-                        int32_t Kp, void* Wp_hi, void* Wp_lo, void* Wt_hi, void* Wt_lo,
-                        int32_t ldwt, void* stream);
+                        int32_t Kp, void* Wp_x, void* Wt_x, int32_t ldwt, void* stream);
 
 #ifdef __cplusplus
 }

@@ -508,9 +508,12 @@ int cu_count() {
     return cached[dev];
 }
 
+// M splits of the weight gradient (a workspace-layout parameter shared by the fp32 and the
+// split-precision kernels and the reduce): enough workgroups for the whole chip even with
+// the 256 x 256 tiles of the split-precision kernel (one workgroup per CU).
 int choose_splits(int64_t M, int tiles) {
-    int64_t target = 512 / (tiles > 0 ? tiles : 1);
-    if (target > 128) target = 128;
+    int64_t target = 1024 / (tiles > 0 ? tiles : 1);
+    if (target > 256) target = 256;
     if (target < 1) target = 1;
     const int64_t max_splits = (M + TBM - 1) / TBM;
     if (target > max_splits) target = max_splits;

@@ -12,11 +12,13 @@
 // packed weights); the weights arrive pre-split (nerf_pack_weight_x3).
 //
 // NT (forward / input gradient): 128 x 128 tile, 4 waves of 64 x 64, K in
-// 32-wide chunks.  A (fp32 in HBM) is split while it is staged into LDS;
-// LDS planes are [row][32 + 8] bf16 (80-byte rows: the 16 rows a ds_read_b128
-// lane group touches hit 16 distinct 16-byte bank slots).  Lane (r, h) of the
-// 32x32x16 MFMA holds row r, k = 8h .. 8h+7 of both operands: one ds_read_b128
-// per plane and block.
+// 32-wide chunks.  A (fp32 in HBM) is split while it is staged into LDS.
+// LDS planes are [row][32] bf16 (64-byte rows, no padding) with the 16-byte
+// slots of each row PAIR permuted (swz below): the 16 rows a ds_read_b128 lane
+// group reads and the 128 contiguous bytes a ds_write_b64 / ds_write_b128 lane
+// group writes (two rows, or one column of 8 rows 4 apart in the transposed TN
+// staging) all land on distinct bank slots.  Lane (r, h) of the 32x32x16 MFMA
+// holds row r, k = 8h .. 8h+7 of both operands: one ds_read_b128 per plane and block.
 //
 // TN (weight gradient): slab[s][n][k] = sum_m dY[m][n] X[m][k]; the sample index
 // is the MFMA reduction dimension, so dY and X are staged TRANSPOSED ([n][m],
@@ -35,7 +37,13 @@ typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 namespace {
 
 constexpr int BK = 32;
-constexpr int LDB = BK + 8;   // bf16 elements per LDS row (80 bytes)
+constexpr int LDB = BK;       // bf16 elements per LDS row (64 bytes)
+
+// bf16 element offset of 16-byte slot `slot` (0..3) of row `row` in a swizzled plane:
+// rows 2p and 2p+1 share a 128-byte line whose 8 slots are XOR-permuted by (row >> 2) & 7.
+__device__ __forceinline__ int swz(int row, int slot) {
+    return (row >> 1) * 64 + ((((row & 1) << 2) | slot) ^ ((row >> 2) & 7)) * 8;
+}
 constexpr int MAX_SEGS = 4;
 
 struct SegList {
@@ -85,7 +93,7 @@ __device__ __forceinline__ bool tile_coords(int tile, int ntm, int ntn, int& tm,
 struct NTArgs {
     SegList A;
     int M;
-    const __bf16* Wh; const __bf16* Wl; int ldw; int N;
+    const __bf16* Wx; int ldw; int N;      // weights, interleaved [row][ldw/32][hi 32 | lo 32]
     const float* bias;
     float* out; int64_t ldo;
     int epi;
@@ -98,7 +106,7 @@ __global__ __launch_bounds__(256, 2) void linear_nt_x3_kernel(NTArgs a, int ntm,
     constexpr int BM = 128, BN = 128;
     constexpr int PL = BM * LDB;                 // one bf16 plane (128 rows)
     constexpr int BUFB = 4 * PL;                 // A hi, A lo, W hi, W lo (bf16 elements)
-    constexpr int LDC = BN + 4;
+    constexpr int LDC = BN;                      // 32-lane row writes / 16-byte row reads: conflict-free
     constexpr int HR = 64;
     static_assert(HR * LDC * 4 <= BUFB * 2, "epilogue half-tile must fit one staging buffer");
     __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUFB];
@@ -142,7 +150,7 @@ __global__ __launch_bounds__(256, 2) void linear_nt_x3_kernel(NTArgs a, int ntm,
     int64_t woff[2];
     auto set_w = [&](int nbase) __attribute__((always_inline)) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) woff[j] = (int64_t)(nbase + j * 64 + wrow) * a.ldw + w8;
+        for (int j = 0; j < 2; ++j) woff[j] = (int64_t)(nbase + j * 64 + wrow) * a.ldw * 2 + w8;
     };
 
     f4 ra[4];
@@ -157,8 +165,8 @@ __global__ __launch_bounds__(256, 2) void linear_nt_x3_kernel(NTArgs a, int ntm,
         for (int i = 0; i < 4; ++i) ra[i] = *reinterpret_cast<const f4*>(sp + aoff[i] + acol);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            rwh[j] = *reinterpret_cast<const u16x8*>(a.Wh + woff[j] + skoff + kc);
-            rwl[j] = *reinterpret_cast<const u16x8*>(a.Wl + woff[j] + skoff + kc);
+            rwh[j] = *reinterpret_cast<const u16x8*>(a.Wx + woff[j] + 2 * (skoff + kc));
+            rwl[j] = *reinterpret_cast<const u16x8*>(a.Wx + woff[j] + 2 * (skoff + kc) + 32);
         }
     };
     auto store_chunk = [&](int buf) __attribute__((always_inline)) {
@@ -171,13 +179,13 @@ __global__ __launch_bounds__(256, 2) void linear_nt_x3_kernel(NTArgs a, int ntm,
             const f4 v = ((rmask >> i) & 1u) ? ra[i] : f4{0.f, 0.f, 0.f, 0.f};
             bf16x4 h, l;
             split4(v, h, l);
-            const int o = (i * 32 + rbase) * LDB + c4 * 4;
+            const int o = swz(i * 32 + rbase, c4 >> 1) + (c4 & 1) * 4;
             *reinterpret_cast<bf16x4*>(Ah + o) = h;
             *reinterpret_cast<bf16x4*>(Al + o) = l;
         }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const int o = (j * 64 + wrow) * LDB + w8;
+            const int o = swz(j * 64 + wrow, w8 >> 3);
             *reinterpret_cast<u16x8*>(Whp + o) = rwh[j];
             *reinterpret_cast<u16x8*>(Wlp + o) = rwl[j];
         }
@@ -222,17 +230,17 @@ __global__ __launch_bounds__(256, 2) void linear_nt_x3_kernel(NTArgs a, int ntm,
             load_chunk(kc);
             __builtin_amdgcn_sched_barrier(0);
 
-            const __bf16* Ah = smem + cur * BUFB + (wr * 64 + li) * LDB + lh * 8;
-            const __bf16* Wb = smem + cur * BUFB + 2 * PL + (wc * 64 + li) * LDB + lh * 8;
 #pragma unroll
             for (int s = 0; s < BK / 16; ++s) {
+                const __bf16* Ah = smem + cur * BUFB + swz(wr * 64 + li, 2 * s + lh);
+                const __bf16* Wb = smem + cur * BUFB + 2 * PL + swz(wc * 64 + li, 2 * s + lh);
                 bf16x8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
-                    ah[i] = *reinterpret_cast<const bf16x8*>(Ah + i * 32 * LDB + s * 16);
-                    al[i] = *reinterpret_cast<const bf16x8*>(Ah + PL + i * 32 * LDB + s * 16);
-                    bh[i] = *reinterpret_cast<const bf16x8*>(Wb + i * 32 * LDB + s * 16);
-                    bl[i] = *reinterpret_cast<const bf16x8*>(Wb + PL + i * 32 * LDB + s * 16);
+                    ah[i] = *reinterpret_cast<const bf16x8*>(Ah + i * 32 * LDB);
+                    al[i] = *reinterpret_cast<const bf16x8*>(Ah + PL + i * 32 * LDB);
+                    bh[i] = *reinterpret_cast<const bf16x8*>(Wb + i * 32 * LDB);
+                    bl[i] = *reinterpret_cast<const bf16x8*>(Wb + PL + i * 32 * LDB);
                 }
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
@@ -305,6 +313,263 @@ __global__ __launch_bounds__(256, 2) void linear_nt_x3_kernel(NTArgs a, int ntm,
     }
 }
 
+// ------------------------------------------------------------------- NT glds
+// 32 < N <= 256: 256-row x BN-column tile (BN = 128 JN), 8 waves (2 x 4) of 128 x 32 JN,
+// every operand staged by LDS-DMA (global_load_lds_dwordx4: no VGPR round trip, no
+// ds_write pass).  A is staged as raw fp32 and split into bf16 hi/lo as the fragments
+// are read out of LDS; the weights arrive pre-split and interleaved ([row][k/32][hi 32 | lo 32]).
+// Both LDS images have 128-byte rows whose 16-byte slots are XOR-permuted by (row >> 1) & 7;
+// the permutation is applied to the per-lane SOURCE address (the DMA destination is
+// lane-linear) and to the fragment reads, which it makes bank-conflict-free.
+// Two stages: chunk g+1 is in flight while chunk g is multiplied; the in-loop waits are
+// counted (vmcnt(NG)), the barriers raw, so a __syncthreads() never drains the prefetch.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+__device__ __forceinline__ int swz128(int row, int slot) { return row * 128 + ((slot ^ ((row >> 1) & 7)) << 4); }
+
+template <int EPI, int JN>
+__global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int ntiles) {
+    constexpr int BM = 256, BN = 128 * JN;
+    constexpr int ABYTES = BM * 128, WBYTES = BN * 128;
+    constexpr int STAGE = ABYTES + WBYTES;
+    constexpr int QA = BM / 64;                 // A glds instructions per wave per chunk (8 rows each)
+    constexpr int QW = BN / 64;                 // W glds instructions per wave per chunk
+    constexpr int NG = QA + QW;
+    // ONE __shared__ array (a second LDS object makes hipcc drain the DMA before ds_reads)
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 256];
+    SegList* segs_lds = reinterpret_cast<SegList*>(smem + 2 * STAGE);
+    static_assert(sizeof(SegList) <= 256, "segment table");
+
+    const int t = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
+    const int wr = wave >> 2, wc = wave & 3;
+    const int li = lane & 31, lh = lane >> 5;
+    const int lrow = lane >> 3, lphys = lane & 7;        // DMA lane -> (row in 8-row group, physical slot)
+
+    if ((int)blockIdx.x >= ntiles) return;
+    if (t == 0) *segs_lds = a.A;
+    __syncthreads();
+    const int nchunks = a.A.ktot / BK;
+    const int my_tiles = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int total = my_tiles * nchunks;
+
+    // ---- DMA cursor (advanced once per issued chunk)
+    int l_tile = blockIdx.x, l_seg = 0, l_kc = 0, l_c = 0;
+    const float* sp = nullptr;
+    int sk = 0, skp = 0;
+    int64_t aoff[QA];
+    int alog[QA];                 // logical slot each A lane fetches
+    auto set_seg = [&](int s) __attribute__((always_inline)) {
+        sp = segs_lds->ptr[s];
+        const int64_t ld = segs_lds->ld[s];
+        const unsigned rd = (unsigned)segs_lds->row_div[s];
+        sk = segs_lds->k[s];
+        skp = segs_lds->kp[s];
+        const int m0 = l_tile * BM;
+#pragma unroll
+        for (int q = 0; q < QA; ++q) {
+            const int row = (wave * QA + q) * 8 + lrow;
+            int m = m0 + row;
+            m = m < a.M ? m : a.M - 1;                    // rows past M: any valid row (discarded)
+            const unsigned src = (rd == 1u) ? (unsigned)m : (unsigned)m / rd;
+            aoff[q] = (int64_t)src * ld;
+            alog[q] = lphys ^ ((row >> 1) & 7);
+        }
+    };
+    const int nkc = a.ldw / BK;                          // 32-wide chunks per weight row
+    int64_t woff[QW];
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+        const int row = (wave * QW + q) * 8 + lrow;
+        const int n = row < a.N ? row : a.N - 1;         // rows past N: any valid row (discarded)
+        woff[q] = (int64_t)n * nkc * 64 + ((lphys ^ ((row >> 1) & 7)) << 3);
+    }
+    set_seg(0);
+
+    auto issue = [&](int stage) __attribute__((always_inline)) {
+        char* base = smem + stage * STAGE;
+#pragma unroll
+        for (int q = 0; q < QA; ++q) {
+            const int col = l_kc + alog[q] * 4;
+            const float* src = sp + aoff[q] + (col < sk ? col : 0);   // past k: finite data x zero weights
+            __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(base + (wave * QA + q) * 1024), 16, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < QW; ++q) {
+            const __bf16* src = a.Wx + woff[q] + (int64_t)l_c * 64;
+            __builtin_amdgcn_global_load_lds((glb_void_t*)src,
+                                             (lds_void_t*)(base + ABYTES + (wave * QW + q) * 1024), 16, 0, 0);
+        }
+        l_kc += BK;
+        ++l_c;
+        if (l_kc >= skp) {
+            l_kc = 0;
+            ++l_seg;
+            if (l_seg >= a.A.n) {
+                l_seg = 0;
+                l_c = 0;
+                l_tile += gridDim.x;
+            }
+            if (l_tile < ntiles) set_seg(l_seg);
+        }
+    };
+
+    f32x16 acc[4][JN];
+    auto zero_acc = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < JN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    };
+    auto compute = [&](int stage) __attribute__((always_inline)) {
+        const char* Ab = smem + stage * STAGE;
+        const char* Wb = Ab + ABYTES;
+#pragma unroll
+        for (int s = 0; s < BK / 16; ++s) {
+            bf16x8 bh[JN], bl[JN];
+#pragma unroll
+            for (int j = 0; j < JN; ++j) {
+                const int row = wc * (BN / 4) + j * 32 + li;
+                bh[j] = *reinterpret_cast<const bf16x8*>(Wb + swz128(row, 2 * s + lh));
+                bl[j] = *reinterpret_cast<const bf16x8*>(Wb + swz128(row, 4 + 2 * s + lh));
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = wr * 128 + i * 32 + li;
+                const f4 x0 = *reinterpret_cast<const f4*>(Ab + swz128(row, 4 * s + 2 * lh));
+                const f4 x1 = *reinterpret_cast<const f4*>(Ab + swz128(row, 4 * s + 2 * lh + 1));
+                bf16x4 h0, l0, h1, l1;
+                split4(x0, h0, l0);
+                split4(x1, h1, l1);
+                const bf16x8 ah = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+                const bf16x8 al = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+                for (int j = 0; j < JN; ++j) acc[i][j] = mfma_x3(ah, al, bh[j], bl[j], acc[i][j]);
+            }
+        }
+    };
+
+    // bias of this thread's epilogue column quad (N <= BN: one column tile), loaded before
+    // any DMA is in flight
+    constexpr int C4 = BN / 4;                    // float4 columns per row
+    constexpr int RS = 512 / C4;                  // rows per epilogue sweep
+    const int ec4 = t % C4, erow = t / C4;
+    const int en = ec4 * 4;
+    f4 bias4 = f4{0.f, 0.f, 0.f, 0.f};
+    if ((EPI & NERF_EPI_BIAS) && en < a.N) {
+        if (a.vec_ok && en + 4 <= a.N) {
+            bias4 = *reinterpret_cast<const f4*>(a.bias + en);
+        } else {
+            bias4.x = a.bias[en];
+            bias4.y = en + 1 < a.N ? a.bias[en + 1] : 0.f;
+            bias4.z = en + 2 < a.N ? a.bias[en + 2] : 0.f;
+            bias4.w = en + 3 < a.N ? a.bias[en + 3] : 0.f;
+        }
+    }
+    auto barrier = []() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // epilogue through the stage just consumed, 64 rows per pass
+    int c_tile = blockIdx.x, c_chunk = 0;
+    auto epilogue = [&](int free_stage) __attribute__((always_inline)) {
+        float* Cs = reinterpret_cast<float*>(smem + free_stage * STAGE);
+        static_assert(64 * BN * 4 <= STAGE, "epilogue pass must fit one stage");
+        const int tm0 = c_tile * BM;
+        auto pass = [&](int p, const f32x16 (&c)[JN], const f32x16 (&d)[JN]) __attribute__((always_inline)) {
+            if (wr == (p >> 1)) {
+#pragma unroll
+                for (int j = 0; j < JN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+                        Cs[row * BN + wc * (BN / 4) + j * 32 + li] = c[j][r];
+                        Cs[(32 + row) * BN + wc * (BN / 4) + j * 32 + li] = d[j][r];
+                    }
+            }
+            barrier();
+            const bool vec = a.vec_ok && en + 4 <= a.N;
+            // aux / out reads of a batch of rows are issued together (one memory round trip
+            // per batch instead of one per row)
+#pragma unroll
+            for (int qb = 0; qb < 64 / RS; qb += 4) {
+                f4 xa[4], xo[4];
+                if (vec && (EPI & (NERF_EPI_MASK | NERF_EPI_ACCUM))) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        int m = tm0 + 64 * p + erow + RS * (qb + u);
+                        m = m < a.M ? m : a.M - 1;
+                        if (EPI & NERF_EPI_MASK) xa[u] = *reinterpret_cast<const f4*>(a.aux + (int64_t)m * a.ldaux + en);
+                        if (EPI & NERF_EPI_ACCUM) xo[u] = *reinterpret_cast<const f4*>(a.out + (int64_t)m * a.ldo + en);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int row = erow + RS * (qb + u);
+                    const int m = tm0 + 64 * p + row;
+                    if (m >= a.M || en >= a.N) continue;
+                    f4 v = *reinterpret_cast<const f4*>(Cs + row * BN + en);
+                    float* o = a.out + (int64_t)m * a.ldo + en;
+                    if (vec) {
+                        if (EPI & NERF_EPI_BIAS) v += bias4;
+                        if (EPI & NERF_EPI_RELU) {
+                            v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+                        }
+                        if (EPI & NERF_EPI_MASK) {
+                            const f4 x = xa[u];
+                            v.x = x.x > 0.f ? v.x : 0.f; v.y = x.y > 0.f ? v.y : 0.f;
+                            v.z = x.z > 0.f ? v.z : 0.f; v.w = x.w > 0.f ? v.w : 0.f;
+                        }
+                        if (EPI & NERF_EPI_ACCUM) v = xo[u] + v;
+                        *reinterpret_cast<f4*>(o) = v;
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            if (en + e >= a.N) break;
+                            float x = e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
+                            if (EPI & NERF_EPI_BIAS) x = x + (e == 0 ? bias4.x : (e == 1 ? bias4.y : (e == 2 ? bias4.z : bias4.w)));
+                            if (EPI & NERF_EPI_RELU) x = fmaxf(x, 0.f);
+                            if (EPI & NERF_EPI_MASK) x = (a.aux[(int64_t)m * a.ldaux + en + e] > 0.f) ? x : 0.f;
+                            if (EPI & NERF_EPI_ACCUM) x = o[e] + x;
+                            o[e] = x;
+                        }
+                    }
+                }
+            }
+            barrier();
+        };
+        pass(0, acc[0], acc[1]);
+        pass(1, acc[2], acc[3]);
+        pass(2, acc[0], acc[1]);
+        pass(3, acc[2], acc[3]);
+    };
+
+    issue(0);
+    zero_acc();
+    for (int g = 0; g < total; ++g) {
+        const bool more = g + 1 < total;
+        if (more) {
+            issue((g + 1) & 1);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG) : "memory");   // chunk g landed, g+1 in flight
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        barrier();                      // chunk g visible to every wave
+        compute(g & 1);
+        barrier();                      // every wave done reading stage g & 1
+        if (++c_chunk == nchunks) {
+            epilogue(g & 1);
+            zero_acc();
+            c_chunk = 0;
+            c_tile += gridDim.x;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------- TN
 constexpr int TB = 128, TBM = 32;
 
@@ -319,7 +584,7 @@ struct TNArgs {
 };
 
 __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
-    constexpr int PL = TB * LDB;          // one transposed bf16 plane: 128 rows x (32 samples + pad)
+    constexpr int PL = TB * LDB;          // one transposed bf16 plane: 128 rows x 32 samples (swizzled)
     constexpr int BUFB = 4 * PL;          // dY^T hi, lo, X^T hi, lo
     __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUFB];
 
@@ -412,7 +677,7 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
                 h[r] = hb;
                 l[r] = (__bf16)(x - (float)hb);
             }
-            const int o = (cg * 4 + e) * LDB + rg * 8;
+            const int o = swz(cg * 4 + e, rg);
             *reinterpret_cast<bf16x8*>(Ph + o) = h;
             *reinterpret_cast<bf16x8*>(Pl + o) = l;
         }
@@ -427,17 +692,17 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
             const bool has_next = mc + TBM < mend;
             gload(has_next ? mc + TBM : mc);
             __builtin_amdgcn_sched_barrier(0);
-            const __bf16* Yb = smem + cur * BUFB + (wr * 64 + li) * LDB + lh * 8;
-            const __bf16* Xb = smem + cur * BUFB + 2 * PL + (wc * 64 + li) * LDB + lh * 8;
 #pragma unroll
             for (int s = 0; s < TBM / 16; ++s) {
+                const __bf16* Yb = smem + cur * BUFB + swz(wr * 64 + li, 2 * s + lh);
+                const __bf16* Xb = smem + cur * BUFB + 2 * PL + swz(wc * 64 + li, 2 * s + lh);
                 bf16x8 yh[2], yl[2], xh[2], xl[2];
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
-                    yh[i] = *reinterpret_cast<const bf16x8*>(Yb + i * 32 * LDB + s * 16);
-                    yl[i] = *reinterpret_cast<const bf16x8*>(Yb + PL + i * 32 * LDB + s * 16);
-                    xh[i] = *reinterpret_cast<const bf16x8*>(Xb + i * 32 * LDB + s * 16);
-                    xl[i] = *reinterpret_cast<const bf16x8*>(Xb + PL + i * 32 * LDB + s * 16);
+                    yh[i] = *reinterpret_cast<const bf16x8*>(Yb + i * 32 * LDB);
+                    yl[i] = *reinterpret_cast<const bf16x8*>(Yb + PL + i * 32 * LDB);
+                    xh[i] = *reinterpret_cast<const bf16x8*>(Xb + i * 32 * LDB);
+                    xl[i] = *reinterpret_cast<const bf16x8*>(Xb + PL + i * 32 * LDB);
                 }
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
@@ -479,9 +744,175 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
     }
 }
 
+// ------------------------------------------------------------------- TN wide
+// 256 (n) x 256 (k) weight-gradient tile per workgroup (8 waves, 2 x 4 of 128 x 64): dY and
+// X are each read from HBM once per M split (the 128 x 128 tiling reads them twice).  Both
+// operands are staged transposed through registers: a thread loads 8 samples x 2 columns
+// (8-byte loads, a wave covers 512 contiguous bytes of a row) and writes one 8-sample hi
+// and lo vector per column into the [column][32 samples hi | 32 lo] image (the 128-byte
+// row swizzle of the NT kernels; the writes of 8 consecutive threads hit 8 distinct slots).
+// Slab layout, bias-gradient slab and split policy are those of the fp32 kernel, so
+// nerf_linear_wgrad_reduce combines either.
+__global__ __launch_bounds__(512, 1) void linear_wgrad_x3_wide_kernel(TNArgs a, int npad, int kpad) {
+    constexpr int T2 = 256;
+    constexpr int IMG = T2 * 128;              // one operand image (bytes)
+    constexpr int STAGE = 2 * IMG;
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+    const int ntn = (a.N + T2 - 1) / T2;
+    const int ntk = (a.X.ktot + T2 - 1) / T2;
+    const int tiles = ntn * ntk;
+    const int bid = blockIdx.x;
+    const int split = bid / tiles;
+    const int tile = bid - split * tiles;
+    const int tn = tile / ntk, tk = tile - (tile / ntk) * ntk;
+    const int n0 = tn * T2, k0 = tk * T2;
+    const int mbeg = split * a.m_per_split;
+    int mend = mbeg + a.m_per_split;
+    if (mend > a.M) mend = a.M;
+
+    const int t = threadIdx.x;
+    const int wave = t >> 6, lane = t & 63;
+    const int wr = wave >> 2, wc = wave & 3;
+    const int li = lane & 31, lh = lane >> 5;
+    const int cp = t & 127, rg = t >> 7;      // staging: columns 2cp, 2cp+1; samples 8rg .. 8rg+7
+
+    // dY columns
+    const int ycol = n0 + 2 * cp;
+    const bool y_ok = ycol < a.N;
+    const int ycl = y_ok ? ycol : 0;
+    // X columns: the segment holding packed column k0 + 2cp (segments span multiples of 32)
+    const int kx = k0 + 2 * cp;
+    int xs = -1, xoff = 0;
+#pragma unroll
+    for (int q = 0; q < MAX_SEGS; ++q)
+        if (q < a.X.n && kx >= a.X.koff[q] && kx < a.X.koff[q] + a.X.kp[q]) { xs = q; xoff = kx - a.X.koff[q]; }
+    const bool x_ok = xs >= 0 && xoff < (xs >= 0 ? pick4(a.X.k, xs) : 0);
+    const float* xptr = x_ok ? pick4(a.X.ptr, xs) : a.dY;
+    const int64_t xld = x_ok ? pick4(a.X.ld, xs) : 0;
+    const unsigned xrd = x_ok ? (unsigned)pick4(a.X.row_div, xs) : 1u;
+    const int xcl = x_ok ? xoff : 0;
+
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 ry[8], rx[8];
+    unsigned mmask = 0;
+    auto gload = [&](int mc) __attribute__((always_inline)) {
+        mmask = 0;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int m = mc + rg * 8 + r;
+            const bool mok = m < mend;
+            mmask |= (mok ? 1u : 0u) << r;
+            const unsigned mm = (unsigned)(mok ? m : mbeg);
+            ry[r] = *reinterpret_cast<const f2*>(a.dY + (int64_t)mm * a.lddy + ycl);
+            rx[r] = *reinterpret_cast<const f2*>(xptr + (int64_t)(xrd == 1u ? mm : mm / xrd) * xld + xcl);
+        }
+    };
+    f2 dbacc = f2{0.f, 0.f};
+    auto put = [&](char* img, const f2 (&v)[8], bool ok, int e) __attribute__((always_inline)) {
+        bf16x8 h, l;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const float x = (ok && ((mmask >> r) & 1u)) ? (e == 0 ? v[r].x : v[r].y) : 0.f;
+            const __bf16 hb = (__bf16)x;
+            h[r] = hb;
+            l[r] = (__bf16)(x - (float)hb);
+        }
+        const int row = 2 * cp + e;
+        *reinterpret_cast<bf16x8*>(img + swz128(row, rg)) = h;
+        *reinterpret_cast<bf16x8*>(img + swz128(row, 4 + rg)) = l;
+    };
+    auto sstore = [&](int stage) __attribute__((always_inline)) {
+        char* Yi = smem + stage * STAGE;
+        char* Xi = Yi + IMG;
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+            if (y_ok && ((mmask >> r) & 1u)) dbacc += ry[r];
+        put(Yi, ry, y_ok, 0);
+        put(Yi, ry, y_ok, 1);
+        put(Xi, rx, x_ok, 0);
+        put(Xi, rx, x_ok, 1);
+    };
+
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    // waves whose k columns lie wholly past the packed K skip the MFMAs (wave-uniform)
+    const bool active = k0 + wc * 64 < a.X.ktot && n0 + wr * 128 < a.N;
+
+    if (mbeg < mend) {
+        gload(mbeg);
+        sstore(0);
+        __syncthreads();
+        int cur = 0;
+        for (int mc = mbeg; mc < mend; mc += TBM) {
+            const bool has_next = mc + TBM < mend;
+            gload(has_next ? mc + TBM : mc);
+            __builtin_amdgcn_sched_barrier(0);
+            if (active) {
+                const char* Yb = smem + cur * STAGE;
+                const char* Xb = Yb + IMG;
+#pragma unroll
+                for (int s = 0; s < TBM / 16; ++s) {
+                    bf16x8 xh[2], xl[2];
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const int row = wc * 64 + j * 32 + li;
+                        xh[j] = *reinterpret_cast<const bf16x8*>(Xb + swz128(row, 2 * s + lh));
+                        xl[j] = *reinterpret_cast<const bf16x8*>(Xb + swz128(row, 4 + 2 * s + lh));
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int row = wr * 128 + i * 32 + li;
+                        const bf16x8 yh = *reinterpret_cast<const bf16x8*>(Yb + swz128(row, 2 * s + lh));
+                        const bf16x8 yl = *reinterpret_cast<const bf16x8*>(Yb + swz128(row, 4 + 2 * s + lh));
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x3(yh, yl, xh[j], xl[j], acc[i][j]);
+                    }
+                }
+            }
+            if (has_next) sstore(cur ^ 1);
+            __syncthreads();
+            cur ^= 1;
+        }
+    }
+
+    float* slab = a.slab + (size_t)split * npad * kpad;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int k = k0 + wc * 64 + j * 32 + li;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int n = n0 + wr * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (n < npad && k < kpad) slab[(size_t)n * kpad + k] = acc[i][j][r];
+            }
+        }
+    // bias gradient: the 4 sample groups reduce through LDS in a fixed order
+    if (tk == 0) {
+        float* dbred = reinterpret_cast<float*>(smem);   // [4][256]; the loop ended on a barrier
+        dbred[rg * T2 + 2 * cp] = dbacc.x;
+        dbred[rg * T2 + 2 * cp + 1] = dbacc.y;
+        __syncthreads();
+        if (t < T2 && n0 + t < npad)
+            a.db_slab[(size_t)split * npad + n0 + t] =
+                ((dbred[t] + dbred[T2 + t]) + dbred[2 * T2 + t]) + dbred[3 * T2 + t];
+    }
+}
+
+// Interleaved split weights: element (r, c) of a [rows][ld] matrix goes to
+// Wx[r][c / 32][c % 32] (hi) and Wx[r][c / 32][32 + c % 32] (lo), i.e. each 32-column
+// chunk of a row is 128 contiguous bytes: 32 hi then 32 lo.
+__device__ __forceinline__ int64_t xoff(int64_t r, int c, int ld) { return r * ld * 2 + (c >> 5) * 64 + (c & 31); }
+
 __global__ void pack_weight_x3_kernel(const float* __restrict__ W, int N, int K_orig, const int32_t* __restrict__ col_map,
-                                      int Kp, int npad, __bf16* __restrict__ Wph, __bf16* __restrict__ Wpl,
-                                      __bf16* __restrict__ Wth, __bf16* __restrict__ Wtl, int ldwt, int kpad_rows) {
+                                      int Kp, int npad, __bf16* __restrict__ Wpx, __bf16* __restrict__ Wtx, int ldwt,
+                                      int kpad_rows) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t total = (int64_t)npad * Kp;
     if (idx < total) {
@@ -490,14 +921,16 @@ __global__ void pack_weight_x3_kernel(const float* __restrict__ W, int N, int K_
         const float v = (n < N && src >= 0 && src < K_orig) ? W[(int64_t)n * K_orig + src] : 0.f;
         const __bf16 h = (__bf16)v;
         const __bf16 l = (__bf16)(v - (float)h);
-        if (Wph) { Wph[idx] = h; Wpl[idx] = l; }
-        if (Wth && n < ldwt) { Wth[(int64_t)k * ldwt + n] = h; Wtl[(int64_t)k * ldwt + n] = l; }
+        if (Wpx) { const int64_t o = xoff(n, k, Kp); Wpx[o] = h; Wpx[o + 32] = l; }
+        if (Wtx && n < ldwt) { const int64_t o = xoff(k, n, ldwt); Wtx[o] = h; Wtx[o + 32] = l; }
     }
-    if (Wth) {
+    if (Wtx) {
+        // rows Kp .. kpad_rows of the transposed matrix are zero (columns N .. ldwt: n >= N above)
         const int64_t pad_total = (int64_t)(kpad_rows - Kp) * ldwt;
         if (idx < pad_total) {
-            Wth[(int64_t)Kp * ldwt + idx] = (__bf16)0.f;
-            Wtl[(int64_t)Kp * ldwt + idx] = (__bf16)0.f;
+            const int64_t o = xoff(Kp + idx / ldwt, (int)(idx % ldwt), ldwt);
+            Wtx[o] = (__bf16)0.f;
+            Wtx[o + 32] = (__bf16)0.f;
         }
     }
 }
@@ -539,21 +972,43 @@ int cu_count_x3() {
 extern "C" size_t nerf_linear_wgrad_workspace(int64_t M, int32_t N, int32_t K);
 int nerf_wgrad_choose_splits(int64_t M, int tiles);
 
-extern "C" int nerf_linear_fwd_x3(const nerf_seg* segs, int32_t n_segs, int64_t M, const void* W_hi, const void* W_lo,
-                                  int32_t ldw, int32_t N, const float* bias, float* out, int64_t ldo,
-                                  int32_t epilogue, const float* aux, int64_t ld_aux, void* stream) {
+extern "C" int nerf_linear_fwd_x3(const nerf_seg* segs, int32_t n_segs, int64_t M, const void* W_x, int32_t ldw,
+                                  int32_t N, const float* bias, float* out, int64_t ldo, int32_t epilogue,
+                                  const float* aux, int64_t ld_aux, void* stream) {
     NERF_REQUIRE(M >= 0 && M < (1ll << 31) && N >= 1);
     if (M == 0) return NERF_OK;
     SegList L;
     NERF_REQUIRE(build_segs(segs, n_segs, L));
-    NERF_REQUIRE(W_hi && W_lo && out && aligned16(W_hi) && aligned16(W_lo) && ldw == L.ktot && (ldw % 8) == 0 &&
-                 ldo >= N);
+    NERF_REQUIRE(W_x && out && aligned16(W_x) && ldw == L.ktot && (ldw % BK) == 0 && ldo >= N);
     if (epilogue & NERF_EPI_BIAS) NERF_REQUIRE(bias != nullptr);
     if (epilogue & NERF_EPI_MASK) NERF_REQUIRE(aux != nullptr && ld_aux >= N);
     const int vec_ok = aligned16(out) && (ldo % 4) == 0 && (!(epilogue & NERF_EPI_BIAS) || aligned16(bias)) &&
                        (!(epilogue & NERF_EPI_MASK) || (aligned16(aux) && (ld_aux % 4) == 0));
-    NTArgs a{L, (int)M, reinterpret_cast<const __bf16*>(W_hi), reinterpret_cast<const __bf16*>(W_lo), ldw, N, bias,
-             out, ldo, epilogue, aux, ld_aux, vec_ok};
+    NTArgs a{L, (int)M, reinterpret_cast<const __bf16*>(W_x), ldw, N, bias, out, ldo, epilogue, aux, ld_aux, vec_ok};
+    hipStream_t st = as_stream(stream);
+    if (N <= 256 && !(epilogue & NERF_EPI_NARROW_TILE)) {
+        const int ntiles = (int)((M + 255) / 256);
+        int grid = cu_count_x3();
+        if (grid > ntiles) grid = ntiles;
+        const dim3 g3((unsigned)grid), b3(512);
+#define NERF_GLDS_LAUNCH(E)                                                                          \
+    do {                                                                                            \
+        if (N > 128) hipLaunchKernelGGL((linear_nt_x3_glds_kernel<E, 2>), g3, b3, 0, st, a, ntiles); \
+        else hipLaunchKernelGGL((linear_nt_x3_glds_kernel<E, 1>), g3, b3, 0, st, a, ntiles);         \
+    } while (0)
+        switch (epilogue & 15) {
+            case NERF_EPI_BIAS | NERF_EPI_RELU: NERF_GLDS_LAUNCH(NERF_EPI_BIAS | NERF_EPI_RELU); break;
+            case NERF_EPI_BIAS: NERF_GLDS_LAUNCH(NERF_EPI_BIAS); break;
+            case 0: NERF_GLDS_LAUNCH(0); break;
+            case NERF_EPI_MASK: NERF_GLDS_LAUNCH(NERF_EPI_MASK); break;
+            case NERF_EPI_MASK | NERF_EPI_ACCUM: NERF_GLDS_LAUNCH(NERF_EPI_MASK | NERF_EPI_ACCUM); break;
+            case NERF_EPI_ACCUM: NERF_GLDS_LAUNCH(NERF_EPI_ACCUM); break;
+            default: return NERF_ERR_UNSUPPORTED;
+        }
+#undef NERF_GLDS_LAUNCH
+        NERF_CHECK_LAUNCH();
+        return NERF_OK;
+    }
     const int ntm = (int)((M + 127) / 128);
     const int ntn = (N + 127) / 128;
     const int ntiles = (ntm + 7) / 8 * 8 * ntn;
@@ -562,7 +1017,7 @@ extern "C" int nerf_linear_fwd_x3(const nerf_seg* segs, int32_t n_segs, int64_t 
         const int cap = 2 * cu_count_x3();
         if (grid > cap) grid = cap;
     }
-    hipLaunchKernelGGL(linear_nt_x3_kernel, dim3((unsigned)grid), dim3(256), 0, as_stream(stream), a, ntm, ntiles);
+    hipLaunchKernelGGL(linear_nt_x3_kernel, dim3((unsigned)grid), dim3(256), 0, st, a, ntm, ntiles);
     NERF_CHECK_LAUNCH();
     return NERF_OK;
 }
@@ -582,6 +1037,13 @@ extern "C" int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N, c
     int64_t mps = (M + splits - 1) / splits;
     mps = ((mps + TBM - 1) / TBM) * TBM;
     TNArgs a{dY, ld_dy, N, L, (int)M, (int)mps, splits, slab, db_slab};
+    if ((N > 128 || L.ktot > 128) && N <= 256 && L.ktot <= 256) {   // one 256 x 256 tile covers the layer
+        const int64_t blocks = (int64_t)splits * ((N + 255) / 256) * ((L.ktot + 255) / 256);
+        hipLaunchKernelGGL(linear_wgrad_x3_wide_kernel, dim3((unsigned)blocks), dim3(512), 0, as_stream(stream), a,
+                           ntn * TB, ntk * TB);
+        NERF_CHECK_LAUNCH();
+        return NERF_OK;
+    }
     const int64_t blocks = (int64_t)splits * ntn * ntk;
     hipLaunchKernelGGL(linear_wgrad_x3_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
     NERF_CHECK_LAUNCH();
@@ -589,18 +1051,19 @@ extern "C" int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N, c
 }
 
 extern "C" int nerf_pack_weight_x3(const float* W, int32_t N, int32_t K_orig, const int32_t* col_map, int32_t Kp,
-                                   void* Wp_hi, void* Wp_lo, void* Wt_hi, void* Wt_lo, int32_t ldwt, void* stream) {
+                                   void* Wp_x, void* Wt_x, int32_t ldwt, void* stream) {
     NERF_REQUIRE(W && col_map && N >= 1 && K_orig >= 1 && Kp >= 1 && (Kp % BK) == 0);
-    NERF_REQUIRE((Wp_hi == nullptr) == (Wp_lo == nullptr) && (Wt_hi == nullptr) == (Wt_lo == nullptr));
     const int npad = ((N + 127) / 128) * 128;
-    if (Wt_hi) NERF_REQUIRE(ldwt >= ((N + 31) / 32) * 32);
+    if (Wt_x) NERF_REQUIRE(ldwt >= ((N + 31) / 32) * 32 && (ldwt % BK) == 0);
     const int kpad_rows = ((Kp + 127) / 128) * 128 + 128;
     int64_t total = (int64_t)npad * Kp;
-    const int64_t pad_total = (int64_t)(kpad_rows - Kp) * (Wt_hi ? ldwt : 0);
-    if (pad_total > total) total = pad_total;
+    if (Wt_x) {
+        const int64_t pad_total = (int64_t)(kpad_rows - Kp) * ldwt;
+        if (pad_total > total) total = pad_total;
+    }
     hipLaunchKernelGGL(pack_weight_x3_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream), W,
-                       N, K_orig, col_map, Kp, npad, reinterpret_cast<__bf16*>(Wp_hi), reinterpret_cast<__bf16*>(Wp_lo),
-                       reinterpret_cast<__bf16*>(Wt_hi), reinterpret_cast<__bf16*>(Wt_lo), ldwt, kpad_rows);
+                       N, K_orig, col_map, Kp, npad, reinterpret_cast<__bf16*>(Wp_x), reinterpret_cast<__bf16*>(Wt_x),
+                       ldwt, kpad_rows);
     NERF_CHECK_LAUNCH();
     return NERF_OK;
 }

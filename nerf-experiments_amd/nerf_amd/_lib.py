@@ -28,6 +28,8 @@ NERF_EPI_BIAS = 1
 NERF_EPI_RELU = 2
 NERF_EPI_MASK = 4
 NERF_EPI_ACCUM = 8
+NERF_EPI_NO_PERSIST = 256
+NERF_EPI_NARROW_TILE = 512
 
 
 class NerfSeg(ctypes.Structure):
@@ -70,10 +72,10 @@ _SIGNATURES = {
     "nerf_linear_wgrad": (c_i32, [c_vp, c_i64, c_i32, ctypes.POINTER(NerfSeg), c_i32, c_i64, c_vp, c_sz, c_vp]),
     "nerf_linear_wgrad_reduce": (c_i32, [c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "nerf_pack_weight": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
-    "nerf_linear_fwd_x3": (c_i32, [ctypes.POINTER(NerfSeg), c_i32, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp,
+    "nerf_linear_fwd_x3": (c_i32, [ctypes.POINTER(NerfSeg), c_i32, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp,
                                    c_i64, c_i32, c_vp, c_i64, c_vp]),
     "nerf_linear_wgrad_x3": (c_i32, [c_vp, c_i64, c_i32, ctypes.POINTER(NerfSeg), c_i32, c_i64, c_vp, c_sz, c_vp]),
-    "nerf_pack_weight_x3": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp]),
+    "nerf_pack_weight_x3": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES.keys())

@@ -243,15 +243,16 @@ def linear_wgrad_reduce(M: int, N4: int, K: int, n_valid: int, workspace: torch.
     _lib.check(st, "nerf_linear_wgrad_reduce")
 
 
-def linear_fwd_x3(segs, M: int, Wh: torch.Tensor, Wl: torch.Tensor, ldw: int, N: int, bias: torch.Tensor | None,
+def linear_fwd_x3(segs, M: int, Wx: torch.Tensor, ldw: int, N: int, bias: torch.Tensor | None,
                   out: torch.Tensor, epilogue: int, aux: torch.Tensor | None = None, w_row_offset: int = 0) -> None:
-    """3 x bf16 split-precision variant of linear_fwd (weights pre-split into bf16 planes)."""
+    """3 x bf16 split-precision variant of linear_fwd; Wx holds the interleaved hi|lo
+    weights of nerf_pack_weight_x3 ([rows][ldw/32][hi 32 | lo 32] bf16)."""
     arr = make_segs(segs)
-    off = w_row_offset * ldw * 2
+    off = w_row_offset * ldw * 2 * 2
     end = TIMER.bracket("linear_nt_x3", 2.0 * M * N * ldw) if TIMER is not None else None
-    st = _lib.load().nerf_linear_fwd_x3(arr, len(segs), M, Wh.data_ptr() + off, Wl.data_ptr() + off, ldw, N,
-                                        _ptr(bias), _ptr(out), out.stride(0), epilogue, _ptr(aux),
-                                        aux.stride(0) if aux is not None else 0, _stream(out.device))
+    st = _lib.load().nerf_linear_fwd_x3(arr, len(segs), M, Wx.data_ptr() + off, ldw, N, _ptr(bias), _ptr(out),
+                                        out.stride(0), epilogue, _ptr(aux), aux.stride(0) if aux is not None else 0,
+                                        _stream(out.device))
     if end is not None:
         end.record()
     _lib.check(st, "nerf_linear_fwd_x3")
@@ -268,11 +269,18 @@ def linear_wgrad_x3(dY: torch.Tensor, N4: int, segs, M: int, workspace: torch.Te
     _lib.check(st, "nerf_linear_wgrad_x3")
 
 
-def pack_weight_x3(W: torch.Tensor, col_map: torch.Tensor, Kp: int, Wph, Wpl, Wth, Wtl, ldwt: int) -> None:
+def pack_weight_x3(W: torch.Tensor, col_map: torch.Tensor, Kp: int, Wpx: torch.Tensor | None,
+                   Wtx: torch.Tensor | None, ldwt: int) -> None:
     N, K_orig = W.shape
-    st = _lib.load().nerf_pack_weight_x3(_ptr(W), N, K_orig, _ptr(col_map), Kp, _ptr(Wph), _ptr(Wpl), _ptr(Wth),
-                                         _ptr(Wtl), ldwt, _stream(W.device))
+    st = _lib.load().nerf_pack_weight_x3(_ptr(W), N, K_orig, _ptr(col_map), Kp, _ptr(Wpx), _ptr(Wtx), ldwt,
+                                         _stream(W.device))
     _lib.check(st, "nerf_pack_weight_x3")
+
+
+def interleave_x3(hi: torch.Tensor, lo: torch.Tensor) -> torch.Tensor:
+    """[rows][ld] hi / lo planes -> the interleaved [rows][ld/32][hi 32 | lo 32] layout."""
+    r, ld = hi.shape
+    return torch.stack((hi.reshape(r, ld // 32, 32), lo.reshape(r, ld // 32, 32)), dim=2).reshape(r, 2 * ld)
 
 
 def pack_weight(W: torch.Tensor, col_map: torch.Tensor, Kp: int, Wp: torch.Tensor | None,

@@ -73,10 +73,8 @@ class LayerPlan:
     Wp: torch.Tensor | None = None
     Wt: torch.Tensor | None = None
     packed_version: tuple = ()
-    Wph: torch.Tensor | None = None
-    Wpl: torch.Tensor | None = None
-    Wth: torch.Tensor | None = None
-    Wtl: torch.Tensor | None = None
+    Wpx: torch.Tensor | None = None
+    Wtx: torch.Tensor | None = None
     packed_version_x3: tuple = ()
 
     def finalize(self, device):
@@ -103,7 +101,7 @@ class LayerPlan:
         self.Wp = torch.empty(K.pad128(self.N), self.Kp, device=device, dtype=torch.float32)
         self.Wt = torch.empty(K.pad128(self.Kp) + 128, self.ldwt, device=device, dtype=torch.float32)
         self.packed_version = ()
-        self.Wph = self.Wpl = self.Wth = self.Wtl = None
+        self.Wpx = self.Wtx = None
         self.packed_version_x3 = ()
 
     def pack(self, precision: str = "fp32"):
@@ -113,14 +111,11 @@ class LayerPlan:
             K.pack_weight(w.detach().contiguous(), self.col_map, self.Kp, self.Wp, self.Wt, self.ldwt)
             self.packed_version = ver
         if precision == "x3" and ver != self.packed_version_x3:
-            if self.Wph is None:
+            if self.Wpx is None:
                 dev = self.Wp.device
-                self.Wph = torch.empty(self.Wp.shape, device=dev, dtype=torch.bfloat16)
-                self.Wpl = torch.empty_like(self.Wph)
-                self.Wth = torch.empty(self.Wt.shape, device=dev, dtype=torch.bfloat16)
-                self.Wtl = torch.empty_like(self.Wth)
-            K.pack_weight_x3(w.detach().contiguous(), self.col_map, self.Kp, self.Wph, self.Wpl, self.Wth, self.Wtl,
-                             self.ldwt)
+                self.Wpx = torch.empty(self.Wp.shape[0], 2 * self.Wp.shape[1], device=dev, dtype=torch.bfloat16)
+                self.Wtx = torch.empty(self.Wt.shape[0], 2 * self.Wt.shape[1], device=dev, dtype=torch.bfloat16)
+            K.pack_weight_x3(w.detach().contiguous(), self.col_map, self.Kp, self.Wpx, self.Wtx, self.ldwt)
             self.packed_version_x3 = ver
 
     def gemm(self, precision: str, segs, M: int, transpose: bool, N: int, bias, out, epi, aux=None,
@@ -128,9 +123,8 @@ class LayerPlan:
         """Forward (W) or input-gradient (W^T) GEMM in the requested precision; layers
         narrower than 33 outputs always use the fp32 kernel (their 128 x 32 tile)."""
         if precision == "x3" and N > 32:
-            wh, wl = (self.Wth, self.Wtl) if transpose else (self.Wph, self.Wpl)
-            K.linear_fwd_x3(segs, M, wh, wl, self.ldwt if transpose else self.Kp, N, bias, out, epi, aux=aux,
-                            w_row_offset=row_offset)
+            K.linear_fwd_x3(segs, M, self.Wtx if transpose else self.Wpx, self.ldwt if transpose else self.Kp, N, bias,
+                            out, epi, aux=aux, w_row_offset=row_offset)
         else:
             K.linear_fwd(segs, M, self.Wt if transpose else self.Wp, self.ldwt if transpose else self.Kp, N, bias,
                          out, epi, aux=aux, w_row_offset=row_offset)

@@ -304,30 +304,27 @@ def test_linear_x3_fwd_wgrad(M, N, ks, rd):
         off += k
     cmd = torch.tensor(cm, dtype=torch.int32, device=DEV)
     ldwt = K.pad32(N)
-    Wph = torch.empty(K.pad128(N), Kp, dtype=torch.bfloat16, device=DEV)
-    Wpl = torch.empty_like(Wph)
-    Wth = torch.empty(K.pad128(Kp) + 128, ldwt, dtype=torch.bfloat16, device=DEV)
-    Wtl = torch.empty_like(Wth)
-    K.pack_weight_x3(W.to(DEV), cmd, Kp, Wph, Wpl, Wth, Wtl, ldwt)
-    # packing is bit-exact against torch's round-to-nearest-even split
+    Wpx = torch.empty(K.pad128(N), 2 * Kp, dtype=torch.bfloat16, device=DEV)
+    Wtx = torch.empty(K.pad128(Kp) + 128, 2 * ldwt, dtype=torch.bfloat16, device=DEV)
+    K.pack_weight_x3(W.to(DEV), cmd, Kp, Wpx, Wtx, ldwt)
+    # packing is bit-exact against torch's round-to-nearest-even split, interleaved per 32 columns
     Wp = torch.zeros(K.pad128(N), Kp)
     for j, c in enumerate(cm):
         if c >= 0:
             Wp[:N, j] = W[:, c]
     h, lo = _split_bf16(Wp)
-    assert torch.equal(Wph.cpu().view(torch.int16), h.view(torch.int16))
-    assert torch.equal(Wpl.cpu().view(torch.int16), lo.view(torch.int16))
-    ht, lt = _split_bf16(Wp.T.contiguous())
-    assert torch.equal(Wth.cpu()[:Kp, :N].view(torch.int16), ht[:, :N].view(torch.int16))
-    assert torch.equal(Wtl.cpu()[:Kp, :N].view(torch.int16), lt[:, :N].view(torch.int16))
-    assert not Wth.cpu()[Kp:].float().abs().any() and not Wth.cpu()[:, N:].float().abs().any()
+    assert torch.equal(Wpx.cpu().view(torch.int16), K.interleave_x3(h, lo).view(torch.int16))
+    Wt = torch.zeros(K.pad128(Kp) + 128, ldwt)
+    Wt[:Kp, :N] = Wp[:N].T
+    ht, lt = _split_bf16(Wt)
+    assert torch.equal(Wtx.cpu().view(torch.int16), K.interleave_x3(ht, lt).view(torch.int16))
 
     segs = [(s.to(DEV), k, r) for s, k, r in zip(segs_cpu, ks, rd)]
     ldo = (N + 3) // 4 * 4
     Xd, Wd = X.double(), W.double()
     bound = 2.0 ** -15 * (Xd.abs() @ Wd.abs().T) + 1e-6
     out = torch.empty(M, ldo, device=DEV)
-    K.linear_fwd_x3(segs, M, Wph, Wpl, Kp, N, b.to(DEV), out, NERF_EPI_BIAS | NERF_EPI_RELU)
+    K.linear_fwd_x3(segs, M, Wpx, Kp, N, b.to(DEV), out, NERF_EPI_BIAS | NERF_EPI_RELU)
     ref = torch.relu(Xd @ Wd.T + b.double())
     err = (out[:, :N].cpu().double() - ref).abs()
     assert (err <= bound + 1e-6).all(), float((err - bound).max())
@@ -335,7 +332,7 @@ def test_linear_x3_fwd_wgrad(M, N, ks, rd):
     aux = torch.randn(M, ldo)
     out2 = torch.randn(M, ldo)
     o2 = out2.clone().to(DEV)
-    K.linear_fwd_x3(segs, M, Wph, Wpl, Kp, N, None, o2, NERF_EPI_MASK | NERF_EPI_ACCUM, aux=aux.to(DEV))
+    K.linear_fwd_x3(segs, M, Wpx, Kp, N, None, o2, NERF_EPI_MASK | NERF_EPI_ACCUM, aux=aux.to(DEV))
     ref2 = out2[:, :N].double() + (Xd @ Wd.T) * (aux[:, :N] > 0)
     err = (o2[:, :N].cpu().double() - ref2).abs()
     assert (err <= bound + 1e-6).all(), float((err - bound).max())
@@ -343,7 +340,7 @@ def test_linear_x3_fwd_wgrad(M, N, ks, rd):
     dY = torch.randn(M, ldo)
     dY[:, N:] = 0
     dX = torch.empty(M, Kp, device=DEV)
-    K.linear_fwd_x3([(dY.to(DEV), ldo, 1)], M, Wth, Wtl, ldwt, Kp, None, dX, 0)
+    K.linear_fwd_x3([(dY.to(DEV), ldo, 1)], M, Wtx, ldwt, Kp, None, dX, 0)
     refx = dY[:, :N].double() @ Wp[:N].double()
     bx = 2.0 ** -15 * (dY[:, :N].double().abs() @ Wp[:N].double().abs()) + 1e-6
     assert ((dX.cpu().double() - refx).abs() <= bx).all()

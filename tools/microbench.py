@@ -22,6 +22,7 @@ from nerf_amd import kernels as K  # noqa: E402
 from nerf_amd._lib import NERF_EPI_BIAS, NERF_EPI_MASK, NERF_EPI_RELU  # noqa: E402
 
 NERF_EPI_NO_PERSIST = 256
+NERF_EPI_NARROW_TILE = 512
 
 DEV = torch.device("cuda", 0)
 
@@ -53,11 +54,14 @@ def bench_linear(M, N, ks, rd, epi=NERF_EPI_BIAS | NERF_EPI_RELU, x3=False):
     fl = 2.0 * M * N * sum(ks)
     if x3:
         Wh = W.bfloat16()
-        Wl = (W - Wh.float()).bfloat16()
-        ms = time_it(lambda: K.linear_fwd_x3(segs, M, Wh, Wl, Kt, N, b, out, epi, aux=aux))
+        Wx = K.interleave_x3(Wh, (W - Wh.float()).bfloat16())
+        ms = time_it(lambda: K.linear_fwd_x3(segs, M, Wx, Kt, N, b, out, epi, aux=aux))
         r = {"kernel": "linear_nt_x3", "M": M, "N": N, "K": ks, "ms": ms, "tflops": fl / ms / 1e9}
-        ms_np = time_it(lambda: K.linear_fwd_x3(segs, M, Wh, Wl, Kt, N, b, out, epi | NERF_EPI_NO_PERSIST, aux=aux))
+        ms_np = time_it(lambda: K.linear_fwd_x3(segs, M, Wx, Kt, N, b, out, epi | NERF_EPI_NO_PERSIST, aux=aux))
         r["tflops_no_persist"] = fl / ms_np / 1e9
+        if 128 < N <= 256:
+            ms_n = time_it(lambda: K.linear_fwd_x3(segs, M, Wx, Kt, N, b, out, epi | NERF_EPI_NARROW_TILE, aux=aux))
+            r["tflops_narrow_tile"] = fl / ms_n / 1e9
         return r
     ms = time_it(lambda: K.linear_fwd(segs, M, W, Kt, N, b, out, epi, aux=aux))
     r = {"kernel": "linear_nt", "M": M, "N": N, "K": ks, "ms": ms, "tflops": fl / ms / 1e9}
