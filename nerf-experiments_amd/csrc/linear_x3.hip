@@ -321,8 +321,10 @@ __global__ __launch_bounds__(256, 2) void linear_nt_x3_kernel(NTArgs a, int ntm,
 // Both LDS images have 128-byte rows whose 16-byte slots are XOR-permuted by (row >> 1) & 7;
 // the permutation is applied to the per-lane SOURCE address (the DMA destination is
 // lane-linear) and to the fragment reads, which it makes bank-conflict-free.
-// Two stages: chunk g+1 is in flight while chunk g is multiplied; the in-loop waits are
-// counted (vmcnt(NG)), the barriers raw, so a __syncthreads() never drains the prefetch.
+// Pipeline: A (streamed from HBM) runs two chunks ahead in a 3-stage ring, W (L2-resident)
+// one chunk ahead in a 2-stage ring — 64 KB of A in flight per CU; all LDS is this ring
+// (160 KB for BN = 256).  In-loop waits are counted vmcnt, barriers raw, so the prefetch is
+// never drained by a __syncthreads().
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 
@@ -332,14 +334,18 @@ template <int EPI, int JN>
 __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int ntiles) {
     constexpr int BM = 256, BN = 128 * JN;
     constexpr int ABYTES = BM * 128, WBYTES = BN * 128;
-    constexpr int STAGE = ABYTES + WBYTES;
-    constexpr int QA = BM / 64;                 // A glds instructions per wave per chunk (8 rows each)
-    constexpr int QW = BN / 64;                 // W glds instructions per wave per chunk
-    constexpr int NG = QA + QW;
+#ifdef NERF_ROLE_SPLIT
+    constexpr int LW = 4;                       // waves 0..LW-1 issue the DMA, the others the stores
+#else
+    constexpr int LW = 8;
+#endif
+    constexpr int EW = LW == 8 ? 8 : 8 - LW;    // waves running the epilogue's global phase
+    constexpr int QA = BM / (8 * LW);           // A DMA instructions per loader wave per chunk (8 rows each)
+    constexpr int QW = BN / (8 * LW);           // W DMA instructions per loader wave per chunk
     // ONE __shared__ array (a second LDS object makes hipcc drain the DMA before ds_reads)
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 256];
-    SegList* segs_lds = reinterpret_cast<SegList*>(smem + 2 * STAGE);
-    static_assert(sizeof(SegList) <= 256, "segment table");
+    __shared__ __attribute__((aligned(16))) char smem[3 * ABYTES + 2 * WBYTES];
+    char* const Aring = smem;
+    char* const Wring = smem + 3 * ABYTES;
 
     const int t = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
@@ -348,70 +354,98 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
     const int lrow = lane >> 3, lphys = lane & 7;        // DMA lane -> (row in 8-row group, physical slot)
 
     if ((int)blockIdx.x >= ntiles) return;
-    if (t == 0) *segs_lds = a.A;
-    __syncthreads();
     const int nchunks = a.A.ktot / BK;
     const int my_tiles = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
     const int total = my_tiles * nchunks;
 
-    // ---- DMA cursor (advanced once per issued chunk)
-    int l_tile = blockIdx.x, l_seg = 0, l_kc = 0, l_c = 0;
+    // segment table in scalar registers; the empty asm keeps the compiler from turning the
+    // selects of pick4 back into an indexed load of the by-value argument (which it would
+    // then copy to scratch)
+    // segment fields indexed by the (wave-uniform) segment number are read straight from the
+    // kernel-argument segment with scalar loads: indexing the by-value argument (or selecting
+    // among its fields, which the optimizer folds into an indexed load) makes hipcc copy the
+    // whole argument to scratch
+    typedef __attribute__((address_space(4))) const char kchar_t;
+    kchar_t* kargs = (kchar_t*)__builtin_amdgcn_kernarg_segment_ptr();
+#define NERF_SEGF(T, field, i)                                                                         \
+    (*(const __attribute__((address_space(4))) T*)(kargs + offsetof(NTArgs, A) + offsetof(SegList, field) + \
+                                                    (size_t)(i) * sizeof(T)))
+    typedef const float* cfptr_t;
+
+    // ---- A DMA cursor.  Each tile walks its K chunks starting at chunk (tile % nchunks),
+    // wrapping around, so workgroups reach their epilogues (store bursts) at different
+    // times; the summation order is a function of the tile index only (grid-independent).
+    int a_tile = blockIdx.x, a_i = 0, a_seg = -1, a_kc = 0;
     const float* sp = nullptr;
-    int sk = 0, skp = 0;
-    int64_t aoff[QA];
-    int alog[QA];                 // logical slot each A lane fetches
-    auto set_seg = [&](int s) __attribute__((always_inline)) {
-        sp = segs_lds->ptr[s];
-        const int64_t ld = segs_lds->ld[s];
-        const unsigned rd = (unsigned)segs_lds->row_div[s];
-        sk = segs_lds->k[s];
-        skp = segs_lds->kp[s];
-        const int m0 = l_tile * BM;
+    int sk = 0;
+    int64_t sld = 0;
+    unsigned asrc[QA];            // source row of each A DMA instruction of this lane
+    // rows of instruction q are q*8 + lrow (mod 64): the swizzle term only depends on q & 1
+    const int alog0 = lphys ^ ((lrow >> 1) & 7), alog1 = lphys ^ (4 + ((lrow >> 1) & 7));
+    auto a_locate = [&](bool new_tile) __attribute__((always_inline)) {
+        int c = a_i + a_tile % nchunks;
+        c = c >= nchunks ? c - nchunks : c;
+        int sgi = 0;
+        while (sgi + 1 < a.A.n && c * BK >= NERF_SEGF(int, koff, sgi + 1)) ++sgi;
+        a_kc = c * BK - NERF_SEGF(int, koff, sgi);
+        if (new_tile || sgi != a_seg) {
+            a_seg = sgi;
+            sp = NERF_SEGF(cfptr_t, ptr, sgi);
+            sld = NERF_SEGF(int64_t, ld, sgi);
+            sk = NERF_SEGF(int, k, sgi);
+            const unsigned rd = (unsigned)NERF_SEGF(int, row_div, sgi);
+            const int m0 = a_tile * BM;
 #pragma unroll
-        for (int q = 0; q < QA; ++q) {
-            const int row = (wave * QA + q) * 8 + lrow;
-            int m = m0 + row;
-            m = m < a.M ? m : a.M - 1;                    // rows past M: any valid row (discarded)
-            const unsigned src = (rd == 1u) ? (unsigned)m : (unsigned)m / rd;
-            aoff[q] = (int64_t)src * ld;
-            alog[q] = lphys ^ ((row >> 1) & 7);
+            for (int q = 0; q < QA; ++q) {
+                int m = m0 + (wave * QA + q) * 8 + lrow;
+                m = m < a.M ? m : a.M - 1;                // rows past M: any valid row (discarded)
+                asrc[q] = (rd == 1u) ? (unsigned)m : (unsigned)m / rd;
+            }
         }
     };
+    a_locate(true);
+    const bool loader = wave < LW;
+    const bool storer = LW == 8 || !loader;
+    auto issue_a = [&](int stage) __attribute__((always_inline)) {
+        char* base = Aring + stage * ABYTES;
+        if (loader)
+#pragma unroll
+        for (int q = 0; q < QA; ++q) {
+            const int col = a_kc + ((q & 1) ? alog1 : alog0) * 4;
+            const float* src = sp + (int64_t)asrc[q] * sld + (col < sk ? col : 0);   // past k: finite data x zero weights
+            __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(base + (wave * QA + q) * 1024), 16, 0, 0);
+        }
+        if (++a_i == nchunks) {
+            a_i = 0;
+            a_tile += gridDim.x;
+            if (a_tile < ntiles) a_locate(true);
+        } else {
+            a_locate(false);
+        }
+    };
+    // ---- W DMA cursor
     const int nkc = a.ldw / BK;                          // 32-wide chunks per weight row
-    int64_t woff[QW];
+    unsigned woff[QW];                                   // bf16 element offsets (weights are small)
 #pragma unroll
     for (int q = 0; q < QW; ++q) {
         const int row = (wave * QW + q) * 8 + lrow;
         const int n = row < a.N ? row : a.N - 1;         // rows past N: any valid row (discarded)
-        woff[q] = (int64_t)n * nkc * 64 + ((lphys ^ ((row >> 1) & 7)) << 3);
+        woff[q] = (unsigned)n * nkc * 64 + ((lphys ^ ((row >> 1) & 7)) << 3);
     }
-    set_seg(0);
-
-    auto issue = [&](int stage) __attribute__((always_inline)) {
-        char* base = smem + stage * STAGE;
-#pragma unroll
-        for (int q = 0; q < QA; ++q) {
-            const int col = l_kc + alog[q] * 4;
-            const float* src = sp + aoff[q] + (col < sk ? col : 0);   // past k: finite data x zero weights
-            __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(base + (wave * QA + q) * 1024), 16, 0, 0);
-        }
+    int w_tile = blockIdx.x, w_i = 0;
+    auto issue_w = [&](int stage) __attribute__((always_inline)) {
+        char* base = Wring + stage * WBYTES;
+        int c = w_i + w_tile % nchunks;
+        c = c >= nchunks ? c - nchunks : c;
+        if (loader)
 #pragma unroll
         for (int q = 0; q < QW; ++q) {
-            const __bf16* src = a.Wx + woff[q] + (int64_t)l_c * 64;
-            __builtin_amdgcn_global_load_lds((glb_void_t*)src,
-                                             (lds_void_t*)(base + ABYTES + (wave * QW + q) * 1024), 16, 0, 0);
+            const __bf16* src = a.Wx + woff[q] + (unsigned)c * 64u;
+            __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(base + (wave * QW + q) * 1024), 16, 0, 0);
         }
-        l_kc += BK;
-        ++l_c;
-        if (l_kc >= skp) {
-            l_kc = 0;
-            ++l_seg;
-            if (l_seg >= a.A.n) {
-                l_seg = 0;
-                l_c = 0;
-                l_tile += gridDim.x;
-            }
-            if (l_tile < ntiles) set_seg(l_seg);
+        if (++w_i == nchunks) {
+            w_i = 0;
+            w_tile += gridDim.x;
         }
     };
 
@@ -424,9 +458,9 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     };
-    auto compute = [&](int stage) __attribute__((always_inline)) {
-        const char* Ab = smem + stage * STAGE;
-        const char* Wb = Ab + ABYTES;
+    auto compute = [&](int astage, int wstage) __attribute__((always_inline)) {
+        const char* Ab = Aring + astage * ABYTES;
+        const char* Wb = Wring + wstage * WBYTES;
 #pragma unroll
         for (int s = 0; s < BK / 16; ++s) {
             bf16x8 bh[JN], bl[JN];
@@ -455,8 +489,9 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
     // bias of this thread's epilogue column quad (N <= BN: one column tile), loaded before
     // any DMA is in flight
     constexpr int C4 = BN / 4;                    // float4 columns per row
-    constexpr int RS = 512 / C4;                  // rows per epilogue sweep
-    const int ec4 = t % C4, erow = t / C4;
+    constexpr int RS = 64 * EW / C4;              // rows per epilogue sweep
+    const int et = t & (64 * EW - 1);
+    const int ec4 = et % C4, erow = et / C4;
     const int en = ec4 * 4;
     f4 bias4 = f4{0.f, 0.f, 0.f, 0.f};
     if ((EPI & NERF_EPI_BIAS) && en < a.N) {
@@ -474,12 +509,14 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
     };
-    // epilogue through the stage just consumed, 64 rows per pass
+    // epilogue: 64 rows per pass, rows 0-31 in the free A stage, 32-63 in the free W stage
     int c_tile = blockIdx.x, c_chunk = 0;
-    auto epilogue = [&](int free_stage) __attribute__((always_inline)) {
-        float* Cs = reinterpret_cast<float*>(smem + free_stage * STAGE);
-        static_assert(64 * BN * 4 <= STAGE, "epilogue pass must fit one stage");
+    auto epilogue = [&](int astage, int wstage) __attribute__((always_inline)) {
+        static_assert(32 * BN * 4 <= ABYTES && 32 * BN * 4 <= WBYTES, "epilogue pass must fit the free stages");
+        float* C0 = reinterpret_cast<float*>(Aring + astage * ABYTES);
+        float* C1 = reinterpret_cast<float*>(Wring + wstage * WBYTES);
         const int tm0 = c_tile * BM;
+        const bool vec = a.vec_ok && en + 4 <= a.N;
         auto pass = [&](int p, const f32x16 (&c)[JN], const f32x16 (&d)[JN]) __attribute__((always_inline)) {
             if (wr == (p >> 1)) {
 #pragma unroll
@@ -487,14 +524,14 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
-                        Cs[row * BN + wc * (BN / 4) + j * 32 + li] = c[j][r];
-                        Cs[(32 + row) * BN + wc * (BN / 4) + j * 32 + li] = d[j][r];
+                        C0[row * BN + wc * (BN / 4) + j * 32 + li] = c[j][r];
+                        C1[row * BN + wc * (BN / 4) + j * 32 + li] = d[j][r];
                     }
             }
             barrier();
-            const bool vec = a.vec_ok && en + 4 <= a.N;
             // aux / out reads of a batch of rows are issued together (one memory round trip
             // per batch instead of one per row)
+            if (storer)
 #pragma unroll
             for (int qb = 0; qb < 64 / RS; qb += 4) {
                 f4 xa[4], xo[4];
@@ -512,7 +549,8 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
                     const int row = erow + RS * (qb + u);
                     const int m = tm0 + 64 * p + row;
                     if (m >= a.M || en >= a.N) continue;
-                    f4 v = *reinterpret_cast<const f4*>(Cs + row * BN + en);
+                    const float* Cr = row < 32 ? C0 + row * BN : C1 + (row - 32) * BN;
+                    f4 v = *reinterpret_cast<const f4*>(Cr + en);
                     float* o = a.out + (int64_t)m * a.ldo + en;
                     if (vec) {
                         if (EPI & NERF_EPI_BIAS) v += bias4;
@@ -525,6 +563,9 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
                             v.z = x.z > 0.f ? v.z : 0.f; v.w = x.w > 0.f ? v.w : 0.f;
                         }
                         if (EPI & NERF_EPI_ACCUM) v = xo[u] + v;
+#ifdef NERF_DIAG_NOSTORE
+                        if (v.x == 1234.5f)
+#endif
                         *reinterpret_cast<f4*>(o) = v;
                     } else {
 #pragma unroll
@@ -548,26 +589,41 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
         pass(3, acc[2], acc[3]);
     };
 
-    issue(0);
+    // prologue: A(0), W(0), A(1); iteration g issues W(g+1), A(g+2) and waits for A(g), W(g)
+    // (a loop, not three call sites: fewer inlined copies of the cursor code)
+    for (int q = 0; q < 3; ++q) {
+        if (q == 1) issue_w(0);
+        else if (q / 2 < total) issue_a(q / 2);
+    }
     zero_acc();
+    int as = 0, ws = 0;                 // ring slots of chunk g
     for (int g = 0; g < total; ++g) {
-        const bool more = g + 1 < total;
-        if (more) {
-            issue((g + 1) & 1);
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG) : "memory");   // chunk g landed, g+1 in flight
-        } else {
+        const int as2 = as == 0 ? 2 : as - 1;           // (g + 2) % 3
+        if (g + 2 < total) {
+            issue_w(ws ^ 1);
+            issue_a(as2);
+            if (loader) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * QA + QW) : "memory");
+        } else if (g + 1 < total) {
+            issue_w(ws ^ 1);
+            if (loader) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QA + QW) : "memory");
+        } else if (loader) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         barrier();                      // chunk g visible to every wave
-        compute(g & 1);
-        barrier();                      // every wave done reading stage g & 1
+#ifndef NERF_DIAG_NOCOMPUTE
+        compute(as, ws);
+#endif
+        barrier();                      // every wave done reading chunk g's stages
         if (++c_chunk == nchunks) {
-            epilogue(g & 1);
+            epilogue(as, ws);
             zero_acc();
             c_chunk = 0;
             c_tile += gridDim.x;
         }
+        as = as == 2 ? 0 : as + 1;
+        ws ^= 1;
     }
+#undef NERF_SEGF
 }
 
 // ------------------------------------------------------------------------- TN

@@ -135,6 +135,7 @@ def main():
               "nt256mask": lambda: bench_linear(M, 256, (256,), (1,), NERF_EPI_MASK),
               "wgrad256": lambda: bench_wgrad(M, 256, (256,), (1,)),
               "nt256x3": lambda: bench_linear(M, 256, (256,), (1,), x3=True),
+              "nt256maskx3": lambda: bench_linear(M, 256, (256,), (1,), NERF_EPI_MASK, x3=True),
               "wgrad256x3": lambda: bench_wgrad(M, 256, (256,), (1,), x3=True)}[args.only]
         print(json.dumps(fn()))
         return
