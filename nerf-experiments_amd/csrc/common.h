@@ -121,4 +121,105 @@ __device__ __forceinline__ float linspace_at(float start, float end, int steps, 
     return (idx < halfway) ? start + step * (float)idx : end - step * (float)(steps - idx - 1);
 }
 
+// ---------------------------------------------------------------------------
+// Epilogue of one output quad (columns n .. n+3 of row m) of the NT linear kernels
+// (nerf_linear_fwd / nerf_linear_fwd_x3), in a fixed operation order:
+//   v (+ bias) (ReLU) (* ReLU-backward mask) (+ out) -> out, then (MASKOUT) mask bits.
+// With NERF_EPI_MASKBITS / NERF_EPI_MASKOUT, aux is a bit mask (N <= 256): row m is 8 uint32
+// words at (char*)aux + m * ld_aux; bit b of word 2e + h is (activation at column
+// 4 (32 h + b) + e) > 0 — component-major, so that a wave's ballot over its lanes' quads is
+// one word.  Otherwise aux is the fp32 activation itself.
+typedef float epi_f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned quad_bits(epi_f4 v) {
+    return (v.x > 0.f ? 1u : 0u) | (v.y > 0.f ? 2u : 0u) | (v.z > 0.f ? 4u : 0u) | (v.w > 0.f ? 8u : 0u);
+}
+__device__ __forceinline__ epi_f4 apply_bits(epi_f4 v, unsigned b) {
+    v.x = (b & 1u) ? v.x : 0.f; v.y = (b & 2u) ? v.y : 0.f;
+    v.z = (b & 4u) ? v.z : 0.f; v.w = (b & 8u) ? v.w : 0.f;
+    return v;
+}
+__device__ __forceinline__ epi_f4 apply_sign(epi_f4 v, epi_f4 x) {
+    v.x = x.x > 0.f ? v.x : 0.f; v.y = x.y > 0.f ? v.y : 0.f;
+    v.z = x.z > 0.f ? v.z : 0.f; v.w = x.w > 0.f ? v.w : 0.f;
+    return v;
+}
+// 4-bit mask of quad q of a bit-mask row (vector loads)
+__device__ __forceinline__ unsigned load_quad_bits(const unsigned char* row, int q) {
+    const unsigned* w = reinterpret_cast<const unsigned*>(row) + (q >> 5);
+    const int b = q & 31;
+    return ((w[0] >> b) & 1u) | (((w[2] >> b) & 1u) << 1) | (((w[4] >> b) & 1u) << 2) | (((w[6] >> b) & 1u) << 3);
+}
+// Write the bits of a group of G consecutive lanes (G = 64, 32 or 8) holding consecutive
+// quads q0 .. q0+G-1 (q0 a multiple of G) of one row.  Every lane of the wave must call it.
+template <int G>
+__device__ __forceinline__ void store_quad_bits(unsigned char* row, bool row_ok, int q0, unsigned nib) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const unsigned long long b = __ballot((nib >> e) & 1u);
+        if (row_ok && (lane & (G - 1)) == 0) {
+            unsigned* w = reinterpret_cast<unsigned*>(row) + 2 * e + (q0 >> 5);
+            if (G == 64) {
+                w[0] = (unsigned)b;
+                w[1] = (unsigned)(b >> 32);
+            } else if (G == 32) {
+                w[0] = (unsigned)(b >> (lane & 32));
+            } else {
+                reinterpret_cast<unsigned char*>(w)[(q0 & 31) >> 3] = (unsigned char)(b >> (lane & 56));
+            }
+        }
+    }
+}
+
+struct EpiOut {
+    float* out; int64_t ldo;
+    const float* bias;
+    const void* aux; int64_t ldaux;
+    int M; int N; int epi; int vec_ok;
+};
+
+// Epilogue of one lane's quad (ok: the quad is in range); returns its (out > 0) bits.
+__device__ __forceinline__ unsigned epi_quad_lane(const EpiOut& E, int m, int n, epi_f4 v) {
+    const bool bits = (E.epi & (NERF_EPI_MASKBITS | NERF_EPI_MASKOUT)) != 0;
+    const unsigned char* mrow = (const unsigned char*)E.aux + (int64_t)m * E.ldaux;
+    float* o = E.out + (int64_t)m * E.ldo + n;
+    if (E.vec_ok && n + 4 <= E.N) {
+        if (E.epi & NERF_EPI_BIAS) v += *reinterpret_cast<const epi_f4*>(E.bias + n);
+        if (E.epi & NERF_EPI_RELU) {
+            v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        }
+        if (E.epi & NERF_EPI_MASK)
+            v = bits ? apply_bits(v, load_quad_bits(mrow, n >> 2))
+                     : apply_sign(v, *reinterpret_cast<const epi_f4*>((const float*)E.aux + (int64_t)m * E.ldaux + n));
+        if (E.epi & NERF_EPI_ACCUM) v = *reinterpret_cast<const epi_f4*>(o) + v;
+        *reinterpret_cast<epi_f4*>(o) = v;
+        return quad_bits(v);
+    }
+    const unsigned mb = (bits && (E.epi & NERF_EPI_MASK)) ? load_quad_bits(mrow, n >> 2) : 0u;
+    unsigned ob = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        if (n + e >= E.N) break;
+        float x = e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
+        if (E.epi & NERF_EPI_BIAS) x = x + E.bias[n + e];
+        if (E.epi & NERF_EPI_RELU) x = fmaxf(x, 0.f);
+        if (E.epi & NERF_EPI_MASK)
+            x = (bits ? ((mb >> e) & 1u) != 0u : ((const float*)E.aux)[(int64_t)m * E.ldaux + n + e] > 0.f) ? x : 0.f;
+        if (E.epi & NERF_EPI_ACCUM) x = o[e] + x;
+        o[e] = x;
+        ob |= (x > 0.f ? 1u : 0u) << e;
+    }
+    return ob;
+}
+
+// Quad epilogue for kernels whose epilogue maps G consecutive lanes to G consecutive quads
+// of one row (G-aligned).  Every lane of the wave calls it; ok = this lane's quad is in range.
+template <int G>
+__device__ __forceinline__ void epi_quad(const EpiOut& E, bool ok, int m, int n, epi_f4 v) {
+    const unsigned nib = ok ? epi_quad_lane(E, m, n, v) : 0u;
+    if (E.epi & NERF_EPI_MASKOUT)
+        store_quad_bits<G>((unsigned char*)E.aux + (int64_t)m * E.ldaux, m < E.M, (n >> 2) & ~(G - 1), nib);
+}
+
 }  // namespace nerf

@@ -105,6 +105,7 @@ __device__ __forceinline__ bool tile_coords(int tile, int ntm, int ntn, int& tm,
 // stages the accumulators through the idle LDS buffer, 64 rows at a time.
 template <int BN>
 __global__ __launch_bounds__(256, 2) void linear_nt_kernel(NTArgs a, int ntm, int ntiles) {
+    const EpiOut E{a.out, a.ldo, a.bias, a.aux, a.ldaux, a.M, a.N, a.epi, a.vec_ok};
     using Cfg = TileCfg<BN>;
     constexpr int BM = Cfg::BM, WM = Cfg::WM, WN = Cfg::WN;
     constexpr int MB = WM / 32, NB = WN / 32;   // MFMA blocks per wave
@@ -277,33 +278,7 @@ __global__ __launch_bounds__(256, 2) void linear_nt_kernel(NTArgs a, int ntm, in
                 const int row = q / Q, cq = q - (q / Q) * Q;
                 const int m = m0 + h * HR + row;
                 const int n = n0 + cq * 4;
-                if (m >= a.M || n >= a.N) continue;
-                f4 v = *reinterpret_cast<const f4*>(Cs + row * LDC + cq * 4);
-                float* o = a.out + (int64_t)m * a.ldo + n;
-                if (a.vec_ok && n + 4 <= a.N) {
-                    if (a.epi & NERF_EPI_BIAS) v += *reinterpret_cast<const f4*>(a.bias + n);
-                    if (a.epi & NERF_EPI_RELU) {
-                        v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
-                    }
-                    if (a.epi & NERF_EPI_MASK) {
-                        const f4 x = *reinterpret_cast<const f4*>(a.aux + (int64_t)m * a.ldaux + n);
-                        v.x = x.x > 0.f ? v.x : 0.f; v.y = x.y > 0.f ? v.y : 0.f;
-                        v.z = x.z > 0.f ? v.z : 0.f; v.w = x.w > 0.f ? v.w : 0.f;
-                    }
-                    if (a.epi & NERF_EPI_ACCUM) v = *reinterpret_cast<const f4*>(o) + v;
-                    *reinterpret_cast<f4*>(o) = v;
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        if (n + e >= a.N) break;
-                        float x = e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
-                        if (a.epi & NERF_EPI_BIAS) x = x + a.bias[n + e];
-                        if (a.epi & NERF_EPI_RELU) x = fmaxf(x, 0.f);
-                        if (a.epi & NERF_EPI_MASK) x = (a.aux[(int64_t)m * a.ldaux + n + e] > 0.f) ? x : 0.f;
-                        if (a.epi & NERF_EPI_ACCUM) x = o[e] + x;
-                        o[e] = x;
-                    }
-                }
+                epi_quad<BN / 4>(E, m < a.M && n < a.N, m, n, *reinterpret_cast<const f4*>(Cs + row * LDC + cq * 4));
             }
             __syncthreads();
         }
@@ -572,9 +547,12 @@ extern "C" int nerf_linear_fwd(const nerf_seg* segs, int32_t n_segs, int64_t M, 
     NERF_REQUIRE(build_segs(segs, n_segs, L));
     NERF_REQUIRE(W && out && aligned16(W) && ldw == L.ktot && (ldw % 4) == 0 && ldo >= N);
     if (epilogue & NERF_EPI_BIAS) NERF_REQUIRE(bias != nullptr);
-    if (epilogue & NERF_EPI_MASK) NERF_REQUIRE(aux != nullptr && ld_aux >= N);
+    const bool mbits = (epilogue & (NERF_EPI_MASKBITS | NERF_EPI_MASKOUT)) != 0;
+    if (mbits) NERF_REQUIRE(aux != nullptr && N <= 256 && ld_aux >= 32 && (ld_aux % 4) == 0 && aligned16(aux));
+    if (epilogue & NERF_EPI_MASK) NERF_REQUIRE(aux != nullptr && (mbits || ld_aux >= N));
+    if (epilogue & NERF_EPI_MASKOUT) NERF_REQUIRE(!(epilogue & NERF_EPI_MASK));
     const int vec_ok = aligned16(out) && (ldo % 4) == 0 && (!(epilogue & NERF_EPI_BIAS) || aligned16(bias)) &&
-                       (!(epilogue & NERF_EPI_MASK) || (aligned16(aux) && (ld_aux % 4) == 0));
+                       (!(epilogue & NERF_EPI_MASK) || mbits || (aligned16(aux) && (ld_aux % 4) == 0));
     NTArgs a{L, (int)M, W, ldw, N, bias, out, ldo, epilogue, aux, ld_aux, vec_ok};
     const int ntm = (int)((M + 127) / 128);
     const int ntn = N <= 32 ? 1 : (N + 127) / 128;

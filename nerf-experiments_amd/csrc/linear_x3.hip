@@ -103,6 +103,7 @@ struct NTArgs {
 
 // ------------------------------------------------------------------------- NT
 __global__ __launch_bounds__(256, 2) void linear_nt_x3_kernel(NTArgs a, int ntm, int ntiles) {
+    const EpiOut E{a.out, a.ldo, a.bias, a.aux, a.ldaux, a.M, a.N, a.epi, a.vec_ok};
     constexpr int BM = 128, BN = 128;
     constexpr int PL = BM * LDB;                 // one bf16 plane (128 rows)
     constexpr int BUFB = 4 * PL;                 // A hi, A lo, W hi, W lo (bf16 elements)
@@ -275,33 +276,7 @@ __global__ __launch_bounds__(256, 2) void linear_nt_x3_kernel(NTArgs a, int ntm,
                 const int row = q / Q, cq = q - (q / Q) * Q;
                 const int m = m0 + h * HR + row;
                 const int n = n0 + cq * 4;
-                if (m >= a.M || n >= a.N) continue;
-                f4 v = *reinterpret_cast<const f4*>(Cs + row * LDC + cq * 4);
-                float* o = a.out + (int64_t)m * a.ldo + n;
-                if (a.vec_ok && n + 4 <= a.N) {
-                    if (a.epi & NERF_EPI_BIAS) v += *reinterpret_cast<const f4*>(a.bias + n);
-                    if (a.epi & NERF_EPI_RELU) {
-                        v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
-                    }
-                    if (a.epi & NERF_EPI_MASK) {
-                        const f4 x = *reinterpret_cast<const f4*>(a.aux + (int64_t)m * a.ldaux + n);
-                        v.x = x.x > 0.f ? v.x : 0.f; v.y = x.y > 0.f ? v.y : 0.f;
-                        v.z = x.z > 0.f ? v.z : 0.f; v.w = x.w > 0.f ? v.w : 0.f;
-                    }
-                    if (a.epi & NERF_EPI_ACCUM) v = *reinterpret_cast<const f4*>(o) + v;
-                    *reinterpret_cast<f4*>(o) = v;
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        if (n + e >= a.N) break;
-                        float x = e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
-                        if (a.epi & NERF_EPI_BIAS) x = x + a.bias[n + e];
-                        if (a.epi & NERF_EPI_RELU) x = fmaxf(x, 0.f);
-                        if (a.epi & NERF_EPI_MASK) x = (a.aux[(int64_t)m * a.ldaux + n + e] > 0.f) ? x : 0.f;
-                        if (a.epi & NERF_EPI_ACCUM) x = o[e] + x;
-                        o[e] = x;
-                    }
-                }
+                epi_quad<BN / 4>(E, m < a.M && n < a.N, m, n, *reinterpret_cast<const f4*>(Cs + row * LDC + cq * 4));
             }
             __syncthreads();
         }
@@ -494,16 +469,13 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
     const int ec4 = et % C4, erow = et / C4;
     const int en = ec4 * 4;
     f4 bias4 = f4{0.f, 0.f, 0.f, 0.f};
-    if ((EPI & NERF_EPI_BIAS) && en < a.N) {
-        if (a.vec_ok && en + 4 <= a.N) {
-            bias4 = *reinterpret_cast<const f4*>(a.bias + en);
-        } else {
-            bias4.x = a.bias[en];
-            bias4.y = en + 1 < a.N ? a.bias[en + 1] : 0.f;
-            bias4.z = en + 2 < a.N ? a.bias[en + 2] : 0.f;
-            bias4.w = en + 3 < a.N ? a.bias[en + 3] : 0.f;
-        }
-    }
+    if ((EPI & NERF_EPI_BIAS) && a.vec_ok && en + 4 <= a.N) bias4 = *reinterpret_cast<const f4*>(a.bias + en);
+    const EpiOut E{a.out, a.ldo, a.bias, a.aux, a.ldaux, a.M, a.N,
+                   EPI | (a.epi & (NERF_EPI_MASKBITS | NERF_EPI_MASKOUT)), a.vec_ok};
+    const bool mbits = (a.epi & NERF_EPI_MASKBITS) != 0, mout = (a.epi & NERF_EPI_MASKOUT) != 0;
+    unsigned char* mask8 = (unsigned char*)a.aux;
+    typedef __attribute__((address_space(4))) const unsigned kmask_t;      // scalar-load view
+    const kmask_t* mrows = (const kmask_t*)(uintptr_t)a.aux;
     auto barrier = []() __attribute__((always_inline)) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -530,55 +502,69 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
             }
             barrier();
             // aux / out reads of a batch of rows are issued together (one memory round trip
-            // per batch instead of one per row)
+            // per batch instead of one per row); bit masks are read with SCALAR loads (a wave's
+            // lanes share one or two rows), which count on lgkmcnt and so never wait for the
+            // LDS-DMA prefetch that the in-order vmcnt would otherwise drain
             if (storer)
 #pragma unroll
             for (int qb = 0; qb < 64 / RS; qb += 4) {
                 f4 xa[4], xo[4];
+                unsigned xb[4];
                 if (vec && (EPI & (NERF_EPI_MASK | NERF_EPI_ACCUM))) {
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         int m = tm0 + 64 * p + erow + RS * (qb + u);
                         m = m < a.M ? m : a.M - 1;
-                        if (EPI & NERF_EPI_MASK) xa[u] = *reinterpret_cast<const f4*>(a.aux + (int64_t)m * a.ldaux + en);
+                        if ((EPI & NERF_EPI_MASK) && !mbits)
+                            xa[u] = *reinterpret_cast<const f4*>(a.aux + (int64_t)m * a.ldaux + en);
                         if (EPI & NERF_EPI_ACCUM) xo[u] = *reinterpret_cast<const f4*>(a.out + (int64_t)m * a.ldo + en);
+                    }
+                }
+                if ((EPI & NERF_EPI_MASK) && mbits) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        // rows of lanes 0 and 32 (the same row when a wave spans one row)
+                        int m0r = tm0 + 64 * p + __builtin_amdgcn_readfirstlane(erow) + RS * (qb + u);
+                        int m1r = tm0 + 64 * p + __builtin_amdgcn_readlane(erow, 32) + RS * (qb + u);
+                        m0r = m0r < a.M ? m0r : a.M - 1;
+                        m1r = m1r < a.M ? m1r : a.M - 1;
+                        const kmask_t* r0 = mrows + (int64_t)m0r * (a.ldaux >> 2);
+                        const kmask_t* r1 = mrows + (int64_t)m1r * (a.ldaux >> 2);
+                        const int h = ec4 >> 5, b = ec4 & 31;
+                        const bool hi_half = (lane >> 5) != 0 && C4 == 32;
+                        unsigned nib = 0;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            // uniform addresses (scalar loads), per-lane selects afterwards
+                            const unsigned w0l = r0[2 * e], w0h = r0[2 * e + 1], w1 = r1[2 * e];
+                            const unsigned w = hi_half ? w1 : (h ? w0h : w0l);
+                            nib |= ((w >> b) & 1u) << e;
+                        }
+                        xb[u] = nib;
                     }
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int row = erow + RS * (qb + u);
                     const int m = tm0 + 64 * p + row;
-                    if (m >= a.M || en >= a.N) continue;
+                    const bool ok = m < a.M && en < a.N;
                     const float* Cr = row < 32 ? C0 + row * BN : C1 + (row - 32) * BN;
                     f4 v = *reinterpret_cast<const f4*>(Cr + en);
-                    float* o = a.out + (int64_t)m * a.ldo + en;
-                    if (vec) {
+                    unsigned nib = 0;
+                    if (ok && vec) {
+                        float* o = a.out + (int64_t)m * a.ldo + en;
                         if (EPI & NERF_EPI_BIAS) v += bias4;
                         if (EPI & NERF_EPI_RELU) {
                             v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
                         }
-                        if (EPI & NERF_EPI_MASK) {
-                            const f4 x = xa[u];
-                            v.x = x.x > 0.f ? v.x : 0.f; v.y = x.y > 0.f ? v.y : 0.f;
-                            v.z = x.z > 0.f ? v.z : 0.f; v.w = x.w > 0.f ? v.w : 0.f;
-                        }
+                        if (EPI & NERF_EPI_MASK) v = mbits ? apply_bits(v, xb[u]) : apply_sign(v, xa[u]);
                         if (EPI & NERF_EPI_ACCUM) v = xo[u] + v;
-#ifdef NERF_DIAG_NOSTORE
-                        if (v.x == 1234.5f)
-#endif
                         *reinterpret_cast<f4*>(o) = v;
-                    } else {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            if (en + e >= a.N) break;
-                            float x = e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
-                            if (EPI & NERF_EPI_BIAS) x = x + (e == 0 ? bias4.x : (e == 1 ? bias4.y : (e == 2 ? bias4.z : bias4.w)));
-                            if (EPI & NERF_EPI_RELU) x = fmaxf(x, 0.f);
-                            if (EPI & NERF_EPI_MASK) x = (a.aux[(int64_t)m * a.ldaux + en + e] > 0.f) ? x : 0.f;
-                            if (EPI & NERF_EPI_ACCUM) x = o[e] + x;
-                            o[e] = x;
-                        }
+                        nib = quad_bits(v);
+                    } else if (ok) {
+                        nib = epi_quad_lane(E, m, en, v);      // partial / unaligned quads (bias from memory)
                     }
+                    if (mout) store_quad_bits<C4>(mask8 + (int64_t)m * a.ldaux, m < a.M, 0, nib);
                 }
             }
             barrier();
@@ -1037,9 +1023,12 @@ extern "C" int nerf_linear_fwd_x3(const nerf_seg* segs, int32_t n_segs, int64_t 
     NERF_REQUIRE(build_segs(segs, n_segs, L));
     NERF_REQUIRE(W_x && out && aligned16(W_x) && ldw == L.ktot && (ldw % BK) == 0 && ldo >= N);
     if (epilogue & NERF_EPI_BIAS) NERF_REQUIRE(bias != nullptr);
-    if (epilogue & NERF_EPI_MASK) NERF_REQUIRE(aux != nullptr && ld_aux >= N);
+    const bool mbits = (epilogue & (NERF_EPI_MASKBITS | NERF_EPI_MASKOUT)) != 0;
+    if (mbits) NERF_REQUIRE(aux != nullptr && N <= 256 && ld_aux >= 32 && (ld_aux % 4) == 0 && aligned16(aux));
+    if (epilogue & NERF_EPI_MASK) NERF_REQUIRE(aux != nullptr && (mbits || ld_aux >= N));
+    if (epilogue & NERF_EPI_MASKOUT) NERF_REQUIRE(!(epilogue & NERF_EPI_MASK));
     const int vec_ok = aligned16(out) && (ldo % 4) == 0 && (!(epilogue & NERF_EPI_BIAS) || aligned16(bias)) &&
-                       (!(epilogue & NERF_EPI_MASK) || (aligned16(aux) && (ld_aux % 4) == 0));
+                       (!(epilogue & NERF_EPI_MASK) || mbits || (aligned16(aux) && (ld_aux % 4) == 0));
     NTArgs a{L, (int)M, reinterpret_cast<const __bf16*>(W_x), ldw, N, bias, out, ldo, epilogue, aux, ld_aux, vec_ok};
     hipStream_t st = as_stream(stream);
     if (N <= 256 && !(epilogue & NERF_EPI_NARROW_TILE)) {

@@ -28,6 +28,8 @@ NERF_EPI_BIAS = 1
 NERF_EPI_RELU = 2
 NERF_EPI_MASK = 4
 NERF_EPI_ACCUM = 8
+NERF_EPI_MASKBITS = 16
+NERF_EPI_MASKOUT = 32
 NERF_EPI_NO_PERSIST = 256
 NERF_EPI_NARROW_TILE = 512
 

@@ -13,7 +13,8 @@ the input-gradient GEMMs) only when a parameter's version counter changed.
             layer outputs kept for backward;
   backward: per layer (in reverse) one ``nerf_linear_wgrad`` + reduce for
             (dW, db) and one ``nerf_linear_fwd`` per consumed source for dX,
-            with the ReLU mask of the producing layer fused into its epilogue.
+            with the ReLU mask of the producing layer fused into its epilogue (read
+            as the bit mask the forward epilogue wrote, 1 bit per activation).
 """
 from __future__ import annotations
 
@@ -23,7 +24,8 @@ import torch
 import torch.nn as nn
 
 from . import kernels as K
-from ._lib import NERF_EPI_ACCUM, NERF_EPI_BIAS, NERF_EPI_MASK, NERF_EPI_RELU
+from ._lib import (NERF_EPI_ACCUM, NERF_EPI_BIAS, NERF_EPI_MASK, NERF_EPI_MASKBITS, NERF_EPI_MASKOUT,
+                   NERF_EPI_RELU)
 
 
 def matmul_precision() -> str:
@@ -170,7 +172,8 @@ class MLPFunction(torch.autograd.Function):
         plan.to_device(pos.device)
         prec = matmul_precision()
         acts: list[torch.Tensor] = []
-        for lp in plan.layers:
+        masks: list[torch.Tensor | None] = []
+        for idx, lp in enumerate(plan.layers):
             lp.pack(prec)
             segs = []
             for s in lp.sources:
@@ -178,8 +181,16 @@ class MLPFunction(torch.autograd.Function):
                 segs.append((t, s.k_seg, rd))
             out = torch.empty(M, lp.out_ld, device=pos.device, dtype=torch.float32)
             epi = NERF_EPI_BIAS | (NERF_EPI_RELU if lp.relu else 0)
-            lp.gemm(prec, segs, M, False, lp.N, lp.module.bias, out, epi)
+            mask = None
+            if lp.relu and plan.consumed[idx] and lp.N <= 256:
+                # the ReLU-backward mask of this output as bits (32 bytes a row): the input-
+                # gradient GEMMs read it instead of the fp32 activation
+                mask = torch.empty(M, 32, device=pos.device, dtype=torch.uint8)
+                epi |= NERF_EPI_MASKOUT
+            lp.gemm(prec, segs, M, False, lp.N, lp.module.bias, out, epi, aux=mask)
             acts.append(out)
+            masks.append(mask)
+        ctx.masks = masks
         ctx.prec = prec
         ctx.plan = plan
         ctx.M = M
@@ -250,8 +261,12 @@ class MLPFunction(torch.autograd.Function):
                     epi = 0
                     aux = None
                     if prod.relu:
-                        epi |= NERF_EPI_MASK
-                        aux = acts[j]
+                        if ctx.masks[j] is not None:
+                            epi |= NERF_EPI_MASK | NERF_EPI_MASKBITS
+                            aux = ctx.masks[j]
+                        else:
+                            epi |= NERF_EPI_MASK
+                            aux = acts[j]
                     if dY[j] is None:
                         if prod.out_ld > s.k_valid:
                             dY[j] = torch.zeros(M, prod.out_ld, device=dev, dtype=torch.float32)

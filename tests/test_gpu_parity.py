@@ -260,6 +260,7 @@ def test_linear_fwd_wgrad(M, N, ks, rd):
     K.linear_fwd(segs, M, Wp.to(DEV), Kp, N, None, o2, NERF_EPI_MASK | NERF_EPI_ACCUM, aux=aux.to(DEV))
     ref2 = out2[:, :N] + (X @ W.T) * (aux[:, :N] > 0)
     np.testing.assert_allclose(o2[:, :N].cpu().numpy(), ref2.numpy(), atol=1e-4, rtol=1e-4)
+    _check_mask_bits(lambda *a, **k: K.linear_fwd(segs, M, Wp.to(DEV), Kp, *a, **k), M, N, ldo, b, aux, out2)
     # weight gradient, scattered through the column map
     dY = torch.randn(M, ldo)
     dY[:, N:] = 0
@@ -272,6 +273,40 @@ def test_linear_fwd_wgrad(M, N, ks, rd):
     np.testing.assert_allclose(dW.cpu().numpy(), (dY[:, :N].T.double() @ X.double()).float().numpy(), atol=2e-4,
                                rtol=1e-4)
     np.testing.assert_allclose(db.cpu().numpy(), dY[:, :N].sum(0).numpy(), atol=2e-4, rtol=1e-4)
+
+
+def _check_mask_bits(fwd, M, N, ldo, b, aux, out2):
+    """NERF_EPI_MASKOUT writes (out > 0) as bits — row m = 8 uint32 words, bit b of word
+    2e + h <-> column 4(32h + b) + e; a MASK epilogue reading those bits (NERF_EPI_MASKBITS)
+    equals the one reading the fp32 activation."""
+    from nerf_amd._lib import NERF_EPI_ACCUM, NERF_EPI_BIAS, NERF_EPI_MASK, NERF_EPI_MASKBITS, NERF_EPI_MASKOUT, \
+        NERF_EPI_RELU
+    if N > 256:
+        return
+    act = torch.empty(M, ldo, device=DEV)
+    bits = torch.full((M, 32), 0xA5, dtype=torch.uint8, device=DEV)
+    fwd(N, b.to(DEV), act, NERF_EPI_BIAS | NERF_EPI_RELU | NERF_EPI_MASKOUT, aux=bits)
+    pos = torch.zeros(M, 256, dtype=torch.int64)
+    pos[:, :N] = (act[:, :N] > 0).cpu().long()
+    q = pos.view(M, 64, 4)                                  # [m][quad][e]
+    want = torch.zeros(M, 8, dtype=torch.int64)
+    for e in range(4):
+        for h in range(2):
+            want[:, 2 * e + h] = (q[:, 32 * h:32 * h + 32, e] << torch.arange(32)).sum(1)
+    got = bits.cpu().view(torch.int32).long() & 0xFFFFFFFF
+    nq = (N + 3) // 4                                       # bits of quads past N are unspecified
+    for h in range(2):
+        nb = min(max(nq - 32 * h, 0), 32)
+        valid = (1 << nb) - 1
+        for e in range(4):
+            assert torch.equal(got[:, 2 * e + h] & valid, want[:, 2 * e + h] & valid), (e, h)
+    # the same masked + accumulated product through float aux and through the bits
+    act_aux = act.clone()
+    o_f = out2.clone().to(DEV)
+    o_b = out2.clone().to(DEV)
+    fwd(N, None, o_f, NERF_EPI_MASK | NERF_EPI_ACCUM, aux=act_aux)
+    fwd(N, None, o_b, NERF_EPI_MASK | NERF_EPI_MASKBITS | NERF_EPI_ACCUM, aux=bits)
+    assert torch.equal(o_f[:, :N], o_b[:, :N])
 
 
 def _split_bf16(W):
@@ -336,6 +371,7 @@ def test_linear_x3_fwd_wgrad(M, N, ks, rd):
     ref2 = out2[:, :N].double() + (Xd @ Wd.T) * (aux[:, :N] > 0)
     err = (o2[:, :N].cpu().double() - ref2).abs()
     assert (err <= bound + 1e-6).all(), float((err - bound).max())
+    _check_mask_bits(lambda *a, **k: K.linear_fwd_x3(segs, M, Wpx, Kp, *a, **k), M, N, ldo, b, aux, out2)
     # transposed (input-gradient) direction through Wt planes: dX = dY @ W
     dY = torch.randn(M, ldo)
     dY[:, N:] = 0

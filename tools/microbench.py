@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "nerf-experiments_amd"))
 
 from nerf_amd import kernels as K  # noqa: E402
-from nerf_amd._lib import NERF_EPI_BIAS, NERF_EPI_MASK, NERF_EPI_RELU  # noqa: E402
+from nerf_amd._lib import NERF_EPI_BIAS, NERF_EPI_MASK, NERF_EPI_MASKBITS, NERF_EPI_MASKOUT, NERF_EPI_RELU  # noqa: E402
 
 NERF_EPI_NO_PERSIST = 256
 NERF_EPI_NARROW_TILE = 512
@@ -51,6 +51,8 @@ def bench_linear(M, N, ks, rd, epi=NERF_EPI_BIAS | NERF_EPI_RELU, x3=False):
     ldo = (N + 3) // 4 * 4
     out = torch.empty(M, ldo, device=DEV)
     aux = torch.randn(M, ldo, device=DEV) if epi & NERF_EPI_MASK else None
+    if epi & NERF_EPI_MASKBITS:
+        aux = torch.randint(0, 256, (M, 32), dtype=torch.uint8, device=DEV)
     fl = 2.0 * M * N * sum(ks)
     if x3:
         Wh = W.bfloat16()
@@ -136,6 +138,7 @@ def main():
               "wgrad256": lambda: bench_wgrad(M, 256, (256,), (1,)),
               "nt256x3": lambda: bench_linear(M, 256, (256,), (1,), x3=True),
               "nt256maskx3": lambda: bench_linear(M, 256, (256,), (1,), NERF_EPI_MASK, x3=True),
+              "nt256bitsx3": lambda: bench_linear(M, 256, (256,), (1,), NERF_EPI_MASK | NERF_EPI_MASKBITS, x3=True),
               "wgrad256x3": lambda: bench_wgrad(M, 256, (256,), (1,), x3=True)}[args.only]
         print(json.dumps(fn()))
         return
@@ -149,7 +152,8 @@ def main():
             res.append(bench_linear(M, 4, (128,), (1,), NERF_EPI_BIAS))
         # input-gradient layers
         res.append(bench_linear(M, 256, (256,), (1,), NERF_EPI_MASK, x3=x3))
-        res.append(bench_linear(M, 128, (4,), (1,), NERF_EPI_MASK, x3=x3))
+        res.append(bench_linear(M, 256, (256,), (1,), NERF_EPI_MASK | NERF_EPI_MASKBITS, x3=x3))
+        res.append(bench_linear(M, 128, (4,), (1,), NERF_EPI_MASK | NERF_EPI_MASKBITS, x3=x3))
         res.append(bench_linear(M, 256, (128,), (1,), 0, x3=x3))
         # weight gradients
         res.append(bench_wgrad(M, 256, (256,), (1,), x3=x3))
