@@ -109,7 +109,10 @@ class LayerPlan:
     def pack(self, precision: str = "fp32"):
         w = self.module.weight
         ver = (w._version, w.data_ptr())
-        if ver != self.packed_version:
+        # in split precision the fp32 packs only serve GEMMs with <= 32 output columns: this
+        # layer's forward (N <= 32) and the input gradients of sources <= 32 columns wide
+        need_fp32 = precision != "x3" or self.N <= 32 or any(s.k_pad <= 32 for s in self.sources)
+        if need_fp32 and ver != self.packed_version:
             K.pack_weight(w.detach().contiguous(), self.col_map, self.Kp, self.Wp, self.Wt, self.ldwt)
             self.packed_version = ver
         if precision == "x3" and ver != self.packed_version_x3:
