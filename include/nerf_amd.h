@@ -185,7 +185,7 @@ typedef struct nerf_seg {
 #define NERF_EPI_MASKBITS 16 /* with MASK: aux is the bit mask written by MASKOUT */
 #define NERF_EPI_MASKOUT  32 /* also write (out > 0) as a bit mask into aux (N <= 256): row m
                                 is 8 uint32 words at (char*)aux + m*ld_aux (ld_aux >= 32 bytes,
-                                multiple of 4); bit b of word 2e+h <-> column 4(32h+b)+e */
+                                multiple of 16); bit b of word 2e+h <-> column 4(32h+b)+e */
 #define NERF_EPI_NO_PERSIST 256  /* tuning: one tile per workgroup instead of a persistent grid */
 #define NERF_EPI_NARROW_TILE 512 /* tuning: force the 128-column tile of the split-precision kernel for N > 128 */
 

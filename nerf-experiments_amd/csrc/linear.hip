@@ -548,7 +548,7 @@ extern "C" int nerf_linear_fwd(const nerf_seg* segs, int32_t n_segs, int64_t M, 
     NERF_REQUIRE(W && out && aligned16(W) && ldw == L.ktot && (ldw % 4) == 0 && ldo >= N);
     if (epilogue & NERF_EPI_BIAS) NERF_REQUIRE(bias != nullptr);
     const bool mbits = (epilogue & (NERF_EPI_MASKBITS | NERF_EPI_MASKOUT)) != 0;
-    if (mbits) NERF_REQUIRE(aux != nullptr && N <= 256 && ld_aux >= 32 && (ld_aux % 4) == 0 && aligned16(aux));
+    if (mbits) NERF_REQUIRE(aux != nullptr && N <= 256 && ld_aux >= 32 && (ld_aux % 16) == 0 && aligned16(aux));
     if (epilogue & NERF_EPI_MASK) NERF_REQUIRE(aux != nullptr && (mbits || ld_aux >= N));
     if (epilogue & NERF_EPI_MASKOUT) NERF_REQUIRE(!(epilogue & NERF_EPI_MASK));
     const int vec_ok = aligned16(out) && (ldo % 4) == 0 && (!(epilogue & NERF_EPI_BIAS) || aligned16(bias)) &&

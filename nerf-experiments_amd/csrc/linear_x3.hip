@@ -380,7 +380,6 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
     };
     a_locate(true);
     const bool loader = wave < LW;
-    const bool storer = LW == 8 || !loader;
     auto issue_a = [&](int stage) __attribute__((always_inline)) {
         char* base = Aring + stage * ABYTES;
         if (loader)
@@ -474,8 +473,6 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
                    EPI | (a.epi & (NERF_EPI_MASKBITS | NERF_EPI_MASKOUT)), a.vec_ok};
     const bool mbits = (a.epi & NERF_EPI_MASKBITS) != 0, mout = (a.epi & NERF_EPI_MASKOUT) != 0;
     unsigned char* mask8 = (unsigned char*)a.aux;
-    typedef __attribute__((address_space(4))) const unsigned kmask_t;      // scalar-load view
-    const kmask_t* mrows = (const kmask_t*)(uintptr_t)a.aux;
     auto barrier = []() __attribute__((always_inline)) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -483,70 +480,69 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
     };
     // epilogue: 64 rows per pass, rows 0-31 in the free A stage, 32-63 in the free W stage
     int c_tile = blockIdx.x, c_chunk = 0;
+    // Epilogue: PR rows per pass through the free A stage (C0, rows 0-31) and the free W stage
+    // (C1, rows 32-63 of a 64-row pass).  Masked variants use 32-row passes and stage the tile's
+    // 256 rows of ReLU mask bits (8 KB) in C1 with one LDS-DMA per thread up front: one memory
+    // round trip per tile instead of one per batch of rows.
+    constexpr bool MSK = (EPI & NERF_EPI_MASK) != 0;
+    constexpr int PR = MSK ? 32 : 64;
+    static_assert(32 * BN * 4 <= ABYTES && 32 * BN * 4 <= WBYTES && BM * 32 <= WBYTES, "epilogue staging");
     auto epilogue = [&](int astage, int wstage) __attribute__((always_inline)) {
-        static_assert(32 * BN * 4 <= ABYTES && 32 * BN * 4 <= WBYTES, "epilogue pass must fit the free stages");
         float* C0 = reinterpret_cast<float*>(Aring + astage * ABYTES);
         float* C1 = reinterpret_cast<float*>(Wring + wstage * WBYTES);
+        const unsigned* mbits_lds = reinterpret_cast<const unsigned*>(C1);
         const int tm0 = c_tile * BM;
         const bool vec = a.vec_ok && en + 4 <= a.N;
-        auto pass = [&](int p, const f32x16 (&c)[JN], const f32x16 (&d)[JN]) __attribute__((always_inline)) {
-            if (wr == (p >> 1)) {
+        if (MSK && mbits) {
+            int m = tm0 + (t >> 1);
+            m = m < a.M ? m : a.M - 1;
+            const char* src = reinterpret_cast<const char*>(a.aux) + (int64_t)m * a.ldaux + (t & 1) * 16;
+            __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(reinterpret_cast<char*>(C1) + wave * 1024),
+                                             16, 0, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        // rows r0 .. r0+PR-1 of the tile; acc blocks c (rows 0-31) and d (rows 32-63, PR = 64)
+        auto pass = [&](int r0, int wr_owner, const f32x16 (&c)[JN], const f32x16 (&d)[JN]) __attribute__((always_inline)) {
+            if (wr == wr_owner) {
 #pragma unroll
                 for (int j = 0; j < JN; ++j)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
                         C0[row * BN + wc * (BN / 4) + j * 32 + li] = c[j][r];
-                        C1[row * BN + wc * (BN / 4) + j * 32 + li] = d[j][r];
+                        if (PR == 64) C1[row * BN + wc * (BN / 4) + j * 32 + li] = d[j][r];
                     }
             }
             barrier();
             // aux / out reads of a batch of rows are issued together (one memory round trip
-            // per batch instead of one per row); bit masks are read with SCALAR loads (a wave's
-            // lanes share one or two rows), which count on lgkmcnt and so never wait for the
-            // LDS-DMA prefetch that the in-order vmcnt would otherwise drain
-            if (storer)
+            // per batch instead of one per row)
+            constexpr int UB = PR / RS < 4 ? PR / RS : 4;       // rows per batch
 #pragma unroll
-            for (int qb = 0; qb < 64 / RS; qb += 4) {
-                f4 xa[4], xo[4];
-                unsigned xb[4];
+            for (int qb = 0; qb < PR / RS; qb += UB) {
+                f4 xa[UB], xo[UB];
+                unsigned xb[UB];
                 if (vec && (EPI & (NERF_EPI_MASK | NERF_EPI_ACCUM))) {
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        int m = tm0 + 64 * p + erow + RS * (qb + u);
+                    for (int u = 0; u < UB; ++u) {
+                        int m = tm0 + r0 + erow + RS * (qb + u);
                         m = m < a.M ? m : a.M - 1;
-                        if ((EPI & NERF_EPI_MASK) && !mbits)
-                            xa[u] = *reinterpret_cast<const f4*>(a.aux + (int64_t)m * a.ldaux + en);
+                        if (MSK && !mbits) xa[u] = *reinterpret_cast<const f4*>(a.aux + (int64_t)m * a.ldaux + en);
                         if (EPI & NERF_EPI_ACCUM) xo[u] = *reinterpret_cast<const f4*>(a.out + (int64_t)m * a.ldo + en);
                     }
                 }
-                if ((EPI & NERF_EPI_MASK) && mbits) {
+                if (MSK && mbits) {
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        // rows of lanes 0 and 32 (the same row when a wave spans one row)
-                        int m0r = tm0 + 64 * p + __builtin_amdgcn_readfirstlane(erow) + RS * (qb + u);
-                        int m1r = tm0 + 64 * p + __builtin_amdgcn_readlane(erow, 32) + RS * (qb + u);
-                        m0r = m0r < a.M ? m0r : a.M - 1;
-                        m1r = m1r < a.M ? m1r : a.M - 1;
-                        const kmask_t* r0 = mrows + (int64_t)m0r * (a.ldaux >> 2);
-                        const kmask_t* r1 = mrows + (int64_t)m1r * (a.ldaux >> 2);
-                        const int h = ec4 >> 5, b = ec4 & 31;
-                        const bool hi_half = (lane >> 5) != 0 && C4 == 32;
-                        unsigned nib = 0;
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            // uniform addresses (scalar loads), per-lane selects afterwards
-                            const unsigned w0l = r0[2 * e], w0h = r0[2 * e + 1], w1 = r1[2 * e];
-                            const unsigned w = hi_half ? w1 : (h ? w0h : w0l);
-                            nib |= ((w >> b) & 1u) << e;
-                        }
-                        xb[u] = nib;
+                    for (int u = 0; u < UB; ++u) {
+                        const unsigned* wrow = mbits_lds + (r0 + erow + RS * (qb + u)) * 8 + (ec4 >> 5);
+                        const int b = ec4 & 31;
+                        xb[u] = ((wrow[0] >> b) & 1u) | (((wrow[2] >> b) & 1u) << 1) | (((wrow[4] >> b) & 1u) << 2) |
+                                (((wrow[6] >> b) & 1u) << 3);
                     }
                 }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < UB; ++u) {
                     const int row = erow + RS * (qb + u);
-                    const int m = tm0 + 64 * p + row;
+                    const int m = tm0 + r0 + row;
                     const bool ok = m < a.M && en < a.N;
                     const float* Cr = row < 32 ? C0 + row * BN : C1 + (row - 32) * BN;
                     f4 v = *reinterpret_cast<const f4*>(Cr + en);
@@ -557,7 +553,7 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
                         if (EPI & NERF_EPI_RELU) {
                             v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
                         }
-                        if (EPI & NERF_EPI_MASK) v = mbits ? apply_bits(v, xb[u]) : apply_sign(v, xa[u]);
+                        if (MSK) v = mbits ? apply_bits(v, xb[u]) : apply_sign(v, xa[u]);
                         if (EPI & NERF_EPI_ACCUM) v = xo[u] + v;
                         *reinterpret_cast<f4*>(o) = v;
                         nib = quad_bits(v);
@@ -569,10 +565,18 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
             }
             barrier();
         };
-        pass(0, acc[0], acc[1]);
-        pass(1, acc[2], acc[3]);
-        pass(2, acc[0], acc[1]);
-        pass(3, acc[2], acc[3]);
+        if (PR == 64) {
+            pass(0, 0, acc[0], acc[1]);
+            pass(64, 0, acc[2], acc[3]);
+            pass(128, 1, acc[0], acc[1]);
+            pass(192, 1, acc[2], acc[3]);
+        } else {
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                // compile-time acc indices once unrolled
+                pass(32 * p, p >> 2, acc[p & 3], acc[p & 3]);
+            }
+        }
     };
 
     // prologue: A(0), W(0), A(1); iteration g issues W(g+1), A(g+2) and waits for A(g), W(g)
@@ -1024,7 +1028,7 @@ extern "C" int nerf_linear_fwd_x3(const nerf_seg* segs, int32_t n_segs, int64_t 
     NERF_REQUIRE(W_x && out && aligned16(W_x) && ldw == L.ktot && (ldw % BK) == 0 && ldo >= N);
     if (epilogue & NERF_EPI_BIAS) NERF_REQUIRE(bias != nullptr);
     const bool mbits = (epilogue & (NERF_EPI_MASKBITS | NERF_EPI_MASKOUT)) != 0;
-    if (mbits) NERF_REQUIRE(aux != nullptr && N <= 256 && ld_aux >= 32 && (ld_aux % 4) == 0 && aligned16(aux));
+    if (mbits) NERF_REQUIRE(aux != nullptr && N <= 256 && ld_aux >= 32 && (ld_aux % 16) == 0 && aligned16(aux));
     if (epilogue & NERF_EPI_MASK) NERF_REQUIRE(aux != nullptr && (mbits || ld_aux >= N));
     if (epilogue & NERF_EPI_MASKOUT) NERF_REQUIRE(!(epilogue & NERF_EPI_MASK));
     const int vec_ok = aligned16(out) && (ldo % 4) == 0 && (!(epilogue & NERF_EPI_BIAS) || aligned16(bias)) &&
