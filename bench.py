@@ -209,6 +209,13 @@ def main():
         with open(tfile) as f:
             traffic = json.load(f).get("bytes_per_launch")
 
+    # HBM roofline of the bandwidth-bound kernels BASELINE.json's north_star names (positional
+    # encoding + alpha compositing): algorithmic bytes (kernels.py, per launch) / event-timed duration
+    hbm_tags = ("encode_fwd", "composite_fwd", "composite_bwd")
+    hbm_bytes = sum(ks.get(k, {}).get("bytes", 0.0) for k in hbm_tags)
+    hbm_ms = sum(ks.get(k, {}).get("ms", 0.0) for k in hbm_tags)
+    hbm_gbs = hbm_bytes / (hbm_ms * 1e-3) / 1e9 if hbm_ms > 0 else 0.0
+
     if rank == 0:
         out = {
             "metric": "ray-samples/sec (coarse+fine), training step",
@@ -236,8 +243,15 @@ def main():
                          "frac": achieved / peak, "traffic": traffic,
                          "avg_launch_us": nt_avg_ms * 1e3, "avg_flops_per_launch": nt_avg_flops,
                          "launches_per_step": nt["launches"] / args.steps},
+            "roofline_hbm": {"kernel": "encode_fwd + composite_fwd + composite_bwd (positional encoding and "
+                                       "alpha compositing; algorithmic bytes per launch)",
+                             "bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": hbm_gbs / HBM_PEAK_GBS,
+                             "us_per_step": hbm_ms * 1e3 / args.steps,
+                             "bytes_per_step": hbm_bytes / args.steps},
             "kernels": {k: {"launches_per_step": v["launches"] / args.steps, "ms_per_step": v["ms"] / args.steps,
-                            "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["ms"] > 0 else 0.0}
+                            "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["ms"] > 0 else 0.0,
+                            "gbs": (v["bytes"] / (v["ms"] * 1e-3) / 1e9) if v["ms"] > 0 else 0.0}
                         for k, v in ks.items()},
             "mlp_tflops_per_step": flops_per_sample(ren) * RAYS * SAMPLES / (elapsed / args.steps) / 1e12,
             "final_loss": final_loss,

@@ -156,6 +156,16 @@ int nerf_encode_bwd(const nerf_pe_params* params, const float* x,
                     const float* grad_out, int64_t g_ld, int64_t n_samples,
                     float* dx, int32_t accumulate, void* stream);
 
+/* Backward of kind-1 (integrated) encodings w.r.t. the position x and the direction xdir
+ * (autograd of positional_encodings.py:186-235 and of the masked variant :274-282), one
+ * thread per sample.  Inputs as nerf_encode_fwd with x != NULL and pw_mode 2 (per-sample
+ * pixel_width[n]).  dx / ddir [n,3] (either may be NULL; accumulate: +=).  t_start, t_end and
+ * pixel_width receive no gradient. */
+int nerf_encode_bwd_integrated(const nerf_pe_params* params, const float* x, const float* xdir,
+                               const float* t_start, const float* t_end, const float* pixel_width,
+                               const float* grad_out, int64_t g_ld, int64_t n_samples,
+                               float* dx, float* ddir, int32_t accumulate, void* stream);
+
 /* Per-ray direction encoding (dir PE evaluated once per ray instead of once
  * per sample; the MLP reads row n / samples_per_ray).  kind 0 only. */
 int nerf_encode_rays(const nerf_pe_params* params, const float* ray_d, int64_t n_rays,
@@ -248,6 +258,23 @@ int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N,
                          void* workspace, size_t workspace_bytes, void* stream);
 int nerf_pack_weight_x3(const float* W, int32_t N, int32_t K_orig, const int32_t* col_map,
                         int32_t Kp, void* Wp_x, void* Wt_x, int32_t ldwt, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Gaussian activation with a learnable per-channel inverse standard deviation (a8, GARF
+ * field MLPs): GaussActivation / GaussAct, garf/gaussian.py:8-63 (copy: barf/gaussian.py).
+ * v_n = inv_std_n^2 + 1e-6;  y[m,n] = exp((-(z*z)) * v_n)  over z [M][N] (row stride ld_z).
+ * Backward: ge = grad_y * exp((-(z*z)) * v);  grad_z = (((-ge) * 2) * z) * v (grad_z may
+ * alias grad_y);  grad_inv_std_n = (sum_m (-ge) * z^2) * (2 * inv_std_n), the column sum
+ * accumulated in fp64 per slab of rows and the slabs summed in a fixed order (deterministic).
+ * workspace: nerf_gauss_act_workspace(M, N) bytes.  accumulate: grad_inv_std += result.
+ * ------------------------------------------------------------------------- */
+size_t nerf_gauss_act_workspace(int64_t M, int32_t N);
+int nerf_gauss_act_fwd(const float* z, int64_t ld_z, const float* inv_std, int64_t M, int32_t N,
+                       float* y, int64_t ld_y, void* stream);
+int nerf_gauss_act_bwd(const float* grad_y, int64_t ld_g, const float* z, int64_t ld_z,
+                       const float* inv_std, int64_t M, int32_t N, float* grad_z, int64_t ld_dz,
+                       float* grad_inv_std, int32_t accumulate, void* workspace, size_t workspace_bytes,
+                       void* stream);
 
 #ifdef __cplusplus
 }

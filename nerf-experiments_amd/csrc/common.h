@@ -75,6 +75,37 @@ __device__ __forceinline__ float softplus_thr8_grad(float x) {
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // ---------------------------------------------------------------------------
+// sin and cos of one fp32 argument for the encodings (|x| up to scale * 2^15 * |p|):
+// k = rint(x * 2/pi); r = x - k * pi/2 reduced in fp64 with a two-term pi/2 (error < 2^-40
+// for |x| < 2^30), then fp32 minimax polynomials on [-pi/4, pi/4] (Cephes sinf/cosf,
+// ~1 ulp) and the quadrant swap.  About a third of the instructions of the libm sincosf,
+// within ~1e-7 absolute of the correctly rounded values; larger or non-finite arguments
+// take sincosf.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void sincos_enc(float x, float* s, float* c) {
+    if (!(fabsf(x) < 1073741824.0f)) {
+        sincosf(x, s, c);
+        return;
+    }
+    const float kf = rintf(x * 0.636619772367581343f);
+    double rd = __builtin_fma((double)kf, -1.5707963267948966, (double)x);
+    rd = __builtin_fma((double)kf, -6.123233995736766e-17, rd);
+    const float r = (float)rd;
+    const float r2 = r * r;
+    float sp = __builtin_fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f);
+    sp = __builtin_fmaf(r2, sp, -1.6666654611e-1f);
+    sp = __builtin_fmaf(r * r2, sp, r);
+    float cp = __builtin_fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f);
+    cp = __builtin_fmaf(r2, cp, 4.166664568298827e-2f);
+    cp = __builtin_fmaf(r2 * r2, cp, __builtin_fmaf(r2, -0.5f, 1.0f));
+    const int q = (int)kf & 3;
+    const float ss = (q & 1) ? cp : sp;
+    const float cc = (q & 1) ? sp : cp;
+    *s = (q & 2) ? -ss : ss;
+    *c = ((q + 1) & 2) ? -cc : cc;
+}
+
+// ---------------------------------------------------------------------------
 // Philox-4x32-10 counter-based RNG -> uniform float in [0, 1) (24-bit).
 // ---------------------------------------------------------------------------
 struct Philox4 {

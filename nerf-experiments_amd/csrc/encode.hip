@@ -9,12 +9,14 @@
 //   IntegratedBarfFourierFeatures        :266-282
 //   NerfInterpolation._compute_positions barf/model_interpolation.py:288-312 (o + t*d)
 //
-// Design: one thread per output column of one sample, so a row of the
-// encoding (e.g. 64 floats for BARF L=10 + identity, padded) is written by 64
-// consecutive lanes — every store is a fully coalesced 256-byte wave write.
-// Each thread recomputes the sample's position (o, d, t are L1/L2 hits) and one
-// sincos; the kernel is store-bound by design.  Floating-point contraction is
-// off so every fp32 operation rounds exactly where the reference's does.
+// Design: the forward is an HBM-store-bound kernel (≈250 B written per sample vs ≈8 B
+// read).  Rows of <= 128 columns go through encode_fwd_lds_kernel: 64 samples per block,
+// positions computed once per sample, ONE sin/cos evaluation per (sample, d, k) feeding both
+// the cos and the sin column, the row image staged in LDS and written with coalesced 16-byte
+// stores.  sin/cos use sincos_enc (fp64 Cody-Waite reduction + fp32 minimax, ~1e-7 abs) —
+// libm sincosf made the kernel VALU-bound.  Wider / unaligned rows: one thread per 4 columns.
+// Floating-point contraction is off so every other fp32 operation rounds exactly where the
+// reference's does.
 #include "common.h"
 
 using namespace nerf;
@@ -29,6 +31,7 @@ struct EncArgs {
     int64_t n; int S; int64_t n_rays;
     float* out; int64_t ld;
     int out_dim;
+    int vec;     // out 16-byte aligned and ld % 4 == 0: float4 stores
 };
 
 __device__ __forceinline__ void load_pos_dir(const EncArgs& a, int64_t n, float p[3], float dv[3]) {
@@ -38,7 +41,7 @@ __device__ __forceinline__ void load_pos_dir(const EncArgs& a, int64_t n, float 
         if (a.xdir) { dv[0] = a.xdir[n * 3 + 0]; dv[1] = a.xdir[n * 3 + 1]; dv[2] = a.xdir[n * 3 + 2]; }
         else { dv[0] = dv[1] = dv[2] = 0.f; }
     } else {
-        const int64_t ray = n / a.S;
+        const int64_t ray = (int64_t)((uint32_t)n / (uint32_t)a.S);   // n < 2^31 (host check)
         const float tq = (a.p.query == 0) ? a.t0[n] : (a.t0[n] + a.t1[n]) / 2.0f;
         dv[0] = a.d[ray * 3 + 0]; dv[1] = a.d[ray * 3 + 1]; dv[2] = a.d[ray * 3 + 2];
         p[0] = a.o[ray * 3 + 0] + tq * dv[0];
@@ -52,92 +55,196 @@ __device__ __forceinline__ float sel3(const float v[3], int i) {
 }
 
 __device__ __forceinline__ float pixel_width_at(const EncArgs& a, int64_t n) {
-    if (a.p.pw_mode == 0) return a.pw[n / a.S];
-    if (a.p.pw_mode == 1) return a.pw[n % a.n_rays];
+    if (a.p.pw_mode == 0) return a.pw[(uint32_t)n / (uint32_t)a.S];
+    if (a.p.pw_mode == 1) return a.pw[(uint32_t)n % (uint32_t)a.n_rays];
     return a.pw[n];
 }
 
-__global__ __launch_bounds__(256) void encode_fwd_kernel(EncArgs a) {
+// Per-sample quantities of the mip-NeRF integrated encoding (positional_encodings.py:186-226),
+// in the reference's fp32 operation order:
+//   pm      = pos + mu_diff * dir                         (eq 8, :190-191)
+//   vb[d]   = variance of coordinate d before the 4^k level scale: (st + 2 sr) / 3 when the
+//             variance is distributed (:213-215), st d_d^2 + sr (1 - d_d^2 / |d|^2) otherwise
+//             (eq 16, :219); weight(d, k) = exp(-(vb[d] * 4^k) / 2).
+// st, sr (eq 7, :201-207) and mu_diff are returned for the backward.
+struct IpeSample {
+    float pm[3], vb[3];
+    float st, sr, mu_diff, ssum;
+};
+
+__device__ __forceinline__ IpeSample ipe_sample(const nerf_pe_params& p, const float pos[3], const float dv[3],
+                                                float t0, float t1, float pwv) {
 #pragma clang fp contract(off)
-    const int64_t total = a.n * a.ld;
+    IpeSample r;
+    const float tm = (t0 + t1) / 2.0f;
+    const float td = (t1 - t0) / 2.0f;
+    const float tm2 = tm * tm, td2 = td * td;
+    const float td4 = powf(td, 4.0f);
+    r.mu_diff = ((2.0f * tm) * td2) / ((3.0f * tm2) + td2);
+    r.pm[0] = pos[0] + r.mu_diff * dv[0];
+    r.pm[1] = pos[1] + r.mu_diff * dv[1];
+    r.pm[2] = pos[2] + r.mu_diff * dv[2];
+    const float r_dot = (pwv * 2.0f) / 3.4641016151377544f;
+    const float q3 = (3.0f * tm2) + td2;
+    float st = (td2 / 3.0f) - (((4.0f * td4) * ((12.0f * tm2) - td2)) / (15.0f * (q3 * q3)));
+    float sr = (r_dot * r_dot) * (((tm2 / 4.0f) + ((5.0f * td2) / 12.0f)) - ((4.0f * td4) / (15.0f * q3)));
+    if (p.pixel_width_sigma > 0.25f) {
+        const float as_ = (p.pixel_width_sigma * pwv) * tm;
+        const float add = as_ * as_;
+        st = st + add;
+        sr = sr + add;
+    }
+    r.st = st;
+    r.sr = sr;
+    r.ssum = (dv[0] * dv[0] + dv[1] * dv[1]) + dv[2] * dv[2];
+    if (p.distribute_variance) {
+        const float v = (st + sr * 2.0f) / 3.0f;
+        r.vb[0] = r.vb[1] = r.vb[2] = v;
+    } else {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const float d2 = dv[d] * dv[d];
+            r.vb[d] = (st * d2) + (sr * (1.0f - (d2 / r.ssum)));
+        }
+    }
+    return r;
+}
+
+// Value of encoding column c (< out_dim) of one sample.  pm = the (mean-shifted, for kind 1)
+// position; q = the IPE per-sample terms (kind 1 only).
+__device__ __forceinline__ float enc_column(const nerf_pe_params& p, int L, int id, int c, const float pm[3],
+                                            const IpeSample& q) {
+#pragma clang fp contract(off)
+    if (c < id) return sel3(pm, c);
+    const int j = c - id;
+    const int blk = j >= 3 * L ? 1 : 0;              // 0 cos, 1 sin
+    const int jj = j - blk * 3 * L;
+    const int dd = jj >= 2 * L ? 2 : (jj >= L ? 1 : 0);
+    const int k = jj - dd * L;
+    const float s = p.scale * (float)(1u << k);
+    const float arg = sel3(pm, dd) * s;
+    float sn, cs;
+    sincos_enc(arg, &sn, &cs);
+    float val = blk == 0 ? cs : sn;
+    if (p.kind == 1) {
+        // mip-NeRF weight exp(-(var_d * 4^k) / 2) (positional_encodings.py:213-232)
+        const float sc4 = (float)(1u << (2 * k));   // 4^k (exact)
+        val = val * expf((-(sel3(q.vb, dd) * sc4)) / 2.0f);
+    }
+    if (p.use_mask) val = p.mask[k] * val;
+    return val;
+}
+
+// One thread per 4 consecutive output columns (one 16-byte store) of one sample: the Q = ld/4
+// threads of a row write it contiguously, rows_per_block = 256 / Q rows per block, so a wave
+// stores 1 KB of consecutive rows per instruction.  The position (o + t d, or x), and for the
+// integrated encoding the per-sample variance terms, are computed once per thread.
+__global__ __launch_bounds__(256) void encode_fwd_kernel(EncArgs a, int Q, int RB) {
+#pragma clang fp contract(off)
+    const int t = threadIdx.x;
+    const int rloc = t / Q;
+    const int qd = t - rloc * Q;
+    if (rloc >= RB) return;
+    const int64_t n = (int64_t)blockIdx.x * RB + rloc;
+    if (n >= a.n) return;
     const int L = a.p.levels;
     const int id = a.p.include_identity ? 3 : 0;
-    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-         idx += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t n = idx / a.ld;
-        const int c = (int)(idx - n * a.ld);
-        float val = 0.0f;
-        if (c < a.out_dim) {
-            float p[3], dv[3];
-            load_pos_dir(a, n, p, dv);
-            if (a.p.kind == 1) {
-                // mip-NeRF integrated encoding (positional_encodings.py:186-235)
-                const float t0 = a.t0[n], t1 = a.t1[n];
-                const float tm = (t0 + t1) / 2.0f;
-                const float td = (t1 - t0) / 2.0f;
-                const float tm2 = tm * tm, td2 = td * td;
-                const float td4 = powf(td, 4.0f);
-                const float mu_diff = ((2.0f * tm) * td2) / ((3.0f * tm2) + td2);
-                float pm[3];
-                pm[0] = p[0] + mu_diff * dv[0];
-                pm[1] = p[1] + mu_diff * dv[1];
-                pm[2] = p[2] + mu_diff * dv[2];
-                if (c < id) {
-                    val = sel3(pm, c);
-                } else {
-                    const int j = c - id;
-                    const int blk = j / (3 * L);       // 0 cos, 1 sin
-                    const int jj = j - blk * 3 * L;
-                    const int dd = jj / L, k = jj - dd * L;
-                    const float pwv = pixel_width_at(a, n);
-                    const float r_dot = (pwv * 2.0f) / 3.4641016151377544f;
-                    const float q3 = (3.0f * tm2) + td2;
-                    float st = (td2 / 3.0f) - (((4.0f * td4) * ((12.0f * tm2) - td2)) / (15.0f * (q3 * q3)));
-                    float sr = (r_dot * r_dot) *
-                               (((tm2 / 4.0f) + ((5.0f * td2) / 12.0f)) - ((4.0f * td4) / (15.0f * q3)));
-                    if (a.p.pixel_width_sigma > 0.25f) {
-                        const float as_ = (a.p.pixel_width_sigma * pwv) * tm;
-                        const float add = as_ * as_;
-                        st = st + add;
-                        sr = sr + add;
-                    }
-                    const float sc4 = (float)(1u << (2 * k));   // 4^k (exact)
-                    float sig;
-                    if (a.p.distribute_variance) {
-                        sig = ((st + sr * 2.0f) / 3.0f) * sc4;
-                    } else {
-                        const float dsel = sel3(dv, dd);
-                        const float d2 = dsel * dsel;
-                        const float ssum = (dv[0] * dv[0] + dv[1] * dv[1]) + dv[2] * dv[2];
-                        const float diag = (st * d2) + (sr * (1.0f - (d2 / ssum)));
-                        sig = diag * sc4;
-                    }
-                    const float wgt = expf((-sig) / 2.0f);
-                    const float s = a.p.scale * (float)(1u << k);
-                    const float arg = sel3(pm, dd) * s;
-                    float sn, cs;
-                    sincosf(arg, &sn, &cs);
-                    val = (blk == 0 ? cs : sn) * wgt;
-                    if (a.p.use_mask) val = a.p.mask[k] * val;
-                }
-            } else {
-                if (c < id) {
-                    val = sel3(p, c);
-                } else {
-                    const int j = c - id;
-                    const int blk = j / (3 * L);
-                    const int jj = j - blk * 3 * L;
-                    const int dd = jj / L, k = jj - dd * L;
-                    const float s = a.p.scale * (float)(1u << k);
-                    const float arg = sel3(p, dd) * s;
-                    float sn, cs;
-                    sincosf(arg, &sn, &cs);
-                    val = (blk == 0) ? cs : sn;
-                    if (a.p.use_mask) val = a.p.mask[k] * val;
-                }
+    float p[3], dv[3];
+    load_pos_dir(a, n, p, dv);
+    IpeSample q;
+    const float* pm = p;
+    if (a.p.kind == 1) {
+        q = ipe_sample(a.p, p, dv, a.t0[n], a.t1[n], a.pw ? pixel_width_at(a, n) : 0.f);
+        pm = q.pm;
+    }
+    const int c0 = 4 * qd;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (c0 + e < a.out_dim) ? enc_column(a.p, L, id, c0 + e, pm, q) : 0.0f;
+    float* o = a.out + n * a.ld + c0;
+    if (a.vec) {
+        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (c0 + e < a.ld) o[e] = v[e];
+    }
+}
+
+// LDS-staged variant for rows of <= 128 columns (every encoding of the reference's configs):
+// a block encodes 64 samples in three phases —
+//   0. one thread per sample: position (and the IPE variance terms) into LDS, identity and
+//      zero-pad columns into the row image;
+//   1. one thread per (sample, d, k): ONE sincos per argument, writing both the cos and the sin
+//      column (half the transcendental work of a per-column mapping);
+//   2. the 64-row image leaves LDS as coalesced 16-byte stores (ld/4 consecutive lanes per row).
+constexpr int kEncRows = 64;
+constexpr int kEncMaxLd = 128;
+
+__global__ __launch_bounds__(256) void encode_fwd_lds_kernel(EncArgs a) {
+#pragma clang fp contract(off)
+    __shared__ float img[kEncRows * (kEncMaxLd + 4)];
+    __shared__ float spm[kEncRows][3];
+    __shared__ float svb[kEncRows][3];
+    const int t = threadIdx.x;
+    const int L = a.p.levels;
+    const int id = a.p.include_identity ? 3 : 0;
+    const int ld = (int)a.ld;
+    const int lds_ld = ld + 4;          // 16-byte aligned rows, staggered banks
+    const int64_t n0 = (int64_t)blockIdx.x * kEncRows;
+    const int rows = a.n - n0 < kEncRows ? (int)(a.n - n0) : kEncRows;
+    if (t < rows) {
+        const int64_t n = n0 + t;
+        float p[3], dv[3];
+        load_pos_dir(a, n, p, dv);
+        float* row = img + t * lds_ld;
+        if (a.p.kind == 1) {
+            const IpeSample q = ipe_sample(a.p, p, dv, a.t0[n], a.t1[n], a.pw ? pixel_width_at(a, n) : 0.f);
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                spm[t][d] = q.pm[d];
+                svb[t][d] = q.vb[d];
             }
+        } else {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) spm[t][d] = p[d];
         }
-        a.out[n * a.ld + c] = val;
+        for (int c = 0; c < id; ++c) row[c] = spm[t][c];
+        for (int c = a.out_dim; c < ld; ++c) row[c] = 0.0f;
+    }
+    __syncthreads();
+    const int tl = 3 * L;
+    const int tasks = rows * tl;
+    for (int i = t; i < tasks; i += 256) {
+        const int r = i / tl;
+        const int j = i - r * tl;
+        const int dd = j >= 2 * L ? 2 : (j >= L ? 1 : 0);
+        const int k = j - dd * L;
+        const float s = a.p.scale * (float)(1u << k);
+        float sn, cs;
+        sincos_enc(spm[r][dd] * s, &sn, &cs);
+        if (a.p.kind == 1) {
+            const float sc4 = (float)(1u << (2 * k));
+            const float w = expf((-(svb[r][dd] * sc4)) / 2.0f);
+            cs = cs * w;
+            sn = sn * w;
+        }
+        if (a.p.use_mask) {
+            cs = a.p.mask[k] * cs;
+            sn = a.p.mask[k] * sn;
+        }
+        float* row = img + r * lds_ld;
+        row[id + j] = cs;
+        row[id + tl + j] = sn;
+    }
+    __syncthreads();
+    const int Q = ld >> 2;
+    const int stores = rows * Q;
+    for (int i = t; i < stores; i += 256) {
+        const int r = i / Q;
+        const int qd = i - r * Q;
+        const float4 v = *reinterpret_cast<const float4*>(img + r * lds_ld + 4 * qd);
+        *reinterpret_cast<float4*>(a.out + (n0 + r) * a.ld + 4 * qd) = v;
     }
 }
 
@@ -159,7 +266,7 @@ __global__ __launch_bounds__(256) void encode_bwd_kernel(nerf_pe_params p, const
         const float s = p.scale * (float)(1u << k);
         const float arg = xv * s;
         float sn, cs;
-        sincosf(arg, &sn, &cs);
+        sincos_enc(arg, &sn, &cs);
         const float m = p.use_mask ? p.mask[k] : 1.0f;
         const float gc = gr[id + dd * L + k];
         const float gs = gr[id + 3 * L + dd * L + k];
@@ -167,6 +274,70 @@ __global__ __launch_bounds__(256) void encode_bwd_kernel(nerf_pe_params p, const
     }
     if (accumulate) acc += dx[idx];
     dx[idx] = acc;
+}
+
+// Backward of the integrated encoding (autograd of positional_encodings.py:186-235, and of the
+// masked variant :274-282) w.r.t. the position and the direction, one thread per sample:
+//   out_cos(d,k) = m_k * (cos(a) * w),  out_sin(d,k) = m_k * (sin(a) * w),
+//   a = pm_d * scale * 2^k,  w = exp(-(vb_d * 4^k) / 2),  pm = pos + mu_diff * dir.
+//   g_pm_d = g_id_d + sum_k s_k * w * (-m g_cos sin a + m g_sin cos a)
+//   g_vb_d = sum_k -(4^k / 2) * w * (m g_cos cos a + m g_sin sin a)
+//   dpos = g_pm;  ddir_j = g_pm_j * mu_diff + [diagonal variance only]
+//          2 d_j (st - sr / S) g_vb_j + 2 d_j sr / S^2 * sum_d g_vb_d d_d^2   (S = |d|^2)
+// t_start / t_end / pixel_width receive no gradient (the reference's samplers never need one).
+__global__ __launch_bounds__(256) void encode_bwd_integrated_kernel(
+    nerf_pe_params p, const float* __restrict__ x, const float* __restrict__ xdir, const float* __restrict__ t0,
+    const float* __restrict__ t1, const float* __restrict__ pw, const float* __restrict__ g, int64_t g_ld,
+    int64_t n_total, float* __restrict__ dx, float* __restrict__ ddir, int accumulate) {
+#pragma clang fp contract(off)
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_total) return;
+    const int L = p.levels;
+    const int id = p.include_identity ? 3 : 0;
+    float pos[3], dv[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        pos[d] = x[n * 3 + d];
+        dv[d] = xdir[n * 3 + d];
+    }
+    const IpeSample q = ipe_sample(p, pos, dv, t0[n], t1[n], pw[n]);
+    const float* gr = g + n * g_ld;
+    float gpm[3], gvb[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        float apm = id ? gr[d] : 0.0f;
+        float avb = 0.0f;
+        for (int k = 0; k < L; ++k) {
+            const float m = p.use_mask ? p.mask[k] : 1.0f;
+            const float sc4 = (float)(1u << (2 * k));
+            const float w = expf((-(q.vb[d] * sc4)) / 2.0f);
+            const float s = p.scale * (float)(1u << k);
+            float sn, cs;
+            sincos_enc(q.pm[d] * s, &sn, &cs);
+            const float gc = gr[id + d * L + k] * m;
+            const float gs = gr[id + 3 * L + d * L + k] * m;
+            apm += (((-gc) * sn + gs * cs) * w) * s;
+            avb += ((gc * cs + gs * sn) * w) * (-(sc4 / 2.0f));
+        }
+        gpm[d] = apm;
+        gvb[d] = avb;
+    }
+    float dd[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) dd[j] = gpm[j] * q.mu_diff;
+    if (!p.distribute_variance) {
+        const float S = q.ssum;
+        const float cross = ((gvb[0] * (dv[0] * dv[0]) + gvb[1] * (dv[1] * dv[1])) + gvb[2] * (dv[2] * dv[2])) *
+                            ((2.0f * q.sr) / (S * S));
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            dd[j] += (2.0f * dv[j]) * ((q.st - q.sr / S) * gvb[j]) + dv[j] * cross;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        if (dx) dx[n * 3 + j] = accumulate ? dx[n * 3 + j] + gpm[j] : gpm[j];
+        if (ddir) ddir[n * 3 + j] = accumulate ? ddir[n * 3 + j] + dd[j] : dd[j];
+    }
 }
 
 int out_dim_of(const nerf_pe_params& p) { return (2 * p.levels + (p.include_identity ? 1 : 0)) * 3; }
@@ -191,12 +362,19 @@ extern "C" int nerf_encode_fwd(const nerf_pe_params* params, const float* x, con
         if (p.pw_mode == 1) NERF_REQUIRE(n_rays >= 1);
         if (p.pw_mode == 0) NERF_REQUIRE(samples_per_ray >= 1);
     }
+    NERF_REQUIRE(n_samples < (1ll << 31) && out_ld <= 1024);
+    const int vec = aligned16(out) && (out_ld % 4) == 0;
     EncArgs a{p, x, xdir, ray_o, ray_d, t_start, t_end, pixel_width, n_samples,
-              samples_per_ray > 0 ? samples_per_ray : 1, n_rays, out, out_ld, od};
-    const int64_t total = n_samples * out_ld;
-    int64_t blocks = (total + 255) / 256;
-    if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(encode_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
+              samples_per_ray > 0 ? samples_per_ray : 1, n_rays, out, out_ld, od, vec};
+    if (vec && out_ld <= kEncMaxLd) {
+        const int64_t blocks = (n_samples + kEncRows - 1) / kEncRows;
+        hipLaunchKernelGGL(encode_fwd_lds_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
+    } else {
+        const int Q = (int)((out_ld + 3) / 4);      // threads per row (4 columns each)
+        const int RB = 256 / Q;                     // rows per block
+        const int64_t blocks = (n_samples + RB - 1) / RB;
+        hipLaunchKernelGGL(encode_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a, Q, RB);
+    }
     NERF_CHECK_LAUNCH();
     return NERF_OK;
 }
@@ -210,6 +388,22 @@ extern "C" int nerf_encode_bwd(const nerf_pe_params* params, const float* x, con
     const int64_t total = n_samples * 3;
     hipLaunchKernelGGL(encode_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream),
                        *params, x, grad_out, g_ld, n_samples, dx, accumulate);
+    NERF_CHECK_LAUNCH();
+    return NERF_OK;
+}
+
+extern "C" int nerf_encode_bwd_integrated(const nerf_pe_params* params, const float* x, const float* xdir,
+                                          const float* t_start, const float* t_end, const float* pixel_width,
+                                          const float* grad_out, int64_t g_ld, int64_t n_samples, float* dx,
+                                          float* ddir, int32_t accumulate, void* stream) {
+    NERF_REQUIRE(params && n_samples >= 0);
+    if (n_samples == 0) return NERF_OK;
+    NERF_REQUIRE(params->kind == 1 && params->levels >= 0 && params->levels <= 16);
+    NERF_REQUIRE(x && xdir && t_start && t_end && pixel_width && grad_out && (dx || ddir));
+    NERF_REQUIRE(g_ld >= out_dim_of(*params));
+    hipLaunchKernelGGL(encode_bwd_integrated_kernel, dim3((unsigned)((n_samples + 255) / 256)), dim3(256), 0,
+                       as_stream(stream), *params, x, xdir, t_start, t_end, pixel_width, grad_out, g_ld, n_samples,
+                       dx, ddir, accumulate);
     NERF_CHECK_LAUNCH();
     return NERF_OK;
 }

@@ -1048,6 +1048,7 @@ extern "C" int nerf_linear_fwd_x3(const nerf_seg* segs, int32_t n_segs, int64_t 
         switch (epilogue & 15) {
             case NERF_EPI_BIAS | NERF_EPI_RELU: NERF_GLDS_LAUNCH(NERF_EPI_BIAS | NERF_EPI_RELU); break;
             case NERF_EPI_BIAS: NERF_GLDS_LAUNCH(NERF_EPI_BIAS); break;
+            case NERF_EPI_BIAS | NERF_EPI_ACCUM: NERF_GLDS_LAUNCH(NERF_EPI_BIAS | NERF_EPI_ACCUM); break;
             case 0: NERF_GLDS_LAUNCH(0); break;
             case NERF_EPI_MASK: NERF_GLDS_LAUNCH(NERF_EPI_MASK); break;
             case NERF_EPI_MASK | NERF_EPI_ACCUM: NERF_GLDS_LAUNCH(NERF_EPI_MASK | NERF_EPI_ACCUM); break;

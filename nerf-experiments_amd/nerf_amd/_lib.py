@@ -67,7 +67,13 @@ _SIGNATURES = {
     "nerf_encode_fwd": (c_i32, [ctypes.POINTER(NerfPEParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                 c_i64, c_i32, c_i64, c_vp, c_i64, c_vp]),
     "nerf_encode_bwd": (c_i32, [ctypes.POINTER(NerfPEParams), c_vp, c_vp, c_i64, c_i64, c_vp, c_i32, c_vp]),
+    "nerf_encode_bwd_integrated": (c_i32, [ctypes.POINTER(NerfPEParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                           c_i64, c_i64, c_vp, c_vp, c_i32, c_vp]),
     "nerf_encode_rays": (c_i32, [ctypes.POINTER(NerfPEParams), c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "nerf_gauss_act_workspace": (c_sz, [c_i64, c_i32]),
+    "nerf_gauss_act_fwd": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp]),
+    "nerf_gauss_act_bwd": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_i32,
+                                   c_vp, c_sz, c_vp]),
     "nerf_linear_fwd": (c_i32, [ctypes.POINTER(NerfSeg), c_i32, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp, c_i64,
                                 c_i32, c_vp, c_i64, c_vp]),
     "nerf_linear_wgrad_workspace": (c_sz, [c_i64, c_i32, c_i32]),

@@ -18,29 +18,31 @@ from ._lib import NerfPEParams, NerfSeg
 
 
 class KernelTimer:
-    """Optional HIP-event bracketing of the MFMA linear launches (used by bench.py).
+    """Optional HIP-event bracketing of kernel launches (used by bench.py).
 
     Events are recorded on the same stream the kernel is launched on (torch's
     current stream, which is the stream passed to the C-ABI), so
-    elapsed_time() is the kernel's device duration.  Records (tag, flops, start, end)."""
+    elapsed_time() is the kernel's device duration.  Records (tag, flops, algorithmic
+    HBM bytes, start, end)."""
 
     def __init__(self):
         self.records = []
 
-    def bracket(self, tag: str, flops: float):
+    def bracket(self, tag: str, flops: float = 0.0, nbytes: float = 0.0):
         start = torch.cuda.Event(enable_timing=True)
         end = torch.cuda.Event(enable_timing=True)
         start.record()
-        self.records.append((tag, flops, start, end))
+        self.records.append((tag, flops, nbytes, start, end))
         return end
 
     def summary(self):
         out = {}
-        for tag, flops, s, e in self.records:
+        for tag, flops, nbytes, s, e in self.records:
             ms = s.elapsed_time(e)
-            d = out.setdefault(tag, {"launches": 0, "flops": 0.0, "ms": 0.0})
+            d = out.setdefault(tag, {"launches": 0, "flops": 0.0, "bytes": 0.0, "ms": 0.0})
             d["launches"] += 1
             d["flops"] += flops
+            d["bytes"] += nbytes
             d["ms"] += ms
         return out
 
@@ -85,9 +87,15 @@ def composite_fwd(density: torch.Tensor, density_stride: int, color: torch.Tenso
     dev = dist.device
     rgb = torch.empty(n_rays, 3, device=dev, dtype=torch.float32)
     w = torch.empty(n_rays, samples_per_ray, device=dev, dtype=torch.float32) if want_weights else None
+    n = n_rays * samples_per_ray
+    # algorithmic bytes: sigma, rgb, delta in (+ weights out) per sample, rgb out per ray
+    end = TIMER.bracket("composite_fwd", nbytes=n * (20 + (4 if want_weights else 0)) + 12 * n_rays) \
+        if TIMER is not None else None
     st = _lib.load().nerf_composite_fwd(_ptr(density), density_stride, _ptr(color), color_stride, _ptr(dist),
                                         n_rays, samples_per_ray, scale_a, scale_b, int(act), density_shift,
                                         _ptr(rgb), _ptr(w), _stream(dev))
+    if end is not None:
+        end.record()
     _lib.check(st, "nerf_composite_fwd")
     return rgb, w
 
@@ -97,10 +105,17 @@ def composite_bwd(density, density_stride, color, color_stride, dist, n_rays, sa
     grad_rgb = grad_rgb.contiguous()
     if grad_weights is not None:
         grad_weights = grad_weights.contiguous()
+    n = n_rays * samples_per_ray
+    # algorithmic bytes: sigma, rgb, delta (+ dL/dw) in, dL/dsigma, dL/drgb out per sample; dL/drgb in per ray
+    nb = n * (20 + (4 if grad_weights is not None else 0) + (4 if grad_density is not None else 0)
+              + (12 if grad_color is not None else 0)) + 12 * n_rays
+    end = TIMER.bracket("composite_bwd", nbytes=nb) if TIMER is not None else None
     st = _lib.load().nerf_composite_bwd(_ptr(density), density_stride, _ptr(color), color_stride, _ptr(dist),
                                         n_rays, samples_per_ray, scale_a, scale_b, int(act), density_shift,
                                         _ptr(grad_rgb), _ptr(grad_weights), _ptr(grad_density), gd_stride,
                                         _ptr(grad_color), gc_stride, _stream(dist.device))
+    if end is not None:
+        end.record()
     _lib.check(st, "nerf_composite_bwd")
 
 
@@ -172,9 +187,22 @@ def encode_fwd(params: NerfPEParams, out_dim: int, *, x=None, xdir=None, ray_o=N
             if not t.is_contiguous():
                 raise ValueError(f"{name} must be contiguous")
     out = torch.empty(n_samples, ld, device=device, dtype=torch.float32)
+    end = None
+    if TIMER is not None:
+        # algorithmic bytes: the encoding's out_dim columns written, its inputs read once
+        per_sample = 4 * out_dim
+        if x is not None:
+            per_sample += 12 + (12 if params.kind == 1 else 0) + (12 if params.kind == 1 else 0)
+            per_ray = 0
+        else:
+            per_sample += 4 + (4 if (params.query == 1 or params.kind == 1) else 0)
+            per_ray = 24 + (4 if params.kind == 1 else 0)
+        end = TIMER.bracket("encode_fwd", nbytes=n_samples * per_sample + n_rays * per_ray)
     st = _lib.load().nerf_encode_fwd(ctypes.byref(params), _ptr(x), _ptr(xdir), _ptr(ray_o), _ptr(ray_d),
                                      _ptr(t_start), _ptr(t_end), _ptr(pixel_width), n_samples, samples_per_ray,
                                      n_rays, _ptr(out), ld, _stream(out.device))
+    if end is not None:
+        end.record()
     _lib.check(st, "nerf_encode_fwd")
     return out
 
@@ -190,6 +218,42 @@ def encode_bwd(params: NerfPEParams, x: torch.Tensor, grad_out: torch.Tensor, dx
                                      _ptr(dx), int(accumulate), _stream(x.device))
     _lib.check(st, "nerf_encode_bwd")
     return dx
+
+
+def encode_bwd_integrated(params: NerfPEParams, x: torch.Tensor, xdir: torch.Tensor, t_start: torch.Tensor,
+                          t_end: torch.Tensor, pixel_width: torch.Tensor, grad_out: torch.Tensor, want_dx: bool,
+                          want_ddir: bool):
+    """(dx, ddir) of an integrated encoding; per-sample t_start / t_end / pixel_width rows."""
+    n = x.shape[0]
+    dx = torch.empty(n, 3, device=x.device, dtype=torch.float32) if want_dx else None
+    ddir = torch.empty(n, 3, device=x.device, dtype=torch.float32) if want_ddir else None
+    if grad_out.stride(1) != 1:
+        grad_out = grad_out.contiguous()
+    st = _lib.load().nerf_encode_bwd_integrated(ctypes.byref(params), _ptr(x), _ptr(xdir), _ptr(t_start),
+                                                _ptr(t_end), _ptr(pixel_width), _ptr(grad_out), grad_out.stride(0),
+                                                n, _ptr(dx), _ptr(ddir), 0, _stream(x.device))
+    _lib.check(st, "nerf_encode_bwd_integrated")
+    return dx, ddir
+
+
+# ----------------------------------------------------------------------------- gaussian activation
+def gauss_act_fwd(z: torch.Tensor, N: int, inv_std: torch.Tensor, y: torch.Tensor) -> None:
+    _require_cuda_f32("inv_standard_deviation", inv_std)
+    st = _lib.load().nerf_gauss_act_fwd(_ptr(z), z.stride(0), _ptr(inv_std), z.shape[0], N, _ptr(y), y.stride(0),
+                                        _stream(z.device))
+    _lib.check(st, "nerf_gauss_act_fwd")
+
+
+def gauss_act_bwd(grad_y: torch.Tensor, z: torch.Tensor, N: int, inv_std: torch.Tensor, grad_z: torch.Tensor,
+                  grad_inv_std: torch.Tensor) -> None:
+    M = z.shape[0]
+    lib = _lib.load()
+    ws = torch.empty(max(1, (int(lib.nerf_gauss_act_workspace(M, N)) + 7) // 8), device=z.device,
+                     dtype=torch.float64)
+    st = lib.nerf_gauss_act_bwd(_ptr(grad_y), grad_y.stride(0), _ptr(z), z.stride(0), _ptr(inv_std), M, N,
+                                _ptr(grad_z), grad_z.stride(0), _ptr(grad_inv_std), 0, _ptr(ws),
+                                ws.numel() * 8, _stream(z.device))
+    _lib.check(st, "nerf_gauss_act_bwd")
 
 
 # ----------------------------------------------------------------------------- linear layers

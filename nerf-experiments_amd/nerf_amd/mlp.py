@@ -63,9 +63,17 @@ class Source:
 
 @dataclass
 class LayerPlan:
+    """One nn.Linear of a field MLP.  Activation: ReLU (fused in the GEMM epilogue), or the
+    GARF Gaussian activation with learnable inverse std ``gauss`` (garf/gaussian.py:34-63;
+    the pre-activation is kept for the backward), or none.  ``residual`` = index of an earlier
+    layer whose output's first ``residual_cols`` columns are added to this layer's output
+    (RadianceNetwork's ``z1[:, :128] + z2[:, :128]``, garf/model_radiance.py:92)."""
     module: nn.Linear
     sources: list[Source]
     relu: bool
+    gauss: nn.Parameter | None = None
+    residual: int = -1
+    residual_cols: int = 0
     N: int = 0
     out_ld: int = 0
     Kp: int = 0
@@ -147,6 +155,8 @@ class MLPPlan:
             for s in lp.sources:
                 if s.kind == "act":
                     self.consumed[s.layer] = True
+            if lp.residual >= 0:
+                self.consumed[lp.residual] = True
 
     def to_device(self, device):
         if self.device != device:
@@ -155,9 +165,12 @@ class MLPPlan:
             self.device = device
 
     def params(self):
+        """Autograd inputs in a fixed order: per layer weight, bias (+ Gaussian inverse std)."""
         ps = []
         for lp in self.layers:
             ps += [lp.module.weight, lp.module.bias]
+            if lp.gauss is not None:
+                ps.append(lp.gauss)
         return ps
 
 
@@ -176,6 +189,7 @@ class MLPFunction(torch.autograd.Function):
         prec = matmul_precision()
         acts: list[torch.Tensor] = []
         masks: list[torch.Tensor | None] = []
+        pre: list[torch.Tensor] = []
         for idx, lp in enumerate(plan.layers):
             lp.pack(prec)
             segs = []
@@ -183,6 +197,9 @@ class MLPFunction(torch.autograd.Function):
                 t, rd = _src_tensor(s, pos, dirs, acts, dir_rd)
                 segs.append((t, s.k_seg, rd))
             out = torch.empty(M, lp.out_ld, device=pos.device, dtype=torch.float32)
+            # Gaussian layers: the GEMM writes the pre-activation z (kept for the backward),
+            # nerf_gauss_act_fwd then writes exp(-z^2 v) into the layer's output
+            target = torch.empty_like(out) if lp.gauss is not None else out
             epi = NERF_EPI_BIAS | (NERF_EPI_RELU if lp.relu else 0)
             mask = None
             if lp.relu and plan.consumed[idx] and lp.N <= 256:
@@ -190,7 +207,18 @@ class MLPFunction(torch.autograd.Function):
                 # gradient GEMMs read it instead of the fp32 activation
                 mask = torch.empty(M, 32, device=pos.device, dtype=torch.uint8)
                 epi |= NERF_EPI_MASKOUT
-            lp.gemm(prec, segs, M, False, lp.N, lp.module.bias, out, epi, aux=mask)
+            if lp.residual >= 0:
+                # out = residual + (x W^T + b): the accumulate epilogue adds onto the copied residual
+                rc = lp.residual_cols
+                target[:, rc:].zero_()
+                target[:, :rc].copy_(acts[lp.residual][:, :rc])
+                epi |= NERF_EPI_ACCUM
+            lp.gemm(prec, segs, M, False, lp.N, lp.module.bias, target, epi, aux=mask)
+            if lp.gauss is not None:
+                K.gauss_act_fwd(target, lp.N, lp.gauss, out)
+                if lp.out_ld > lp.N:
+                    out[:, lp.N:].zero_()
+                pre.append(target)
             acts.append(out)
             masks.append(mask)
         ctx.masks = masks
@@ -199,7 +227,9 @@ class MLPFunction(torch.autograd.Function):
         ctx.M = M
         ctx.dir_rd = dir_rd
         ctx.has_dirs = dirs is not None
-        ctx.save_for_backward(pos, dirs if dirs is not None else pos, *acts)
+        ctx.n_pos_cols = pos.shape[1]
+        ctx.n_dir_cols = dirs.shape[1] if dirs is not None else 0
+        ctx.save_for_backward(pos, dirs if dirs is not None else pos, *acts, *pre)
         return tuple(acts[i] for i in plan.outputs)
 
     @staticmethod
@@ -209,10 +239,13 @@ class MLPFunction(torch.autograd.Function):
         saved = ctx.saved_tensors
         pos = saved[0]
         dirs = saved[1] if ctx.has_dirs else None
-        acts = list(saved[2:])
-        dev = pos.device
         L = len(plan.layers)
+        acts = list(saved[2:2 + L])
+        pre_it = iter(saved[2 + L:])
+        pre = [next(pre_it) if lp.gauss is not None else None for lp in plan.layers]
+        dev = pos.device
         dY: list[torch.Tensor | None] = [None] * L
+        owned = [True] * L       # False: dY[i] is autograd's incoming tensor (never written in place)
         for idx, g in zip(plan.outputs, grads):
             if g is None:
                 continue
@@ -220,11 +253,12 @@ class MLPFunction(torch.autograd.Function):
                 raise RuntimeError(f"unexpected gradient shape {tuple(g.shape)} for MLP output {idx}")
             # outputs that also feed a later layer are accumulated into: never write autograd's tensor
             dY[idx] = g.contiguous().clone() if plan.consumed[idx] else g.contiguous()
+            owned[idx] = plan.consumed[idx]
         need_pos = ctx.needs_input_grad[2]
         need_dir = ctx.needs_input_grad[3]
         dpos = None
         ddir = None
-        param_grads: list[torch.Tensor | None] = [None] * (2 * L)
+        layer_grads: list[list[torch.Tensor]] = [[] for _ in range(L)]
 
         # one workspace sized for the largest weight-gradient launch
         ws_bytes = 0
@@ -237,9 +271,22 @@ class MLPFunction(torch.autograd.Function):
             dZ = dY[li]
             w = lp.module.weight
             if dZ is None:
-                param_grads[2 * li] = torch.zeros_like(w)
-                param_grads[2 * li + 1] = torch.zeros_like(lp.module.bias)
+                layer_grads[li] = [torch.zeros_like(w), torch.zeros_like(lp.module.bias)]
+                if lp.gauss is not None:
+                    layer_grads[li].append(torch.zeros_like(lp.gauss))
                 continue
+            gs = None
+            if lp.gauss is not None:
+                # dY -> dZ through the Gaussian activation (+ the inverse-std gradient)
+                gs = torch.empty_like(lp.gauss)
+                dz = dZ if owned[li] else torch.empty_like(dZ)
+                K.gauss_act_bwd(dZ, pre[li], lp.N, lp.gauss, dz, gs)
+                dZ = dz
+            if lp.residual >= 0:
+                r, rc = lp.residual, lp.residual_cols
+                if dY[r] is None:
+                    dY[r] = torch.zeros(M, plan.layers[r].out_ld, device=dev, dtype=torch.float32)
+                dY[r][:, :rc] += dZ[:, :rc]
             segs = []
             for s in lp.sources:
                 t, rd = _src_tensor(s, pos, dirs, acts, ctx.dir_rd)
@@ -253,8 +300,7 @@ class MLPFunction(torch.autograd.Function):
             else:
                 K.linear_wgrad(dZ, N4, segs, M, workspace)
             K.linear_wgrad_reduce(M, N4, lp.Kp, lp.N, workspace, lp.col_map, gW, gb)
-            param_grads[2 * li] = gW
-            param_grads[2 * li + 1] = gb
+            layer_grads[li] = [gW, gb] + ([gs] if gs is not None else [])
             # ---- input gradients
             a_seg = [(dZ, lp.out_ld, 1)]
             for s, koff in zip(lp.sources, lp.koffs):
@@ -294,6 +340,12 @@ class MLPFunction(torch.autograd.Function):
                     lp.gemm(ctx.prec, a_seg, M, True, s.k_pad, None, ddir, epi, row_offset=koff)
         if ddir is not None and ctx.dir_rd > 1:
             ddir = ddir.view(-1, ctx.dir_rd, ddir.shape[1]).sum(dim=1)
+        # the packed gradients span pad32 columns; the inputs may be narrower (e.g. [M, 4])
+        if dpos is not None and dpos.shape[1] != ctx.n_pos_cols:
+            dpos = dpos[:, :ctx.n_pos_cols]
+        if ddir is not None and ddir.shape[1] != ctx.n_dir_cols:
+            ddir = ddir[:, :ctx.n_dir_cols]
+        param_grads = [g for lg in layer_grads for g in lg]
         return (None, None, dpos, ddir, None, *param_grads)
 
 

@@ -25,7 +25,12 @@ from . import kernels as K
 
 
 class _EncodeFn(th.autograd.Function):
-    """x [N,3] (+ IPE side inputs) -> padded encoding; backward d/dx for Fourier/BARF."""
+    """x [N,3] (+ IPE side inputs) -> padded encoding.
+
+    Backward: d/dx for every encoding (nerf_encode_bwd, kind 0; nerf_encode_bwd_integrated,
+    kind 1) and d/d(dir) for the integrated encodings, whose output depends on the direction
+    through the mean shift and the diagonal variance (positional_encodings.py:190-226) — the
+    gradient BARF-style pose refinement needs.  Fourier/BARF encodings ignore dir."""
 
     @staticmethod
     def forward(ctx, x, xdir, pixel_width, t_start, t_end, enc: "PositionalEncoding"):
@@ -36,21 +41,26 @@ class _EncodeFn(th.autograd.Function):
                            out_ld=enc.padded_dim, device=x.device)
         ctx.params = params
         ctx.kind = params.kind
-        ctx.save_for_backward(x)
+        if params.kind == 1:
+            ctx.save_for_backward(x, xdir, pixel_width, t_start, t_end)
+        else:
+            ctx.save_for_backward(x)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        (x,) = ctx.saved_tensors
-        dx = None
-        if ctx.needs_input_grad[0]:
-            if ctx.kind != 0:
-                raise NotImplementedError("integrated positional encoding: gradient w.r.t. position is not "
-                                          "implemented in nerf_amd yet")
+        if any(ctx.needs_input_grad[2:5]):
+            raise NotImplementedError("nerf_amd encodings do not propagate gradients to pixel_width / t")
+        dx = ddir = None
+        if ctx.kind == 1:
+            x, xdir, pw, t0, t1 = ctx.saved_tensors
+            if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+                dx, ddir = K.encode_bwd_integrated(ctx.params, x, xdir, t0, t1, pw, g, ctx.needs_input_grad[0],
+                                                   ctx.needs_input_grad[1])
+        elif ctx.needs_input_grad[0]:
+            (x,) = ctx.saved_tensors
             dx = K.encode_bwd(ctx.params, x, g)
-        if any(ctx.needs_input_grad[1:5]):
-            raise NotImplementedError("nerf_amd encodings do not propagate gradients to dir / pixel_width / t")
-        return dx, None, None, None, None, None
+        return dx, ddir, None, None, None, None
 
 
 def _as_rows(t, n: int, device=None) -> th.Tensor | None:

@@ -16,6 +16,10 @@ Fixtures:
   model.npz      NerfModel (barf config and naive-to-vanilla config): weights, inputs, outputs, gradients
   color.npz      _compute_color end to end with explicit t, and forward coarse+fine with injected t
   cos_kat.npz    barf/cos_test_barf.pt (the reference's own fixture, loaded weights_only)
+  ipe_grad.npz   integrated encodings: outputs and gradients w.r.t. position and direction
+  garf.npz       GARF RadianceNetwork / ProposalNetwork / GaussAct: checksummed init, outputs, gradients
+
+    python tests/golden/make_golden.py [pe composite resample model color cos_kat ipe_grad garf]
 """
 from __future__ import annotations
 
@@ -258,15 +262,108 @@ def gen_cos_kat():
     np.savez_compressed(os.path.join(OUT, "cos_kat.npz"), cos=f32(t))
 
 
+def gen_ipe_grad():
+    """Autograd of the integrated encodings w.r.t. position AND direction (BARF-style pose
+    refinement through mip-NeRF's IPE), positional_encodings.py:170-282."""
+    (pe,) = _import_from("barf", ["positional_encodings"])
+    g = th.Generator().manual_seed(6)
+    N = 193
+    x = th.rand(N, 3, generator=g) * 8 - 4
+    d = th.randn(N, 3, generator=g)
+    d = d / th.linalg.vector_norm(d, dim=1, keepdim=True)
+    t0 = 2 + th.rand(N, 1, generator=g) * 6
+    t1 = t0 + th.rand(N, 1, generator=g) * 0.2 + 1e-3
+    pw = th.full((N, 1), 1 / 1111.1)
+    out = {"x": f32(x), "dir": f32(d), "t0": f32(t0), "t1": f32(t1), "pw": f32(pw)}
+    cases = {}
+    for dv in (True, False):
+        for pws in (0.0, 0.5):
+            enc = pe.IntegratedFourierFeatures(10, 2 * th.pi, True, dv)
+            enc.pixel_width_sigma = pws
+            cases[f"ipe_dv{int(dv)}_pws{pws}"] = enc
+    for dv in (True, False):
+        enc = pe.IntegratedBarfFourierFeatures(10, 6.3, 0, 1, True, 1.0, dv)
+        enc.pixel_width_sigma = 0.0
+        cases[f"ipebarf_dv{int(dv)}_a6.3"] = enc
+    for key, enc in cases.items():
+        xx = x.clone().requires_grad_(True)
+        dd = d.clone().requires_grad_(True)
+        y = enc.forward(xx, dd, pw, t0, t1)
+        gy = th.randn(y.shape, generator=g)
+        (y * gy).sum().backward()
+        out[key] = f32(y)
+        out[key + "_gy"] = f32(gy)
+        out[key + "_dx"] = f32(xx.grad)
+        out[key + "_ddir"] = f32(dd.grad)
+    np.savez_compressed(os.path.join(OUT, "ipe_grad.npz"), **out)
+
+
+def gen_garf():
+    """GARF field MLPs (barf/model_garf_radiance.py, barf/model_garf_proposal.py, barf/gaussian.py;
+    same layers as garf/model_radiance.py / model_proposal.py): th.manual_seed(0) construction with
+    the garf/main.py:29-30 Gaussian init range, forward outputs and all parameter gradients."""
+    rad_m, prop_m, gauss_m = _import_from("barf", ["model_garf_radiance", "model_garf_proposal", "gaussian"])
+    g = th.Generator().manual_seed(7)
+    out = {}
+    N = 257
+    pos = th.rand(N, 3, generator=g) * 4 - 2
+    d = th.randn(N, 3, generator=g)
+    d = d / th.linalg.vector_norm(d, dim=1, keepdim=True)
+    out["pos"], out["dir"] = f32(pos), f32(d)
+    th.manual_seed(0)
+    rad = rad_m.RadianceNetwork(0.5, 2.0, 5e-4, 5e-5, 0, 1.0, 0.0)
+    th.manual_seed(0)
+    prop = prop_m.ProposalNetwork(0.5, 2.0, 5e-4, 5e-5, 0, 1.0, 0.0)
+    for name, m in (("radiance", rad), ("proposal", prop)):
+        for k, v in m.state_dict().items():
+            out[f"{name}.sdsum.{k}"] = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+        p = pos.clone().requires_grad_(True)
+        dd = d.clone().requires_grad_(True)
+        if name == "radiance":
+            rgb, dens = m.forward(p, dd)
+            gc = th.randn(N, 3, generator=g)
+            gd = th.randn(N, generator=g)
+            ((rgb * gc).sum() + (dens * gd).sum()).backward()
+            out[f"{name}.rgb"], out[f"{name}.density"] = f32(rgb), f32(dens)
+            out[f"{name}.gc"], out[f"{name}.gd"] = f32(gc), f32(gd)
+            out[f"{name}.ddir"] = f32(dd.grad)
+        else:
+            dens = m.forward(p)
+            gd = th.randn(dens.shape, generator=g)
+            (dens * gd).sum().backward()
+            out[f"{name}.density"], out[f"{name}.gd"] = f32(dens), f32(gd)
+        out[f"{name}.dpos"] = f32(p.grad)
+        for k, prm in m.named_parameters():
+            if prm.numel() <= 4096:
+                out[f"{name}.grad.{k}"] = f32(prm.grad)
+            out[f"{name}.gradsum.{k}"] = np.array([prm.grad.double().sum().item(),
+                                                   prm.grad.double().abs().sum().item()])
+    # GaussActivation alone (forward and both gradients) on extreme inputs
+    z = th.randn(64, 48, generator=g) * 3
+    z[0, :4] = th.tensor([0.0, -0.0, 30.0, -1e-3])
+    s = th.rand(48, generator=g) * 2 - 1
+    s[0] = 0.0
+    zz = z.clone().requires_grad_(True)
+    act = gauss_m.GaussAct(48)
+    with th.no_grad():
+        act.inv_standard_deviation.copy_(s)
+    y = act(zz)
+    gy = th.randn(y.shape, generator=g)
+    (y * gy).sum().backward()
+    out.update({"act.z": f32(z), "act.s": f32(s), "act.y": f32(y), "act.gy": f32(gy), "act.dz": f32(zz.grad),
+                "act.ds": f32(act.inv_standard_deviation.grad)})
+    np.savez_compressed(os.path.join(OUT, "garf.npz"), **out)
+
+
+GENERATORS = {"pe": gen_pe, "composite": gen_composite, "resample": gen_resample, "model": gen_model,
+              "color": gen_color, "cos_kat": gen_cos_kat, "ipe_grad": gen_ipe_grad, "garf": gen_garf}
+
+
 if __name__ == "__main__":
     _install_stubs()
     th.set_num_threads(8)
-    gen_pe()
-    gen_composite()
-    gen_resample()
-    gen_model()
-    gen_color()
-    gen_cos_kat()
+    for name in (sys.argv[1:] or list(GENERATORS)):
+        GENERATORS[name]()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

@@ -70,6 +70,18 @@ def test_argument_validation_returns_status_without_launch():
     p.levels = 20
     assert lib.nerf_encode_fwd(ctypes.byref(p), None, None, None, None, None, None, None, 10, 1, 10, 16, 64,
                                None) == -1
+    p.levels = 10
+    p.kind = 0   # the integrated backward needs kind 1
+    assert lib.nerf_encode_bwd_integrated(ctypes.byref(p), 16, 16, 16, 16, 16, 16, 64, 10, 16, None, 0, None) == -1
+    p.kind = 1
+    assert lib.nerf_encode_bwd_integrated(ctypes.byref(p), None, 16, 16, 16, 16, 16, 64, 10, 16, None, 0,
+                                          None) == -1
+    assert lib.nerf_encode_bwd_integrated(ctypes.byref(p), 16, 16, 16, 16, 16, 16, 64, 0, 16, None, 0, None) == 0
+    # Gaussian activation: strides narrower than N, missing workspace
+    assert lib.nerf_gauss_act_fwd(16, 8, 16, 10, 16, 16, 16, None) == -1
+    assert lib.nerf_gauss_act_fwd(None, 16, None, 0, 16, None, 16, None) == 0
+    assert lib.nerf_gauss_act_workspace(1000, 64) >= 64 * 8
+    assert lib.nerf_gauss_act_bwd(16, 16, 16, 16, 16, 10, 16, 16, 16, 16, 0, None, 0, None) == -4
 
 
 def test_check_raises_with_message():

@@ -103,6 +103,28 @@ def test_encode_rays_matches_oracle():
         assert torch.all(got[:, 63:] == 0)
 
 
+@pytest.mark.parametrize("kind", [0, 1])
+def test_encode_layouts_agree(kind):
+    """The LDS-staged kernel (16-byte aligned rows of <= 128 columns) and the per-quad kernel
+    (wider or unaligned rows) write identical encodings; pad columns are zero."""
+    from nerf_amd import kernels as K
+    torch.manual_seed(5)
+    B, S = 29, 67
+    o = (torch.randn(B, 3) * 2).to(DEV)
+    d = torch.nn.functional.normalize(torch.randn(B, 3), dim=1).to(DEV)
+    t0 = torch.sort(2 + torch.rand(B, S) * 6, dim=1).values
+    t1 = torch.cat((t0[:, 1:], torch.full((B, 1), 8.0)), dim=1)
+    pw = torch.full((B,), 1 / 555.56, device=DEV)
+    p = K.make_pe_params(kind, 10, True, 1.0, query=1, pixel_width_sigma=0.0, distribute_variance=False,
+                         pw_mode=0, mask=[1.0] * 7 + [0.3, 0.0, 0.0])
+    outs = [K.encode_fwd(p, 63, ray_o=o, ray_d=d, t_start=t0.to(DEV), t_end=t1.to(DEV), pixel_width=pw,
+                         n_samples=B * S, samples_per_ray=S, n_rays=B, out_ld=ld, device=DEV) for ld in (64, 67, 160)]
+    for out in outs[1:]:
+        assert torch.equal(out[:, :63], outs[0][:, :63])
+        assert torch.all(out[:, 63:] == 0)
+    assert torch.all(outs[0][:, 63] == 0)
+
+
 # ----------------------------------------------------------------------------- compositing
 @pytest.mark.parametrize("S", [64, 128, 192])
 @pytest.mark.parametrize("magic", [1 / 3, 7.0])

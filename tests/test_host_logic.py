@@ -74,6 +74,43 @@ def test_mlp_lowering(name):
         assert kinds == expect
 
 
+@pytest.mark.parametrize("name", ["radiance", "proposal"])
+def test_garf_lowering_and_state_dict(golden, name):
+    """GARF networks: reference key names and init (checksums), one plan layer per Linear, a
+    Gaussian activation on every Linear followed by GaussAct, the z1 + z2 residual."""
+    from nerf_amd.model_garf import GaussAct, ProposalNetwork, RadianceNetwork, strip_compile_prefix
+    g = golden("garf")
+    torch.manual_seed(0)
+    m = (RadianceNetwork if name == "radiance" else ProposalNetwork)(0.5, 2.0, 5e-4, 5e-5, 0, 1.0, 0.0)
+    keys = sorted(k.split(".sdsum.", 1)[1] for k in g if k.startswith(f"{name}.sdsum."))
+    assert sorted(m.state_dict().keys()) == keys
+    assert len(m.param_groups) == 2
+    assert len(list(m.parameters_gaussian())) == sum(isinstance(x, GaussAct) for x in m.modules())
+    plan = m._get_plan()
+    linears = [x for x in m.modules() if isinstance(x, torch.nn.Linear)]
+    assert [id(lp.module) for lp in plan.layers] == [id(x) for x in linears]
+    n_gauss = sum(lp.gauss is not None for lp in plan.layers)
+    assert n_gauss == len(list(m.parameters_gaussian()))
+    assert len(plan.params()) == 2 * len(linears) + n_gauss
+    for lp in plan.layers:
+        lp.finalize("cpu")
+        assert sorted(c for c in lp.col_map.tolist() if c >= 0) == list(range(lp.module.in_features))
+    if name == "radiance":
+        assert plan.outputs == [7, 9]
+        assert plan.layers[7].residual == 3 and plan.layers[7].residual_cols == 128
+        assert plan.layers[7].gauss is None and plan.layers[9].gauss is None
+        assert [s.kind for s in plan.layers[4].sources] == ["act", "pos"]
+        assert [s.kind for s in plan.layers[8].sources] == ["act", "dir"]
+        assert plan.layers[8].sources[0].layer == 7 and plan.layers[8].sources[0].k_valid == 128
+        assert plan.consumed[3] and plan.consumed[7]
+    else:
+        assert plan.outputs == [3]
+    sd = {k.replace("model", "model._orig_mod", 1): v for k, v in m.state_dict().items()}
+    assert strip_compile_prefix(sd).keys() == m.state_dict().keys()
+    # garf's two-argument constructor (no learning rates): no param groups
+    assert (RadianceNetwork if name == "radiance" else ProposalNetwork)(0.5, 2.0).param_groups == []
+
+
 def test_col_map_follows_reference_concatenation():
     """Packed column j of a segment maps to the Linear input column of the same feature."""
     from nerf_amd.mlp import LayerPlan, Source

@@ -101,6 +101,72 @@ def test_resample_n2v(golden):
     np.testing.assert_array_equal(t1.numpy(), g["n2v_t1"])
 
 
+@pytest.mark.parametrize("key", ["ipe_dv1_pws0.0", "ipe_dv1_pws0.5", "ipe_dv0_pws0.0", "ipe_dv0_pws0.5",
+                                 "ipebarf_dv1_a6.3", "ipebarf_dv0_a6.3"])
+def test_integrated_pe_grads(golden, key):
+    """Autograd of the restated IPE w.r.t. position and direction vs the reference's."""
+    g = golden("ipe_grad")
+    dv = "_dv1" in key
+    barf = key.startswith("ipebarf")
+    pws = 0.5 if key.endswith("pws0.5") else 0.0
+    x = t(g["x"]).clone().requires_grad_(True)
+    d = t(g["dir"]).clone().requires_grad_(True)
+    y = O.integrated_pe(x, d, t(g["pw"]), t(g["t0"]), t(g["t1"]), 10, 1.0 if barf else 2 * np.pi, True, dv, pws,
+                        mask=O.barf_mask(6.3, 10) if barf else None)
+    np.testing.assert_allclose(y.detach().numpy(), g[key], atol=1e-6, rtol=0)
+    (y * t(g[key + "_gy"])).sum().backward()
+    np.testing.assert_allclose(x.grad.numpy(), g[key + "_dx"], atol=2e-3, rtol=1e-5)
+    np.testing.assert_allclose(d.grad.numpy(), g[key + "_ddir"], atol=2e-3, rtol=1e-5)
+
+
+def _garf_state(name):
+    """Initial parameters of the reference construction: the build's modules (host-side
+    construction only) under th.manual_seed(0), proven identical by the golden checksums."""
+    from nerf_amd.model_garf import ProposalNetwork, RadianceNetwork
+    torch.manual_seed(0)
+    m = (RadianceNetwork if name == "radiance" else ProposalNetwork)(0.5, 2.0, 5e-4, 5e-5, 0, 1.0, 0.0)
+    return m
+
+
+@pytest.mark.parametrize("name", ["radiance", "proposal"])
+def test_garf_oracle(golden, name):
+    g = golden("garf")
+    m = _garf_state(name)
+    sd = {}
+    for k, v in m.state_dict().items():
+        ref = g[f"{name}.sdsum.{k}"]
+        assert abs(v.double().sum().item() - ref[0]) <= 1e-9 * max(1.0, abs(ref[1])), k
+        assert abs(v.double().abs().sum().item() - ref[1]) <= 1e-9 * max(1.0, ref[1]), k
+        sd[k] = v.clone().requires_grad_(True)
+    pos = t(g["pos"]).clone().requires_grad_(True)
+    if name == "radiance":
+        d = t(g["dir"]).clone().requires_grad_(True)
+        rgb, dens = O.garf_radiance_forward(sd, pos, d)
+        np.testing.assert_allclose(rgb.detach().numpy(), g["radiance.rgb"], atol=1e-5, rtol=1e-5)
+        np.testing.assert_allclose(dens.detach().numpy(), g["radiance.density"], atol=1e-5, rtol=1e-5)
+        ((rgb * t(g["radiance.gc"])).sum() + (dens * t(g["radiance.gd"])).sum()).backward()
+        np.testing.assert_allclose(d.grad.numpy(), g["radiance.ddir"], atol=1e-5, rtol=1e-4)
+    else:
+        dens = O.garf_proposal_forward(sd, pos)
+        np.testing.assert_allclose(dens.detach().numpy(), g["proposal.density"], atol=1e-5, rtol=1e-5)
+        (dens * t(g["proposal.gd"])).sum().backward()
+    np.testing.assert_allclose(pos.grad.numpy(), g[f"{name}.dpos"], atol=1e-5, rtol=1e-4)
+    for k, v in sd.items():
+        s = g[f"{name}.gradsum.{k}"]
+        assert abs(v.grad.double().abs().sum().item() - s[1]) <= 1e-5 * s[1] + 1e-7, k
+
+
+def test_gauss_act_oracle(golden):
+    g = golden("garf")
+    z = t(g["act.z"]).clone().requires_grad_(True)
+    s = t(g["act.s"]).clone().requires_grad_(True)
+    y = O.gauss_act(z, s)
+    np.testing.assert_allclose(y.detach().numpy(), g["act.y"], atol=1e-7, rtol=1e-6)
+    (y * t(g["act.gy"])).sum().backward()
+    np.testing.assert_allclose(z.grad.numpy(), g["act.dz"], atol=1e-6, rtol=1e-5)
+    np.testing.assert_allclose(s.grad.numpy(), g["act.ds"], atol=1e-5, rtol=1e-5)
+
+
 def test_cos_kat():
     """barf/cos_test_barf.pt: the 10-level cos block of a 3-D PE, [x*2^0..x*2^9, y.., z..].
     Inputs were not saved: recover x from column 0 and check the double-angle chain."""
