@@ -166,6 +166,19 @@ int nerf_encode_bwd_integrated(const nerf_pe_params* params, const float* x, con
                                const float* grad_out, int64_t g_ld, int64_t n_samples,
                                float* dx, float* ddir, int32_t accumulate, void* stream);
 
+/* Backward of a ray-mode encoding (nerf_encode_fwd with x == NULL: positions o + tq*d
+ * generated in-kernel) w.r.t. the rays:
+ *   d_origs[r] = sum_s g_pos(r,s),  d_dirs[r] = sum_s (tq(r,s) * g_pos(r,s) + g_dir(r,s)),
+ * g_pos / g_dir = the encoding's gradient w.r.t. the sample position / direction (g_dir = 0 for
+ * kind 0).  This is the gradient pose refinement takes through _compute_positions
+ * (barf/model_interpolation.py:288-312) into CameraExtrinsics (model_camera_extrinsics.py:77-85).
+ * One wavefront per ray, fp64 accumulation in a fixed order.  Same params / inputs as the
+ * forward; either output may be NULL; accumulate: +=. */
+int nerf_encode_bwd_rays(const nerf_pe_params* params, const float* ray_o, const float* ray_d,
+                         const float* t_start, const float* t_end, const float* pixel_width,
+                         const float* grad_out, int64_t g_ld, int64_t n_rays, int32_t samples_per_ray,
+                         float* d_origs, float* d_dirs, int32_t accumulate, void* stream);
+
 /* Per-ray direction encoding (dir PE evaluated once per ray instead of once
  * per sample; the MLP reads row n / samples_per_ray).  kind 0 only. */
 int nerf_encode_rays(const nerf_pe_params* params, const float* ray_d, int64_t n_rays,
@@ -275,6 +288,31 @@ int nerf_gauss_act_bwd(const float* grad_y, int64_t ld_g, const float* z, int64_
                        const float* inv_std, int64_t M, int32_t N, float* grad_z, int64_t ld_dz,
                        float* grad_inv_std, int32_t accumulate, void* workspace, size_t workspace_bytes,
                        void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Fused Adam step (the optimizer of every reference experiment: torch.optim.Adam(eps=1e-5),
+ * barf/model_interpolation.py:543-584) for up to NERF_ADAM_MAX_TENSORS tensors in ONE launch.
+ * Per element, in torch's fp32 operation order:
+ *   g = grad (+ weight_decay*param);  m = m + (1-beta1)*(g-m);  v = v*beta2 + ((1-beta2)*g)*g;
+ *   param = param + step_size*(m / (sqrt(v)/bc2_sqrt + eps)),
+ * step_size = -lr/(1-beta1^t), bc2_sqrt = sqrt(1-beta2^t) (host scalars per tensor).  The
+ * table is copied by value into the kernel arguments: no device table, no copy per step.
+ * ------------------------------------------------------------------------- */
+#define NERF_ADAM_MAX_TENSORS 48
+typedef struct nerf_adam_batch {
+    int32_t n_tensors;
+    float beta1, beta2, eps;
+    float one_minus_beta1, one_minus_beta2;   /* 1 - beta as the host forms it (double -> fp32) */
+    float* param[NERF_ADAM_MAX_TENSORS];
+    const float* grad[NERF_ADAM_MAX_TENSORS];
+    float* exp_avg[NERF_ADAM_MAX_TENSORS];
+    float* exp_avg_sq[NERF_ADAM_MAX_TENSORS];
+    int64_t numel[NERF_ADAM_MAX_TENSORS];
+    float step_size[NERF_ADAM_MAX_TENSORS];
+    float bc2_sqrt[NERF_ADAM_MAX_TENSORS];
+    float weight_decay[NERF_ADAM_MAX_TENSORS];
+} nerf_adam_batch;
+int nerf_adam_step(const nerf_adam_batch* batch, void* stream);
 
 #ifdef __cplusplus
 }

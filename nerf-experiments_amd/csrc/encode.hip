@@ -183,7 +183,7 @@ constexpr int kEncMaxLd = 128;
 
 __global__ __launch_bounds__(256) void encode_fwd_lds_kernel(EncArgs a) {
 #pragma clang fp contract(off)
-    __shared__ float img[kEncRows * (kEncMaxLd + 4)];
+    extern __shared__ float img[];      // kEncRows x (ld + 4) floats (dynamic: sized to the row)
     __shared__ float spm[kEncRows][3];
     __shared__ float svb[kEncRows][3];
     const int t = threadIdx.x;
@@ -248,30 +248,74 @@ __global__ __launch_bounds__(256) void encode_fwd_lds_kernel(EncArgs a) {
     }
 }
 
-// dx[n, d] = g_id + sum_k mask_k * s_k * (-g_cos * sin(a) + g_sin * cos(a))
-__global__ __launch_bounds__(256) void encode_bwd_kernel(nerf_pe_params p, const float* __restrict__ x,
-                                                         const float* __restrict__ g, int64_t g_ld, int64_t n_total,
-                                                         float* __restrict__ dx, int accumulate) {
+// Gradient of one integrated-encoding row g w.r.t. the sample's position (gpm) and direction
+// (gdd).  Used by the per-sample kernel below and by the per-ray kernel of nerf_encode_bwd_rays.
+__device__ __forceinline__ void ipe_grad(const nerf_pe_params& p, const float pos[3], const float dv[3], float t0,
+                                         float t1, float pwv, const float* gr, float gpm[3], float gdd[3]) {
 #pragma clang fp contract(off)
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= n_total * 3) return;
-    const int64_t n = idx / 3;
-    const int dd = (int)(idx - n * 3);
     const int L = p.levels;
     const int id = p.include_identity ? 3 : 0;
-    const float xv = x[n * 3 + dd];
-    const float* gr = g + n * g_ld;
+    const IpeSample q = ipe_sample(p, pos, dv, t0, t1, pwv);
+    float gvb[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        float apm = id ? gr[d] : 0.0f;
+        float avb = 0.0f;
+        for (int k = 0; k < L; ++k) {
+            const float m = p.use_mask ? p.mask[k] : 1.0f;
+            const float sc4 = (float)(1u << (2 * k));
+            const float w = expf((-(q.vb[d] * sc4)) / 2.0f);
+            const float s = p.scale * (float)(1u << k);
+            float sn, cs;
+            sincos_enc(q.pm[d] * s, &sn, &cs);
+            const float gc = gr[id + d * L + k] * m;
+            const float gs = gr[id + 3 * L + d * L + k] * m;
+            apm += (((-gc) * sn + gs * cs) * w) * s;
+            avb += ((gc * cs + gs * sn) * w) * (-(sc4 / 2.0f));
+        }
+        gpm[d] = apm;
+        gvb[d] = avb;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) gdd[j] = gpm[j] * q.mu_diff;
+    if (!p.distribute_variance) {
+        const float S = q.ssum;
+        const float cross = ((gvb[0] * (dv[0] * dv[0]) + gvb[1] * (dv[1] * dv[1])) + gvb[2] * (dv[2] * dv[2])) *
+                            ((2.0f * q.sr) / (S * S));
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            gdd[j] += (2.0f * dv[j]) * ((q.st - q.sr / S) * gvb[j]) + dv[j] * cross;
+    }
+}
+
+// Gradient of one Fourier/BARF row g w.r.t. coordinate d of the position:
+//   g_id + sum_k mask_k * s_k * (-g_cos * sin(a) + g_sin * cos(a))
+__device__ __forceinline__ float fourier_grad(const nerf_pe_params& p, float xv, int dd, const float* gr) {
+#pragma clang fp contract(off)
+    const int L = p.levels;
+    const int id = p.include_identity ? 3 : 0;
     float acc = id ? gr[dd] : 0.0f;
     for (int k = 0; k < L; ++k) {
         const float s = p.scale * (float)(1u << k);
-        const float arg = xv * s;
         float sn, cs;
-        sincos_enc(arg, &sn, &cs);
+        sincos_enc(xv * s, &sn, &cs);
         const float m = p.use_mask ? p.mask[k] : 1.0f;
         const float gc = gr[id + dd * L + k];
         const float gs = gr[id + 3 * L + dd * L + k];
         acc += ((-(gc * m) * sn) + (gs * m) * cs) * s;
     }
+    return acc;
+}
+
+// dx[n, d] for Fourier/BARF encodings of an explicit position input, one thread per (n, d).
+__global__ __launch_bounds__(256) void encode_bwd_kernel(nerf_pe_params p, const float* __restrict__ x,
+                                                         const float* __restrict__ g, int64_t g_ld, int64_t n_total,
+                                                         float* __restrict__ dx, int accumulate) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n_total * 3) return;
+    const int64_t n = idx / 3;
+    const int dd = (int)(idx - n * 3);
+    float acc = fourier_grad(p, x[n * 3 + dd], dd, g + n * g_ld);
     if (accumulate) acc += dx[idx];
     dx[idx] = acc;
 }
@@ -292,51 +336,61 @@ __global__ __launch_bounds__(256) void encode_bwd_integrated_kernel(
 #pragma clang fp contract(off)
     const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= n_total) return;
-    const int L = p.levels;
-    const int id = p.include_identity ? 3 : 0;
     float pos[3], dv[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
         pos[d] = x[n * 3 + d];
         dv[d] = xdir[n * 3 + d];
     }
-    const IpeSample q = ipe_sample(p, pos, dv, t0[n], t1[n], pw[n]);
-    const float* gr = g + n * g_ld;
-    float gpm[3], gvb[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        float apm = id ? gr[d] : 0.0f;
-        float avb = 0.0f;
-        for (int k = 0; k < L; ++k) {
-            const float m = p.use_mask ? p.mask[k] : 1.0f;
-            const float sc4 = (float)(1u << (2 * k));
-            const float w = expf((-(q.vb[d] * sc4)) / 2.0f);
-            const float s = p.scale * (float)(1u << k);
-            float sn, cs;
-            sincos_enc(q.pm[d] * s, &sn, &cs);
-            const float gc = gr[id + d * L + k] * m;
-            const float gs = gr[id + 3 * L + d * L + k] * m;
-            apm += (((-gc) * sn + gs * cs) * w) * s;
-            avb += ((gc * cs + gs * sn) * w) * (-(sc4 / 2.0f));
-        }
-        gpm[d] = apm;
-        gvb[d] = avb;
-    }
-    float dd[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) dd[j] = gpm[j] * q.mu_diff;
-    if (!p.distribute_variance) {
-        const float S = q.ssum;
-        const float cross = ((gvb[0] * (dv[0] * dv[0]) + gvb[1] * (dv[1] * dv[1])) + gvb[2] * (dv[2] * dv[2])) *
-                            ((2.0f * q.sr) / (S * S));
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-            dd[j] += (2.0f * dv[j]) * ((q.st - q.sr / S) * gvb[j]) + dv[j] * cross;
-    }
+    float gpm[3], dd[3];
+    ipe_grad(p, pos, dv, t0[n], t1[n], pw[n], g + n * g_ld, gpm, dd);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         if (dx) dx[n * 3 + j] = accumulate ? dx[n * 3 + j] + gpm[j] : gpm[j];
         if (ddir) ddir[n * 3 + j] = accumulate ? ddir[n * 3 + j] + dd[j] : dd[j];
+    }
+}
+
+// Ray-mode backward (positions generated in-kernel from rays, nerf_encode_fwd with x == NULL):
+//   pos_s = o + tq_s * d  =>  dL/do = sum_s g_pos_s,  dL/dd = sum_s (tq_s * g_pos_s + g_dir_s)
+// where g_dir_s is the integrated encoding's own direction gradient (0 for Fourier/BARF).  One
+// wavefront per ray; lanes stride over the samples, fp64 accumulation, fixed-order wave sum.
+// This is the gradient the reference's pose refinement takes through _compute_positions
+// (barf/model_interpolation.py:288-312) into CameraExtrinsics (model_camera_extrinsics.py:77-85).
+__global__ __launch_bounds__(256) void encode_bwd_rays_kernel(EncArgs a, const float* __restrict__ g, int64_t g_ld,
+                                                              float* __restrict__ d_o, float* __restrict__ d_d,
+                                                              int accumulate) {
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x & 63;
+    const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (ray >= a.n_rays) return;
+    double ao[3] = {0.0, 0.0, 0.0}, ad[3] = {0.0, 0.0, 0.0};
+    for (int s = lane; s < a.S; s += 64) {
+        const int64_t n = ray * a.S + s;
+        float p[3], dv[3];
+        load_pos_dir(a, n, p, dv);
+        const float tq = (a.p.query == 0) ? a.t0[n] : (a.t0[n] + a.t1[n]) / 2.0f;
+        const float* gr = g + n * g_ld;
+        float gp[3], gd[3] = {0.f, 0.f, 0.f};
+        if (a.p.kind == 1) {
+            ipe_grad(a.p, p, dv, a.t0[n], a.t1[n], pixel_width_at(a, n), gr, gp, gd);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) gp[j] = fourier_grad(a.p, p[j], j, gr);
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            ao[j] += (double)gp[j];
+            ad[j] += (double)(tq * gp[j]) + (double)gd[j];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const double so = wave_sum(ao[j]), sd = wave_sum(ad[j]);
+        if (lane == 0) {
+            if (d_o) d_o[ray * 3 + j] = accumulate ? d_o[ray * 3 + j] + (float)so : (float)so;
+            if (d_d) d_d[ray * 3 + j] = accumulate ? d_d[ray * 3 + j] + (float)sd : (float)sd;
+        }
     }
 }
 
@@ -368,7 +422,8 @@ extern "C" int nerf_encode_fwd(const nerf_pe_params* params, const float* x, con
               samples_per_ray > 0 ? samples_per_ray : 1, n_rays, out, out_ld, od, vec};
     if (vec && out_ld <= kEncMaxLd) {
         const int64_t blocks = (n_samples + kEncRows - 1) / kEncRows;
-        hipLaunchKernelGGL(encode_fwd_lds_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
+        const size_t lds = (size_t)kEncRows * (size_t)(out_ld + 4) * sizeof(float);
+        hipLaunchKernelGGL(encode_fwd_lds_kernel, dim3((unsigned)blocks), dim3(256), lds, as_stream(stream), a);
     } else {
         const int Q = (int)((out_ld + 3) / 4);      // threads per row (4 columns each)
         const int RB = 256 / Q;                     // rows per block
@@ -404,6 +459,28 @@ extern "C" int nerf_encode_bwd_integrated(const nerf_pe_params* params, const fl
     hipLaunchKernelGGL(encode_bwd_integrated_kernel, dim3((unsigned)((n_samples + 255) / 256)), dim3(256), 0,
                        as_stream(stream), *params, x, xdir, t_start, t_end, pixel_width, grad_out, g_ld, n_samples,
                        dx, ddir, accumulate);
+    NERF_CHECK_LAUNCH();
+    return NERF_OK;
+}
+
+extern "C" int nerf_encode_bwd_rays(const nerf_pe_params* params, const float* ray_o, const float* ray_d,
+                                    const float* t_start, const float* t_end, const float* pixel_width,
+                                    const float* grad_out, int64_t g_ld, int64_t n_rays, int32_t samples_per_ray,
+                                    float* d_origs, float* d_dirs, int32_t accumulate, void* stream) {
+    NERF_REQUIRE(params && n_rays >= 0 && samples_per_ray >= 1);
+    if (n_rays == 0) return NERF_OK;
+    const nerf_pe_params& p = *params;
+    NERF_REQUIRE(p.levels >= 0 && p.levels <= 16 && (p.kind == 0 || p.kind == 1));
+    NERF_REQUIRE(ray_o && ray_d && t_start && grad_out && (d_origs || d_dirs));
+    NERF_REQUIRE(g_ld >= out_dim_of(p));
+    if (p.query != 0 || p.kind == 1) NERF_REQUIRE(t_end != nullptr);
+    if (p.kind == 1) NERF_REQUIRE(pixel_width != nullptr && p.pw_mode >= 0 && p.pw_mode <= 2);
+    const int64_t n = n_rays * (int64_t)samples_per_ray;
+    NERF_REQUIRE(n < (1ll << 31));
+    EncArgs a{p, nullptr, nullptr, ray_o, ray_d, t_start, t_end, pixel_width, n, samples_per_ray, n_rays,
+              nullptr, g_ld, out_dim_of(p), 0};
+    hipLaunchKernelGGL(encode_bwd_rays_kernel, dim3((unsigned)((n_rays + 3) / 4)), dim3(256), 0, as_stream(stream), a,
+                       grad_out, g_ld, d_origs, d_dirs, accumulate);
     NERF_CHECK_LAUNCH();
     return NERF_OK;
 }

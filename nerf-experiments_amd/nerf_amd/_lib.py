@@ -53,6 +53,28 @@ class NerfPEParams(ctypes.Structure):
     ]
 
 
+NERF_ADAM_MAX_TENSORS = 48
+
+
+class NerfAdamBatch(ctypes.Structure):
+    _fields_ = [
+        ("n_tensors", c_i32),
+        ("beta1", c_f),
+        ("beta2", c_f),
+        ("eps", c_f),
+        ("one_minus_beta1", c_f),
+        ("one_minus_beta2", c_f),
+        ("param", c_vp * NERF_ADAM_MAX_TENSORS),
+        ("grad", c_vp * NERF_ADAM_MAX_TENSORS),
+        ("exp_avg", c_vp * NERF_ADAM_MAX_TENSORS),
+        ("exp_avg_sq", c_vp * NERF_ADAM_MAX_TENSORS),
+        ("numel", c_i64 * NERF_ADAM_MAX_TENSORS),
+        ("step_size", c_f * NERF_ADAM_MAX_TENSORS),
+        ("bc2_sqrt", c_f * NERF_ADAM_MAX_TENSORS),
+        ("weight_decay", c_f * NERF_ADAM_MAX_TENSORS),
+    ]
+
+
 # name -> (restype, argtypes)
 _SIGNATURES = {
     "nerf_abi_version": (c_i32, []),
@@ -69,7 +91,10 @@ _SIGNATURES = {
     "nerf_encode_bwd": (c_i32, [ctypes.POINTER(NerfPEParams), c_vp, c_vp, c_i64, c_i64, c_vp, c_i32, c_vp]),
     "nerf_encode_bwd_integrated": (c_i32, [ctypes.POINTER(NerfPEParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                            c_i64, c_i64, c_vp, c_vp, c_i32, c_vp]),
+    "nerf_encode_bwd_rays": (c_i32, [ctypes.POINTER(NerfPEParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
+                                     c_i64, c_i32, c_vp, c_vp, c_i32, c_vp]),
     "nerf_encode_rays": (c_i32, [ctypes.POINTER(NerfPEParams), c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "nerf_adam_step": (c_i32, [ctypes.POINTER(NerfAdamBatch), c_vp]),
     "nerf_gauss_act_workspace": (c_sz, [c_i64, c_i32]),
     "nerf_gauss_act_fwd": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp]),
     "nerf_gauss_act_bwd": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_i32,

@@ -15,15 +15,16 @@ import torch.distributed as dist
 class GradAllReduce:
     """Averages ``.grad`` of ``params`` across the process group with ONE collective.
 
-    Gradients are packed into a persistent flat buffer (allocated once), reduced
-    in place and copied back; parameters without a gradient contribute zeros so
-    every rank issues the same collective."""
+    The gradients are concatenated into one flat fp32 bucket (a single copy kernel), reduced
+    in place, scaled by 1/world, and every parameter's ``.grad`` becomes a view of its slice of
+    the bucket — no copy back (3 kernels + the collective per step instead of ~2 per parameter).
+    Parameters without a gradient contribute zeros so every rank issues the same collective."""
 
     def __init__(self, params, group=None):
         self.params = [p for p in params if p.requires_grad]
         self.group = group
-        self.numel = sum(p.numel() for p in self.params)
-        self.flat = None
+        self.sizes = [p.numel() for p in self.params]
+        self.numel = sum(self.sizes)
 
     def __call__(self) -> None:
         if not dist.is_available() or not dist.is_initialized():
@@ -31,28 +32,12 @@ class GradAllReduce:
         world = dist.get_world_size(self.group)
         if world == 1:
             return
-        dev = self.params[0].device
-        if self.flat is None or self.flat.device != dev:
-            self.flat = torch.empty(self.numel, device=dev, dtype=torch.float32)
-        off = 0
-        for p in self.params:
-            n = p.numel()
-            if p.grad is None:
-                self.flat[off:off + n].zero_()
-            else:
-                self.flat[off:off + n].copy_(p.grad.reshape(-1))
-            off += n
-        dist.all_reduce(self.flat, group=self.group)
-        self.flat.div_(world)
-        off = 0
-        for p in self.params:
-            n = p.numel()
-            g = self.flat[off:off + n].view_as(p)
-            if p.grad is None:
-                p.grad = g.clone()
-            else:
-                p.grad.copy_(g)
-            off += n
+        grads = [(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in self.params]
+        flat = torch.cat(grads)
+        dist.all_reduce(flat, group=self.group)
+        flat.div_(world)
+        for p, g in zip(self.params, flat.split(self.sizes)):
+            p.grad = g.view_as(p)
 
 
 def shard_rays(n_global: int, rank: int, world: int) -> slice:

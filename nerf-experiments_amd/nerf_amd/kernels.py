@@ -236,6 +236,46 @@ def encode_bwd_integrated(params: NerfPEParams, x: torch.Tensor, xdir: torch.Ten
     return dx, ddir
 
 
+def encode_bwd_rays(params: NerfPEParams, ray_o: torch.Tensor, ray_d: torch.Tensor, t_start: torch.Tensor,
+                    t_end: torch.Tensor, pixel_width: torch.Tensor | None, grad_out: torch.Tensor,
+                    samples_per_ray: int, want_do: bool, want_dd: bool):
+    """(dL/d origins, dL/d directions) [n_rays, 3] of a ray-mode encoding."""
+    n_rays = ray_o.shape[0]
+    d_o = torch.empty(n_rays, 3, device=ray_o.device, dtype=torch.float32) if want_do else None
+    d_d = torch.empty(n_rays, 3, device=ray_o.device, dtype=torch.float32) if want_dd else None
+    if grad_out.stride(1) != 1:
+        grad_out = grad_out.contiguous()
+    st = _lib.load().nerf_encode_bwd_rays(ctypes.byref(params), _ptr(ray_o), _ptr(ray_d), _ptr(t_start),
+                                          _ptr(t_end), _ptr(pixel_width), _ptr(grad_out), grad_out.stride(0), n_rays,
+                                          samples_per_ray, _ptr(d_o), _ptr(d_d), 0, _stream(ray_o.device))
+    _lib.check(st, "nerf_encode_bwd_rays")
+    return d_o, d_d
+
+
+# ----------------------------------------------------------------------------- optimizer
+def adam_step(entries, beta1: float, beta2: float, eps: float, device) -> None:
+    """entries: (param, grad, exp_avg, exp_avg_sq, step_size, bc2_sqrt, weight_decay) of fp32
+    contiguous device tensors; one nerf_adam_step launch per NERF_ADAM_MAX_TENSORS entries."""
+    lib = _lib.load()
+    cap = _lib.NERF_ADAM_MAX_TENSORS
+    for c in range(0, len(entries), cap):
+        chunk = entries[c:c + cap]
+        b = _lib.NerfAdamBatch()
+        b.n_tensors = len(chunk)
+        b.beta1, b.beta2, b.eps = beta1, beta2, eps
+        b.one_minus_beta1, b.one_minus_beta2 = 1 - beta1, 1 - beta2
+        for i, (p, g, m, v, step, bc2s, wd) in enumerate(chunk):
+            for name, t in (("param", p), ("grad", g), ("exp_avg", m), ("exp_avg_sq", v)):
+                _require_cuda_f32(name, t)
+                if not t.is_contiguous() or t.numel() != p.numel():
+                    raise ValueError(f"adam: {name} must be contiguous with the parameter's size")
+            b.param[i], b.grad[i], b.exp_avg[i], b.exp_avg_sq[i] = p.data_ptr(), g.data_ptr(), m.data_ptr(), \
+                v.data_ptr()
+            b.numel[i] = p.numel()
+            b.step_size[i], b.bc2_sqrt[i], b.weight_decay[i] = step, bc2s, wd
+        _lib.check(lib.nerf_adam_step(ctypes.byref(b), _stream(device)), "nerf_adam_step")
+
+
 # ----------------------------------------------------------------------------- gaussian activation
 def gauss_act_fwd(z: torch.Tensor, N: int, inv_std: torch.Tensor, y: torch.Tensor) -> None:
     _require_cuda_f32("inv_standard_deviation", inv_std)

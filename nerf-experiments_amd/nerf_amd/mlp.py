@@ -186,6 +186,9 @@ class MLPFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, plan: MLPPlan, M: int, pos: torch.Tensor, dirs: torch.Tensor | None, dir_rd: int, *params):
         plan.to_device(pos.device)
+        # outputs the caller never uses get None gradients instead of materialised zeros
+        # (NerfModel with delayed density never reads z_last: a 268 MB memset + clone per step)
+        ctx.set_materialize_grads(False)
         prec = matmul_precision()
         acts: list[torch.Tensor] = []
         masks: list[torch.Tensor | None] = []

@@ -24,6 +24,7 @@ import torch.nn as nn
 
 from . import kernels as K
 from .model_interpolation_architecture import NerfModel, RawHeads
+from .optim import FusedAdam
 
 uniform_sampling_strategies = Literal["stratified_uniform", "equidistant"]
 integration_strategies = Literal["left", "middle"]
@@ -83,7 +84,12 @@ class _CompositeRawFn(th.autograd.Function):
         dens_col, shift, B, S, sa, sb, same = ctx.meta
         if g_rgb is None:
             g_rgb = th.zeros(B, 3, device=distances.device)
-        g_color = th.zeros_like(color_base)
+        # the kernel writes columns 0..2 of g_color and column dens_col of g_dens: other columns
+        # must read as zero for the MLP backward, unless the head buffer is exactly [rgb | sigma]
+        if same and color_base.shape[1] == 4 and dens_col == 3:
+            g_color = th.empty_like(color_base)
+        else:
+            g_color = th.zeros_like(color_base)
         g_dens = g_color if same else th.zeros_like(dens_base)
         ds = dens_base.stride(0)
         K.composite_bwd(dens_base.view(-1)[dens_col:], ds, color_base, color_base.stride(0), distances, B, S,
@@ -200,8 +206,9 @@ class NerfInterpolation(nn.Module):
     def _compute_color(self, model, t_start, t_end, ray_origs, ray_dirs, pixel_width, batch_size: int,
                        samples_per_ray: int):
         sample_dist = t_end - t_start
-        fused = isinstance(model, NerfModel) and not (ray_origs.requires_grad or ray_dirs.requires_grad)
-        if fused:
+        if isinstance(model, NerfModel):
+            # fused: positions in the encoding kernel, direction encoding once per ray, activations
+            # in the compositor; gradients reach the rays through nerf_encode_bwd_rays
             query = 0 if self.integration_strategy == "left" else 1
             if self.integration_strategy not in ("left", "middle"):
                 raise ValueError(f"strategy must be one of ('left', 'middle'), was '{self.integration_strategy}'")
@@ -211,7 +218,7 @@ class NerfInterpolation(nn.Module):
                                      pw_mode)
             rgb, weights = composite_raw(heads, sample_dist, batch_size, samples_per_ray, *self.density_factor)
             return rgb, weights, sample_dist
-        # generic path (any model with the reference forward signature, or rays that need gradients)
+        # generic path (any model with the reference forward signature)
         sample_pos, sample_dir = self._compute_positions(ray_origs, ray_dirs, t_start, t_end)
         n = batch_size * samples_per_ray
         sample_pixel_width = pixel_width.repeat(1, samples_per_ray).view(n, 1)
@@ -257,8 +264,14 @@ class NerfInterpolation(nn.Module):
         return loss, logs
 
     def configure_optimizers(self):
-        optimizer = th.optim.Adam([{"params": g["parameters"], "lr": g["learning_rate_start"],
-                                    "weight_decay": g["weight_decay"]} for g in self.param_groups], eps=1e-5)
+        # Adam(eps=1e-5) as the reference (model_interpolation.py:543-584).  On the GPU it is
+        # nerf_amd's FusedAdam: a torch.optim.Adam whose step is one HIP launch and which bumps
+        # the parameters' version counters (torch's fused=True does not, so the MLP's
+        # version-keyed packed weights went stale: tools/diag/train_ab.py)
+        groups = [{"params": list(g["parameters"]), "lr": g["learning_rate_start"],
+                   "weight_decay": g["weight_decay"]} for g in self.param_groups]
+        on_gpu = all(p.is_cuda for g in groups for p in g["params"])
+        optimizer = (FusedAdam if on_gpu else th.optim.Adam)(groups, eps=1e-5)
         lr_scheduler = SchedulerLeNice(optimizer,
                                        start_LR=[g["learning_rate_start"] for g in self.param_groups],
                                        stop_LR=[g["learning_rate_stop"] for g in self.param_groups],

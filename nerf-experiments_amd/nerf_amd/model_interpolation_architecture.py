@@ -141,9 +141,11 @@ class NerfModel(NerfBaseModel):
     def render_raw(self, ray_origs: th.Tensor, ray_dirs: th.Tensor, pixel_width: th.Tensor | None,
                    t_start: th.Tensor, t_end: th.Tensor, samples_per_ray: int, query: int,
                    pw_mode: int) -> RawHeads:
-        """Raw head outputs for every (ray, sample); positions generated in-kernel."""
+        """Raw head outputs for every (ray, sample); positions generated in-kernel.  Differentiable
+        w.r.t. ray_origs / ray_dirs (pose refinement): the position encoding's ray-mode backward plus
+        the per-ray direction encoding's backward."""
         pos_pe = self.position_encoder.encode_rays(ray_origs, ray_dirs, t_start, t_end, pixel_width,
                                                    samples_per_ray, query, pw_mode)
-        dir_pe = self.direction_encoder.encode_padded(ray_dirs.detach())
+        dir_pe = self.direction_encoder.encode_padded(ray_dirs)
         z_last, head = self._run_mlp(pos_pe, dir_pe, samples_per_ray)
         return self._heads(z_last, head)

@@ -63,6 +63,38 @@ class _EncodeFn(th.autograd.Function):
         return dx, ddir, None, None, None, None
 
 
+class _EncodeRaysFn(th.autograd.Function):
+    """Encoding of o + t_query * d for every (ray, sample), positions generated in-kernel
+    (fuses _compute_positions, model_interpolation.py:288-312).  Backward: dL/d origins and
+    dL/d directions per ray (nerf_encode_bwd_rays) — BARF pose refinement's gradient path."""
+
+    @staticmethod
+    def forward(ctx, ray_o, ray_d, t_start, t_end, pixel_width, enc: "PositionalEncoding", samples_per_ray: int,
+                query: int, pw_mode: int):
+        params = enc._pe_params(query=query, pw_mode=pw_mode)
+        n_rays = ray_o.shape[0]
+        out = K.encode_fwd(params, enc.output_dim, ray_o=ray_o, ray_d=ray_d, t_start=t_start, t_end=t_end,
+                           pixel_width=pixel_width, n_samples=n_rays * samples_per_ray,
+                           samples_per_ray=samples_per_ray, n_rays=n_rays, out_ld=enc.padded_dim,
+                           device=ray_o.device)
+        ctx.params = params
+        ctx.S = samples_per_ray
+        ctx.has_pw = pixel_width is not None
+        ctx.save_for_backward(ray_o, ray_d, t_start, t_end, pixel_width if pixel_width is not None else ray_o)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        if any(ctx.needs_input_grad[2:5]):
+            raise NotImplementedError("nerf_amd encodings do not propagate gradients to t / pixel_width")
+        ray_o, ray_d, t0, t1, pw = ctx.saved_tensors
+        d_o = d_d = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            d_o, d_d = K.encode_bwd_rays(ctx.params, ray_o, ray_d, t0, t1, pw if ctx.has_pw else None, g, ctx.S,
+                                         ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        return d_o, d_d, None, None, None, None, None, None, None
+
+
 def _as_rows(t, n: int, device=None) -> th.Tensor | None:
     if t is None:
         return None
@@ -108,19 +140,12 @@ class PositionalEncoding(nn.Module):
 
     def encode_rays(self, ray_origs: th.Tensor, ray_dirs: th.Tensor, t_start: th.Tensor, t_end: th.Tensor,
                     pixel_width: th.Tensor | None, samples_per_ray: int, query: int, pw_mode: int) -> th.Tensor:
-        """Encoding of o + t_query*d for every (ray, sample); no gradient to the rays."""
-        if ray_origs.requires_grad or ray_dirs.requires_grad:
-            raise ValueError("encode_rays does not propagate gradients to rays; use encode_padded")
-        n_rays = ray_origs.shape[0]
-        n = n_rays * samples_per_ray
-        params = self._pe_params(query=query, pw_mode=pw_mode)
+        """Encoding of o + t_query*d for every (ray, sample); differentiable w.r.t. the rays."""
         pw = None
-        if params.kind == 1:
+        if isinstance(self, (IntegratedFourierFeatures, IntegratedBarfFourierFeatures)):
             pw = pixel_width.reshape(-1).contiguous().float()
-        return K.encode_fwd(params, self.output_dim, ray_o=ray_origs.contiguous(), ray_d=ray_dirs.contiguous(),
-                            t_start=t_start.contiguous(), t_end=t_end.contiguous(), pixel_width=pw,
-                            n_samples=n, samples_per_ray=samples_per_ray, n_rays=n_rays,
-                            out_ld=self.padded_dim, device=ray_origs.device)
+        return _EncodeRaysFn.apply(ray_origs.contiguous(), ray_dirs.contiguous(), t_start.contiguous(),
+                                   t_end.contiguous(), pw, self, samples_per_ray, query, pw_mode)
 
 
 class IdentityPositionalEncoding(PositionalEncoding):

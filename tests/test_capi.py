@@ -82,6 +82,20 @@ def test_argument_validation_returns_status_without_launch():
     assert lib.nerf_gauss_act_fwd(None, 16, None, 0, 16, None, 16, None) == 0
     assert lib.nerf_gauss_act_workspace(1000, 64) >= 64 * 8
     assert lib.nerf_gauss_act_bwd(16, 16, 16, 16, 16, 10, 16, 16, 16, 16, 0, None, 0, None) == -4
+    # ray-mode encoding backward: missing rays / outputs
+    p.kind = 0
+    assert lib.nerf_encode_bwd_rays(ctypes.byref(p), None, 16, 16, 16, None, 16, 64, 4, 8, 16, 16, 0, None) == -1
+    assert lib.nerf_encode_bwd_rays(ctypes.byref(p), 16, 16, 16, 16, None, 16, 64, 4, 8, None, None, 0, None) == -1
+    assert lib.nerf_encode_bwd_rays(ctypes.byref(p), 16, 16, 16, 16, None, 16, 64, 0, 8, 16, 16, 0, None) == 0
+    # fused Adam: table bounds and null pointers
+    b = _lib.NerfAdamBatch()
+    b.n_tensors = 49
+    assert lib.nerf_adam_step(ctypes.byref(b), None) == -1
+    b.n_tensors = 1
+    b.numel[0] = 10
+    assert lib.nerf_adam_step(ctypes.byref(b), None) == -1
+    b.numel[0] = 0
+    assert lib.nerf_adam_step(ctypes.byref(b), None) == 0
 
 
 def test_check_raises_with_message():
