@@ -1,20 +1,28 @@
 #!/usr/bin/env python3
 """Headline benchmark: NeRF training-step throughput in ray-samples/s.
 
-Workload (BASELINE.json configs[1]): naive-to-vanilla NeRF at the Lego 400x400
-setting — per GPU 4096 rays x 64 stratified samples per step, NerfModel with
-n_hidden=4, hidden_dim=256, 2 segments, delayed direction + density, Fourier
-position encoding (L=10, scale 2*pi) and direction encoding (L=4, scale 1),
-near/far 0.1/0.333, density factor 3*7 (naive-to-vanilla/main.py:89-102,
-model_interpolation.py:8,97-125,198-235).  A step is the whole training step:
-t sampling -> encodings -> 12-layer MLP -> compositing -> MSE -> backward ->
-(N>1: RCCL all-reduce of the flat gradient) -> Adam.  Synthetic Lego-shaped
-rays and target colours (no dataset is available offline).
+Default workload (BASELINE.json configs[1], the headline line): naive-to-vanilla NeRF at the
+Lego 400x400 setting — per GPU 4096 rays x 64 stratified samples per step, NerfModel with
+n_hidden=4, hidden_dim=256, 2 segments, delayed direction + density, Fourier position encoding
+(L=10, scale 2*pi) and direction encoding (L=4, scale 1), near/far 0.1/0.333, density factor 3*7
+(naive-to-vanilla/main.py:89-102, model_interpolation.py:8,97-125,198-235).  A step is the whole
+training step: t sampling -> encodings -> 12-layer MLP -> compositing -> MSE -> backward ->
+(N>1: RCCL all-reduce of the flat gradient) -> Adam.  Synthetic Lego-shaped rays and target
+colours (no dataset is available offline).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+Other BASELINE.json configs as extra workloads (same JSON line, their own `config`):
+  --workload mip   configs[2]: mip-NeRF masked integrated PE, coarse 64 + fine 128 samples through
+                   the pdf resample, one shared NerfModel (barf/model_builders.py:106-195,
+                   model_mip.py), Lego 800x800 pixel width, 4096 rays per GPU
+  --workload barf  configs[3]: BARF pose refinement — masked Fourier PE L10/L4 + identity, 128
+                   equidistant samples (run_barf.py:150-196), rays refined by per-image so3
+                   CameraExtrinsics (100 views) whose gradients come back through the fused
+                   ray-mode encoding backward, 4096 rays per GPU
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload n2v|mip|barf]
     (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
 
-Prints ONE JSON line on rank 0 (schema: see README / DESIGN.md §Measurement).
+Prints ONE JSON line on rank 0 (schema: see DESIGN.md §Measurement).
 """
 from __future__ import annotations
 
@@ -40,6 +48,17 @@ RAYS = 4096
 SAMPLES = 64
 NEAR, FAR = 0.1, 1.0 / 3.0
 
+WORKLOADS = {
+    "n2v": {"config": "naive-to-vanilla NeRF training step, Lego 400x400, 4096 rays x 64 samples per GPU "
+                      "(BASELINE.json configs[1])", "rays": RAYS, "coarse": 0, "fine": SAMPLES},
+    "mip": {"config": "mip-NeRF masked integrated PE, coarse 64 + fine 128 samples (pdf resample), shared "
+                      "NerfModel, Lego 800x800, 4096 rays per GPU (BASELINE.json configs[2])",
+            "rays": 4096, "coarse": 64, "fine": 128},
+    "barf": {"config": "BARF camera-pose refinement: masked Fourier PE L10/L4 + identity, 128 equidistant "
+                       "samples, per-image so3 CameraExtrinsics (100 views), 4096 rays per GPU "
+                       "(BASELINE.json configs[3])", "rays": 4096, "coarse": 0, "fine": 128},
+}
+
 
 def synthetic_batch(n_rays: int, seed: int, device):
     """Lego-shaped rays in naive-to-vanilla's normalised space: camera centres on the upper
@@ -57,6 +76,24 @@ def synthetic_batch(n_rays: int, seed: int, device):
     return o.to(device), d.to(device), pw.to(device), target.to(device)
 
 
+def synthetic_batch_lego(n_rays: int, seed: int, device, image_size: int):
+    """Blender-Lego-scale rays in barf space: camera centres at radius 4.03 on the upper hemisphere
+    looking at the origin, pixel width 1/focal for the given image size."""
+    g = torch.Generator().manual_seed(seed)
+    u = torch.rand(n_rays, 2, generator=g)
+    theta = u[:, 0] * 2 * math.pi
+    z = u[:, 1] * 0.9 + 0.1
+    r = torch.sqrt(1 - z * z)
+    o = torch.stack((r * torch.cos(theta), r * torch.sin(theta), z), dim=1) * 4.03
+    jitter = (torch.rand(n_rays, 3, generator=g) - 0.5) * 0.5
+    d = torch.nn.functional.normalize(-o + jitter, dim=1)
+    focal = image_size / 2 / math.tan(0.6911112 / 2)
+    pw = torch.full((n_rays,), 1.0 / focal)
+    target = 0.5 + 0.5 * torch.sin(torch.stack((3 * d[:, 0], 5 * d[:, 1] + 1, 7 * d[:, 2] + 2), dim=1))
+    img = torch.randint(0, 100, (n_rays,), generator=g)
+    return o.to(device), d.to(device), pw.to(device), target.to(device), img.to(device)
+
+
 def build_model(device):
     from nerf_amd import FourierFeatures, NerfInterpolation, NerfModel
     torch.manual_seed(0)
@@ -65,6 +102,56 @@ def build_model(device):
     ren = NerfInterpolation(NEAR, FAR, model, SAMPLES, "stratified_uniform", 0.0, "middle",
                             density_factor=(3.0, 7.0)).to(device)
     return ren
+
+
+def build_workload(name: str, device, rank: int):
+    """(renderer, extra modules, step closure factory inputs) for one workload."""
+    from nerf_amd import (BarfPositionalEncoding, FusedAdam, IntegratedBarfFourierFeatures, NerfInterpolation,
+                          NerfModel)
+    from nerf_amd.model_camera_extrinsics import CameraExtrinsics
+    w = WORKLOADS[name]
+    if name == "n2v":
+        ren = build_model(device)
+        o, d, pw, target = synthetic_batch(w["rays"], 1000 + rank, device)
+        opt = ren.configure_optimizers()["optimizer"]
+
+        def loss_fn():
+            return ren.training_loss(o, d, pw, target)[0]
+        return ren, [ren], opt, loss_fn
+    if name == "mip":
+        torch.manual_seed(0)
+        pos = IntegratedBarfFourierFeatures(10, 10, 1.28, 6.4, True, 1.0, True)
+        pos.pixel_width_sigma = 0.0
+        dirs = BarfPositionalEncoding(4, 4, 1.28, 6.4, True, 1.0)
+        model = NerfModel(4, 256, True, False, 2, pos, dirs, 5e-4, 1e-4, 200000)
+        ren = NerfInterpolation(2.0, 8.0, model, w["fine"], "stratified_uniform", -1.0, "middle", model,
+                                w["coarse"]).to(device)
+        o, d, pw, target, _ = synthetic_batch_lego(w["rays"], 1000 + rank, device, 800)
+        opt = ren.configure_optimizers()["optimizer"]
+
+        def loss_fn():
+            return ren.training_loss(o, d, pw, target)[0]
+        return ren, [ren], opt, loss_fn
+    if name == "barf":
+        torch.manual_seed(0)
+        pos = BarfPositionalEncoding(10, 10.0, 0, 1, True, 1.0)
+        dirs = BarfPositionalEncoding(4, 4.0, 0, 1, True, 1.0)
+        model = NerfModel(4, 256, True, False, 2, pos, dirs, 5e-4, 1e-5, 200000)
+        ren = NerfInterpolation(2.0, 8.0, model, w["fine"], "equidistant", -1.0, "middle").to(device)
+        extr = CameraExtrinsics(100, 1e-3, 1e-5, 200000).to(device)
+        with torch.no_grad():
+            extr.rotation.normal_(0, 0.02)
+            extr.translation.normal_(0, 0.02)
+        o, d, pw, target, img = synthetic_batch_lego(w["rays"], 1000 + rank, device, 400)
+        groups = [{"params": list(g["parameters"]), "lr": g["learning_rate_start"], "weight_decay": g["weight_decay"]}
+                  for g in ren.param_groups + extr.param_groups]
+        opt = FusedAdam(groups, eps=1e-5)
+
+        def loss_fn():
+            o2, d2, _, _ = extr(img, o, d)
+            return ren.training_loss(o2, d2, pw, target)[0]
+        return ren, [ren, extr], opt, loss_fn
+    raise ValueError(name)
 
 
 def flops_per_sample(ren) -> float:
@@ -128,6 +215,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="n2v", choices=tuple(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--matmul-precision", default="high", choices=("highest", "high", "medium"),
@@ -153,15 +241,14 @@ def main():
     from nerf_amd.ddp import GradAllReduce
     nerf_amd._lib.load()
 
-    ren = build_model(device)
-    opt = ren.configure_optimizers()["optimizer"]
-    allreduce = GradAllReduce(ren.parameters())
-    o, d, pw, target = synthetic_batch(RAYS, 1000 + rank, device)
+    wl = WORKLOADS[args.workload]
+    ren, modules, opt, loss_fn = build_workload(args.workload, device, rank)
+    allreduce = GradAllReduce([p for m in modules for p in m.parameters()])
     torch.manual_seed(1234 + rank)
 
     def step():
         opt.zero_grad(set_to_none=True)
-        loss, _ = ren.training_loss(o, d, pw, target)
+        loss = loss_fn()
         loss.backward()
         if dist is not None:
             allreduce()          # one RCCL all-reduce of the flat gradient bucket
@@ -191,7 +278,8 @@ def main():
         elapsed = float(t.item())
     final_loss = float(loss.item())
 
-    samples_total = RAYS * SAMPLES * world * args.steps
+    samples_per_gpu = wl["rays"] * (wl["coarse"] + wl["fine"])
+    samples_total = samples_per_gpu * world * args.steps
     value = samples_total / elapsed
     ks = timer.summary()
     from nerf_amd.mlp import matmul_precision
@@ -205,7 +293,7 @@ def main():
 
     traffic = None
     tfile = os.path.join(ROOT, "profiles", f"traffic_{nt_name}.json")
-    if os.path.exists(tfile):
+    if args.workload == "n2v" and os.path.exists(tfile):
         with open(tfile) as f:
             traffic = json.load(f).get("bytes_per_launch")
 
@@ -232,9 +320,9 @@ def main():
             "matmul": ("3xbf16 split MFMA (hi*hi+hi*lo+lo*hi, fp32 accumulate)" if x3 else "fp32 MFMA"),
             "matmul_precision": args.matmul_precision,
             "data": "synthetic Lego-shaped rays/targets, random-init weights (torch.manual_seed(0))",
-            "config": {"workload": "naive-to-vanilla NeRF training step, Lego 400x400, 4096 rays x 64 samples "
-                                   "per GPU (BASELINE.json configs[1])",
-                       "rays_per_gpu": RAYS, "samples_per_ray": SAMPLES, "global_rays": RAYS * world,
+            "config": {"workload": wl["config"], "workload_key": args.workload,
+                       "rays_per_gpu": wl["rays"], "samples_per_ray": wl["coarse"] + wl["fine"],
+                       "coarse_samples": wl["coarse"], "fine_samples": wl["fine"], "global_rays": wl["rays"] * world,
                        "parallelism": f"ray-batch dp{world}" + (" (RCCL all-reduce)" if world > 1 else "")},
             "roofline": {"kernel": (f"{nt_name} (" + ("3 x bf16 MFMA 32x32x16; peak = bf16 dense / 3"
                                                        if x3 else "fp32 MFMA 32x32x2")
@@ -253,10 +341,10 @@ def main():
                             "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["ms"] > 0 else 0.0,
                             "gbs": (v["bytes"] / (v["ms"] * 1e-3) / 1e9) if v["ms"] > 0 else 0.0}
                         for k, v in ks.items()},
-            "mlp_tflops_per_step": flops_per_sample(ren) * RAYS * SAMPLES / (elapsed / args.steps) / 1e12,
+            "mlp_tflops_per_step": flops_per_sample(ren) * samples_per_gpu / (elapsed / args.steps) / 1e12,
             "final_loss": final_loss,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.workload == "n2v":
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -144,11 +144,15 @@ class LayerPlan:
 
 
 class MLPPlan:
-    """Layers in execution order; ``outputs`` are layer indices exposed to autograd."""
+    """Layers in execution order; ``outputs`` are layer indices exposed to autograd;
+    ``column_outputs`` are (layer, column) pairs additionally exposed as contiguous [M] tensors
+    (NerfModel's density column inside the 257-wide last segment output: the compositor reads
+    and differentiates a 1 MB vector instead of the 268 MB layer output)."""
 
-    def __init__(self, layers: list[LayerPlan], outputs: list[int]):
+    def __init__(self, layers: list[LayerPlan], outputs: list[int], column_outputs: list[tuple[int, int]] = ()):
         self.layers = layers
         self.outputs = outputs
+        self.column_outputs = list(column_outputs)
         self.device = None
         self.consumed = [False] * len(layers)
         for lp in layers:
@@ -233,7 +237,8 @@ class MLPFunction(torch.autograd.Function):
         ctx.n_pos_cols = pos.shape[1]
         ctx.n_dir_cols = dirs.shape[1] if dirs is not None else 0
         ctx.save_for_backward(pos, dirs if dirs is not None else pos, *acts, *pre)
-        return tuple(acts[i] for i in plan.outputs)
+        cols = tuple(acts[li][:, c].contiguous() for li, c in plan.column_outputs)
+        return tuple(acts[i] for i in plan.outputs) + cols
 
     @staticmethod
     def backward(ctx, *grads):
@@ -249,7 +254,11 @@ class MLPFunction(torch.autograd.Function):
         dev = pos.device
         dY: list[torch.Tensor | None] = [None] * L
         owned = [True] * L       # False: dY[i] is autograd's incoming tensor (never written in place)
-        for idx, g in zip(plan.outputs, grads):
+        col_grads: list[list[tuple[int, torch.Tensor]]] = [[] for _ in range(L)]
+        for (li, c), g in zip(plan.column_outputs, grads[len(plan.outputs):]):
+            if g is not None:
+                col_grads[li].append((c, g))
+        for idx, g in zip(plan.outputs, grads[:len(plan.outputs)]):
             if g is None:
                 continue
             if g.shape != (M, plan.layers[idx].out_ld):
@@ -271,6 +280,14 @@ class MLPFunction(torch.autograd.Function):
 
         for li in range(L - 1, -1, -1):
             lp = plan.layers[li]
+            if col_grads[li]:
+                # gradients of the column outputs, added after every consumer's contribution
+                if dY[li] is None:
+                    dY[li] = torch.zeros(M, lp.out_ld, device=dev, dtype=torch.float32)
+                elif not owned[li]:
+                    dY[li] = dY[li].clone()
+                for c, g in col_grads[li]:
+                    dY[li][:, c] += g
             dZ = dY[li]
             w = lp.module.weight
             if dZ is None:
@@ -319,14 +336,14 @@ class MLPFunction(torch.autograd.Function):
                         else:
                             epi |= NERF_EPI_MASK
                             aux = acts[j]
-                    if dY[j] is None:
-                        if prod.out_ld > s.k_valid:
-                            dY[j] = torch.zeros(M, prod.out_ld, device=dev, dtype=torch.float32)
-                        else:
-                            dY[j] = torch.empty(M, prod.out_ld, device=dev, dtype=torch.float32)
+                    fresh = dY[j] is None
+                    if fresh:
+                        dY[j] = torch.empty(M, prod.out_ld, device=dev, dtype=torch.float32)
                     else:
                         epi |= NERF_EPI_ACCUM
                     lp.gemm(ctx.prec, a_seg, M, True, s.k_valid, None, dY[j], epi, aux=aux, row_offset=koff)
+                    if fresh and prod.out_ld > s.k_valid:
+                        dY[j][:, s.k_valid:].zero_()     # columns this consumer does not read
                 elif s.kind == "pos" and need_pos:
                     if dpos is None:
                         dpos = torch.empty(M, s.k_pad, device=dev, dtype=torch.float32)
@@ -394,4 +411,7 @@ def nerf_model_plan(n_segments: int, model_segments: nn.ModuleList, model_color:
     layers.append(LayerPlan(head1, [Source("act", head0.out_features, K.pad32(head0.out_features), len(layers) - 1)],
                             False))
     head_out = len(layers) - 1
-    return MLPPlan(layers, [z_last, head_out]), z_last, head_out
+    # without delayed density, sigma is column hidden_dim of the last segment output: exposed as
+    # its own [M] output so the compositor never touches (or differentiates) the 257-wide buffer
+    cols = [] if delayed_density else [(z_last, hidden_dim)]
+    return MLPPlan(layers, [z_last, head_out], cols), z_last, head_out

@@ -187,13 +187,14 @@ class RadianceNetwork(_GarfBase):
             layers[z2].residual, layers[z2].residual_cols = z1, 128
             head = _gauss_chain(self.model_color, [Source("act", 128, 128, z2), Source("dir", 3, K.pad32(3))],
                                 layers)
-            self._plan = MLPPlan(layers, [z2, head])
+            # sigma = softplus(z2[:, 128] - 1) reads one column: exposed as its own [M] output
+            self._plan = MLPPlan(layers, [z2, head], [(z2, 128)])
         return self._plan
 
     def forward(self, pos: th.Tensor, dir: th.Tensor) -> tuple[th.Tensor, th.Tensor]:
         plan = self._get_plan()
-        y2, head = MLPFunction.apply(plan, pos.shape[0], _pad4(pos), _pad4(dir), 1, *plan.params())
-        density = F.softplus(y2[:, 128] - 1, beta=1, threshold=8)
+        _, head, sigma_raw = MLPFunction.apply(plan, pos.shape[0], _pad4(pos), _pad4(dir), 1, *plan.params())
+        density = F.softplus(sigma_raw - 1, beta=1, threshold=8)
         rgb = th.sigmoid(head[:, :3])
         return rgb, density
 

@@ -118,22 +118,24 @@ class NerfModel(NerfBaseModel):
         return self._plan
 
     def _run_mlp(self, pos_pe: th.Tensor, dir_pe: th.Tensor, dir_row_div: int):
+        """(z_last, head, raw density [M] or None): without delayed density the density column
+        comes out of the MLP node as its own contiguous output."""
         plan = self._get_plan()
         M = pos_pe.shape[0]
-        z_last, head = MLPFunction.apply(plan, M, pos_pe, dir_pe, dir_row_div, *plan.params())
-        return z_last, head
+        outs = MLPFunction.apply(plan, M, pos_pe, dir_pe, dir_row_div, *plan.params())
+        return outs[0], outs[1], (outs[2] if len(outs) > 2 else None)
 
-    def _heads(self, z_last: th.Tensor, head: th.Tensor) -> RawHeads:
+    def _heads(self, z_last: th.Tensor, head: th.Tensor, dens: th.Tensor | None) -> RawHeads:
         if self.delayed_density:
             return RawHeads(head, head, 3)
-        return RawHeads(head, z_last, self.hidden_dim)
+        return RawHeads(head, dens.view(-1, 1), 0)
 
     def forward(self, pos: th.Tensor, dir: th.Tensor, pixel_width: th.Tensor, t_start: th.Tensor,
                 t_end: th.Tensor) -> tuple[th.Tensor, th.Tensor]:
         pos_pe = self.position_encoder.encode_padded(pos, dir, pixel_width, t_start, t_end)
         dir_pe = self.direction_encoder.encode_padded(dir)
-        z_last, head = self._run_mlp(pos_pe, dir_pe, 1)
-        density = head[:, 3] if self.delayed_density else z_last[:, self.hidden_dim]
+        z_last, head, dens = self._run_mlp(pos_pe, dir_pe, 1)
+        density = head[:, 3] if self.delayed_density else dens
         density = F.softplus(density, beta=1, threshold=8)
         rgb = th.sigmoid(head[:, :3])
         return density, rgb
@@ -147,5 +149,5 @@ class NerfModel(NerfBaseModel):
         pos_pe = self.position_encoder.encode_rays(ray_origs, ray_dirs, t_start, t_end, pixel_width,
                                                    samples_per_ray, query, pw_mode)
         dir_pe = self.direction_encoder.encode_padded(ray_dirs)
-        z_last, head = self._run_mlp(pos_pe, dir_pe, samples_per_ray)
-        return self._heads(z_last, head)
+        z_last, head, dens = self._run_mlp(pos_pe, dir_pe, samples_per_ray)
+        return self._heads(z_last, head, dens)
