@@ -353,10 +353,17 @@ __global__ __launch_bounds__(256) void encode_bwd_integrated_kernel(
 
 // Ray-mode backward (positions generated in-kernel from rays, nerf_encode_fwd with x == NULL):
 //   pos_s = o + tq_s * d  =>  dL/do = sum_s g_pos_s,  dL/dd = sum_s (tq_s * g_pos_s + g_dir_s)
-// where g_dir_s is the integrated encoding's own direction gradient (0 for Fourier/BARF).  One
-// wavefront per ray; lanes stride over the samples, fp64 accumulation, fixed-order wave sum.
+// where g_dir_s is the integrated encoding's own direction gradient (0 for Fourier/BARF).
 // This is the gradient the reference's pose refinement takes through _compute_positions
 // (barf/model_interpolation.py:288-312) into CameraExtrinsics (model_camera_extrinsics.py:77-85).
+//
+// One wavefront per ray, LANES OVER THE ENCODING'S COLUMNS: for every sample the wave reads the
+// gradient row as one coalesced 256-byte access, each lane evaluates the sin/cos of its own
+// column's argument and adds its column's share of g_pos (and, for the integrated encoding, of
+// the variance gradient) into per-lane fp64 accumulators; everything that follows is linear in
+// those shares, so the per-sample coefficients (tq, mu_diff, st, sr) are folded in per lane and
+// one fixed-order wave reduction per output component ends the ray.  Columns of an encoding
+// wider than 64 are strided over the lanes.
 __global__ __launch_bounds__(256) void encode_bwd_rays_kernel(EncArgs a, const float* __restrict__ g, int64_t g_ld,
                                                               float* __restrict__ d_o, float* __restrict__ d_d,
                                                               int accumulate) {
@@ -364,29 +371,89 @@ __global__ __launch_bounds__(256) void encode_bwd_rays_kernel(EncArgs a, const f
     const int lane = threadIdx.x & 63;
     const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (ray >= a.n_rays) return;
-    double ao[3] = {0.0, 0.0, 0.0}, ad[3] = {0.0, 0.0, 0.0};
-    for (int s = lane; s < a.S; s += 64) {
-        const int64_t n = ray * a.S + s;
-        float p[3], dv[3];
-        load_pos_dir(a, n, p, dv);
-        const float tq = (a.p.query == 0) ? a.t0[n] : (a.t0[n] + a.t1[n]) / 2.0f;
-        const float* gr = g + n * g_ld;
-        float gp[3], gd[3] = {0.f, 0.f, 0.f};
-        if (a.p.kind == 1) {
-            ipe_grad(a.p, p, dv, a.t0[n], a.t1[n], pixel_width_at(a, n), gr, gp, gd);
-        } else {
-#pragma unroll
-            for (int j = 0; j < 3; ++j) gp[j] = fourier_grad(a.p, p[j], j, gr);
-        }
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            ao[j] += (double)gp[j];
-            ad[j] += (double)(tq * gp[j]) + (double)gd[j];
-        }
-    }
+    const nerf_pe_params& p = a.p;
+    const int L = p.levels;
+    const int id = p.include_identity ? 3 : 0;
+    const int tl = 3 * L;
+    float dv[3], ov[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        const double so = wave_sum(ao[j]), sd = wave_sum(ad[j]);
+        dv[j] = a.d[ray * 3 + j];
+        ov[j] = a.o[ray * 3 + j];
+    }
+    // per lane: accumulated contributions to dL/do_dd, dL/dd_dd (own coordinate) and the
+    // cross term of the diagonal variance (multiplied by d_j for every j at the end); one set per
+    // column slot the lane owns (two slots cover out_dim <= 128)
+    double acc_o[2] = {0.0, 0.0}, acc_d[2] = {0.0, 0.0}, acc_x[2] = {0.0, 0.0};
+    int slot_d[2] = {-1, -1};
+    for (int s = 0; s < a.S; ++s) {
+        const int64_t n = ray * a.S + s;
+        const float t0 = a.t0[n];
+        const float t1 = (p.query != 0 || p.kind == 1) ? a.t1[n] : t0;
+        const float tq = (p.query == 0) ? t0 : (t0 + t1) / 2.0f;
+        float pos[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) pos[j] = ov[j] + tq * dv[j];
+        IpeSample q;
+        const float* pm = pos;
+        if (p.kind == 1) {
+            q = ipe_sample(p, pos, dv, t0, t1, pixel_width_at(a, n));
+            pm = q.pm;
+        }
+        const float* gr = g + n * g_ld;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int c = lane + 64 * u;
+            if (c >= a.out_dim) continue;
+            const float gv = gr[c];
+            int dd;
+            float cpos, cvb = 0.0f;       // this column's share of g_pos[dd] / g_vb[dd]
+            if (c < id) {
+                dd = c;
+                cpos = gv;
+            } else {
+                const int j = c - id;
+                const bool is_sin = j >= tl;
+                const int jj = is_sin ? j - tl : j;
+                dd = jj >= 2 * L ? 2 : (jj >= L ? 1 : 0);
+                const int k = jj - dd * L;
+                const float m = p.use_mask ? p.mask[k] : 1.0f;
+                const float sc = p.scale * (float)(1u << k);
+                float sn, cs;
+                sincos_enc(sel3(pm, dd) * sc, &sn, &cs);
+                const float gm = gv * m;
+                float w = 1.0f;
+                if (p.kind == 1) w = expf((-(sel3(q.vb, dd) * (float)(1u << (2 * k)))) / 2.0f);
+                cpos = (is_sin ? gm * cs : (-gm) * sn) * w * sc;
+                if (p.kind == 1) cvb = (is_sin ? gm * sn : gm * cs) * w * (-((float)(1u << (2 * k)) / 2.0f));
+            }
+            slot_d[u] = dd;
+            acc_o[u] += (double)cpos;
+            double dterm = (double)(tq * cpos);
+            if (p.kind == 1) {
+                dterm += (double)(cpos * q.mu_diff);
+                if (!p.distribute_variance) {
+                    const float S = q.ssum;
+                    dterm += (double)((2.0f * sel3(dv, dd)) * ((q.st - q.sr / S) * cvb));
+                    acc_x[u] += (double)((cvb * (sel3(dv, dd) * sel3(dv, dd))) * ((2.0f * q.sr) / (S * S)));
+                }
+            }
+            acc_d[u] += dterm;
+        }
+    }
+    double cross = wave_sum(acc_x[0] + acc_x[1]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        double so = 0.0, sd = 0.0;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (slot_d[u] == j) {
+                so += acc_o[u];
+                sd += acc_d[u];
+            }
+        }
+        so = wave_sum(so);
+        sd = wave_sum(sd) + cross * (double)dv[j];
         if (lane == 0) {
             if (d_o) d_o[ray * 3 + j] = accumulate ? d_o[ray * 3 + j] + (float)so : (float)so;
             if (d_d) d_d[ray * 3 + j] = accumulate ? d_d[ray * 3 + j] + (float)sd : (float)sd;
@@ -472,7 +539,7 @@ extern "C" int nerf_encode_bwd_rays(const nerf_pe_params* params, const float* r
     const nerf_pe_params& p = *params;
     NERF_REQUIRE(p.levels >= 0 && p.levels <= 16 && (p.kind == 0 || p.kind == 1));
     NERF_REQUIRE(ray_o && ray_d && t_start && grad_out && (d_origs || d_dirs));
-    NERF_REQUIRE(g_ld >= out_dim_of(p));
+    NERF_REQUIRE(g_ld >= out_dim_of(p) && out_dim_of(p) <= 128);
     if (p.query != 0 || p.kind == 1) NERF_REQUIRE(t_end != nullptr);
     if (p.kind == 1) NERF_REQUIRE(pixel_width != nullptr && p.pw_mode >= 0 && p.pw_mode <= 2);
     const int64_t n = n_rays * (int64_t)samples_per_ray;

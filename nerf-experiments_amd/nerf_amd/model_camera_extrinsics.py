@@ -33,16 +33,20 @@ class CameraExtrinsics(NerfBaseModel):
         return th.matrix_exp(th.cross(-th.eye(3, device=so3.device).view(1, 3, 3), so3.view(-1, 3, 1), dim=1))
 
     def get_rotations(self, img_idx: th.Tensor) -> th.Tensor:
-        return CameraExtrinsics.so3_to_SO3(self.rotation)[img_idx]
+        # index_select == [img_idx] for a 1-D index; its backward is an index_add (the advanced-
+        # indexing backward sorts the indices: three extra kernels per step)
+        return CameraExtrinsics.so3_to_SO3(self.rotation).index_select(0, img_idx.reshape(-1)).view(
+            *img_idx.shape, 3, 3)
 
     def forward_origins(self, i: th.Tensor, o: th.Tensor) -> tuple[th.Tensor, th.Tensor]:
-        t = self.translation[i] / MAGIC_NUMBER_THE_SECOND
+        t = self.translation.index_select(0, i.reshape(-1)).view(*i.shape, 3) / MAGIC_NUMBER_THE_SECOND
         return o + t, t
 
     def forward(self, i: th.Tensor, o: th.Tensor, d: th.Tensor):
         new_o, t = self.forward_origins(i, o)
         R = self.get_rotations(i)
-        new_d = th.matmul(R, d.unsqueeze(-1)).squeeze(-1)
+        # R @ d per ray as a 3-term elementwise sum (a batched 3x3 GEMM on hipBLASLt is ~4 kernels)
+        new_d = (R * d.unsqueeze(-2)).sum(-1)
         return new_o, new_d, R, t
 
 

@@ -18,8 +18,9 @@ Fixtures:
   cos_kat.npz    barf/cos_test_barf.pt (the reference's own fixture, loaded weights_only)
   ipe_grad.npz   integrated encodings: outputs and gradients w.r.t. position and direction
   garf.npz       GARF RadianceNetwork / ProposalNetwork / GaussAct: checksummed init, outputs, gradients
+  pose.npz       CameraExtrinsics (BARF pose refinement): refined rays, rotations, parameter gradients
 
-    python tests/golden/make_golden.py [pe composite resample model color cos_kat ipe_grad garf]
+    python tests/golden/make_golden.py [pe composite resample model color cos_kat ipe_grad garf pose]
 """
 from __future__ import annotations
 
@@ -355,8 +356,30 @@ def gen_garf():
     np.savez_compressed(os.path.join(OUT, "garf.npz"), **out)
 
 
+def gen_pose():
+    """CameraExtrinsics (barf/model_camera_extrinsics.py:7-85): so3 -> SO3 and the refined rays,
+    with gradients w.r.t. rotation / translation."""
+    (ce,) = _import_from("barf", ["model_camera_extrinsics"])
+    g = th.Generator().manual_seed(8)
+    m = ce.CameraExtrinsics(10, 1e-3, 1e-5, 100)
+    with th.no_grad():
+        m.rotation.copy_(th.randn(10, 3, generator=g) * 0.3)
+        m.translation.copy_(th.randn(10, 3, generator=g) * 0.1)
+    B = 200
+    idx = th.randint(0, 10, (B,), generator=g)
+    o = th.randn(B, 3, generator=g)
+    d = th.randn(B, 3, generator=g)
+    new_o, new_d, R, t = m.forward(idx, o, d)
+    go, gd = th.randn(B, 3, generator=g), th.randn(B, 3, generator=g)
+    ((new_o * go).sum() + (new_d * gd).sum()).backward()
+    np.savez_compressed(os.path.join(OUT, "pose.npz"), rotation=f32(m.rotation), translation=f32(m.translation),
+                        idx=idx.numpy().astype(np.int64), o=f32(o), d=f32(d), new_o=f32(new_o), new_d=f32(new_d),
+                        R=f32(R), go=f32(go), gd=f32(gd), drot=f32(m.rotation.grad), dtrans=f32(m.translation.grad))
+
+
 GENERATORS = {"pe": gen_pe, "composite": gen_composite, "resample": gen_resample, "model": gen_model,
-              "color": gen_color, "cos_kat": gen_cos_kat, "ipe_grad": gen_ipe_grad, "garf": gen_garf}
+              "color": gen_color, "cos_kat": gen_cos_kat, "ipe_grad": gen_ipe_grad, "garf": gen_garf,
+              "pose": gen_pose}
 
 
 if __name__ == "__main__":
