@@ -76,11 +76,12 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf
 
 // ---------------------------------------------------------------------------
 // sin and cos of one fp32 argument for the encodings (|x| up to scale * 2^15 * |p|):
-// k = rint(x * 2/pi); r = x - k * pi/2 reduced in fp64 with a two-term pi/2 (error < 2^-40
-// for |x| < 2^30), then fp32 minimax polynomials on [-pi/4, pi/4] (Cephes sinf/cosf,
-// ~1 ulp) and the quadrant swap.  About a third of the instructions of the libm sincosf,
-// within ~1e-7 absolute of the correctly rounded values; larger or non-finite arguments
-// take sincosf.
+// k = rint(x * 2/pi); r = x - k * pi/2 by a three-term fp32 Cody-Waite reduction with fused
+// multiply-adds (each k * c_i exact inside its FMA: |r| error ~1e-7 for |k| < 2^24), then fp32
+// minimax polynomials on [-pi/4, pi/4] (Cephes sinf/cosf, ~1 ulp) and the quadrant swap.  About
+// a third of the instructions of the libm sincosf, within ~1e-7 absolute of the correctly
+// rounded values; larger or non-finite arguments take sincosf.  (-DNERF_SINCOS_FP64_REDUCTION:
+// the same with a two-term fp64 reduction, measured 2 % slower in the encoding kernel.)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void sincos_enc(float x, float* s, float* c) {
     if (!(fabsf(x) < 1073741824.0f)) {
@@ -88,9 +89,16 @@ __device__ __forceinline__ void sincos_enc(float x, float* s, float* c) {
         return;
     }
     const float kf = rintf(x * 0.636619772367581343f);
+#ifndef NERF_SINCOS_FP64_REDUCTION
+    // three-term fp32 Cody-Waite with fused multiply-adds (each product exact inside the FMA)
+    float r = __builtin_fmaf(kf, -1.57079637050628662109375f, x);
+    r = __builtin_fmaf(kf, 4.3711388286737929e-08f, r);
+    r = __builtin_fmaf(kf, 1.7763568394002505e-15f, r);
+#else
     double rd = __builtin_fma((double)kf, -1.5707963267948966, (double)x);
     rd = __builtin_fma((double)kf, -6.123233995736766e-17, rd);
     const float r = (float)rd;
+#endif
     const float r2 = r * r;
     float sp = __builtin_fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f);
     sp = __builtin_fmaf(r2, sp, -1.6666654611e-1f);

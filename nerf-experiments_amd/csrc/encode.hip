@@ -178,7 +178,10 @@ __global__ __launch_bounds__(256) void encode_fwd_kernel(EncArgs a, int Q, int R
 //   1. one thread per (sample, d, k): ONE sincos per argument, writing both the cos and the sin
 //      column (half the transcendental work of a per-column mapping);
 //   2. the 64-row image leaves LDS as coalesced 16-byte stores (ld/4 consecutive lanes per row).
-constexpr int kEncRows = 64;
+#ifndef NERF_ENC_ROWS
+#define NERF_ENC_ROWS 64
+#endif
+constexpr int kEncRows = NERF_ENC_ROWS;
 constexpr int kEncMaxLd = 128;
 
 __global__ __launch_bounds__(256) void encode_fwd_lds_kernel(EncArgs a) {
@@ -213,35 +216,41 @@ __global__ __launch_bounds__(256) void encode_fwd_lds_kernel(EncArgs a) {
         for (int c = a.out_dim; c < ld; ++c) row[c] = 0.0f;
     }
     __syncthreads();
+    // phase 1: thread t owns argument column j = t % TPR (fixed d, k, scale, mask for the whole
+    // block) and walks the rows r = t / TPR, + 256/TPR, ...: no per-task index arithmetic
     const int tl = 3 * L;
-    const int tasks = rows * tl;
-    for (int i = t; i < tasks; i += 256) {
-        const int r = i / tl;
-        const int j = i - r * tl;
+    const int TPR = tl <= 32 ? 32 : 64;
+    const int j = t & (TPR - 1);
+    if (j < tl) {
         const int dd = j >= 2 * L ? 2 : (j >= L ? 1 : 0);
         const int k = j - dd * L;
         const float s = a.p.scale * (float)(1u << k);
-        float sn, cs;
-        sincos_enc(spm[r][dd] * s, &sn, &cs);
-        if (a.p.kind == 1) {
-            const float sc4 = (float)(1u << (2 * k));
-            const float w = expf((-(svb[r][dd] * sc4)) / 2.0f);
-            cs = cs * w;
-            sn = sn * w;
+        const float m = a.p.use_mask ? a.p.mask[k] : 1.0f;
+        const float sc4 = (float)(1u << (2 * k));
+        for (int r = t / TPR; r < rows; r += 256 / TPR) {
+            float sn, cs;
+            sincos_enc(spm[r][dd] * s, &sn, &cs);
+            if (a.p.kind == 1) {
+                const float w = expf((-(svb[r][dd] * sc4)) / 2.0f);
+                cs = cs * w;
+                sn = sn * w;
+            }
+            if (a.p.use_mask) {
+                cs = m * cs;
+                sn = m * sn;
+            }
+            float* row = img + r * lds_ld;
+            row[id + j] = cs;
+            row[id + tl + j] = sn;
         }
-        if (a.p.use_mask) {
-            cs = a.p.mask[k] * cs;
-            sn = a.p.mask[k] * sn;
-        }
-        float* row = img + r * lds_ld;
-        row[id + j] = cs;
-        row[id + tl + j] = sn;
     }
     __syncthreads();
     const int Q = ld >> 2;
     const int stores = rows * Q;
+    const bool pow2 = (Q & (Q - 1)) == 0;
+    const int qsh = __builtin_ctz((unsigned)Q);
     for (int i = t; i < stores; i += 256) {
-        const int r = i / Q;
+        const int r = pow2 ? i >> qsh : i / Q;
         const int qd = i - r * Q;
         const float4 v = *reinterpret_cast<const float4*>(img + r * lds_ld + 4 * qd);
         *reinterpret_cast<float4*>(a.out + (n0 + r) * a.ld + 4 * qd) = v;

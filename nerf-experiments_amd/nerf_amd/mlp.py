@@ -117,8 +117,9 @@ class LayerPlan:
     def pack(self, precision: str = "fp32"):
         w = self.module.weight
         ver = (w._version, w.data_ptr())
-        # in split precision every GEMM runs on the split-precision kernels: no fp32 packs
-        need_fp32 = precision != "x3"
+        # in split precision the fp32 packs only serve GEMMs with <= 32 output columns: this
+        # layer's forward (N <= 32) and the input gradients of sources <= 32 columns wide
+        need_fp32 = precision != "x3" or self.N <= 32 or any(s.k_pad <= 32 for s in self.sources)
         if need_fp32 and ver != self.packed_version:
             K.pack_weight(w.detach().contiguous(), self.col_map, self.Kp, self.Wp, self.Wt, self.ldwt)
             self.packed_version = ver
@@ -132,10 +133,10 @@ class LayerPlan:
 
     def gemm(self, precision: str, segs, M: int, transpose: bool, N: int, bias, out, epi, aux=None,
              row_offset: int = 0):
-        """Forward (W) or input-gradient (W^T) GEMM in the requested precision.  Narrow outputs
-        (the 4-wide head, 32-wide encoding gradients) also take the split-precision LDS-DMA kernel
-        in x3 mode: HBM-bound either way, it reads A at a higher rate than the fp32 128 x 32 tile."""
-        if precision == "x3":
+        """Forward (W) or input-gradient (W^T) GEMM in the requested precision; outputs of at
+        most 32 columns always use the fp32 kernel's 128 x 32 tile (measured: the 4-wide head at
+        M = 262144 takes 42 us there against 55 us on the split-precision 256 x 128 tile)."""
+        if precision == "x3" and N > 32:
             K.linear_fwd_x3(segs, M, self.Wtx if transpose else self.Wpx, self.ldwt if transpose else self.Kp, N, bias,
                             out, epi, aux=aux, w_row_offset=row_offset)
         else:

@@ -139,7 +139,9 @@ def main():
               "nt256x3": lambda: bench_linear(M, 256, (256,), (1,), x3=True),
               "nt256maskx3": lambda: bench_linear(M, 256, (256,), (1,), NERF_EPI_MASK, x3=True),
               "nt256bitsx3": lambda: bench_linear(M, 256, (256,), (1,), NERF_EPI_MASK | NERF_EPI_MASKBITS, x3=True),
-              "wgrad256x3": lambda: bench_wgrad(M, 256, (256,), (1,), x3=True)}[args.only]
+              "wgrad256x3": lambda: bench_wgrad(M, 256, (256,), (1,), x3=True),
+              "encode": lambda: bench_encode(4096, 64),
+              "encode_big": lambda: bench_encode(65536, 128)}[args.only]
         print(json.dumps(fn()))
         return
     for x3 in (False, True):
