@@ -273,6 +273,54 @@ int nerf_pack_weight_x3(const float* W, int32_t N, int32_t K_orig, const int32_t
                         int32_t Kp, void* Wp_x, void* Wt_x, int32_t ldwt, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Fused field-MLP forward (a7: NerfModel.forward, barf/model_interpolation_architecture.py:96-141,
+ * every Linear + bias + ReLU of the network in ONE launch, split precision as above).
+ *
+ * Each wave owns 32 samples and keeps their activations in registers from layer to layer
+ * (as the B operand of v_mfma_f32_32x32x16_bf16, bf16 hi/lo): only the HBM-fed inputs
+ * (position / direction encodings) are read and only the outputs the backward needs are
+ * written.  Weights stream through LDS by LDS-DMA in "chunks" (32 output rows of one layer:
+ * its 32-deep k-blocks as ready-to-use MFMA fragments, 4 KB each), all packed into one image by
+ * nerf_fused_pack together with the biases ([nb][32] fp32 per layer at bias_off).  Layer l's
+ * input is [previous layer's output (kbr 32-wide blocks, none for the first layer) | up to 2 HBM
+ * segments (kbh blocks in all)]; type = 3*(kbr/4) + kbh with kbr in {0, 4, 8}, kbh in {0, 1, 2}.  out[m, n] for n < ldo
+ * (columns >= N are written as 0), ReLU mask bits as NERF_EPI_MASKOUT (N <= 256), column
+ * col_idx (a multiple of 32) additionally into col_out[m].  Buffers: byte extents < 2^31.
+ * ------------------------------------------------------------------------- */
+#define NERF_FUSED_MAX_LAYERS 16
+typedef struct nerf_fused_layer {
+    int32_t type;          /* 3*(kbr/4) + kbh */
+    int32_t N;             /* output columns */
+    int32_t nb;            /* ceil(N / 32), <= 9 (blocks >= 8 are written, never fed forward) */
+    int32_t relu;
+    int32_t nseg;          /* HBM segments, 0..2 */
+    int32_t seg_kb[2];     /* 32-column blocks of each segment (sum = kbh) */
+    int32_t seg_k[2];      /* valid columns of each segment (multiple of 4; the rest reads 0) */
+    int32_t seg_rd[2];     /* row divisor (row m reads row m / rd) */
+    int32_t seg_rows[2];   /* rows of each segment buffer */
+    int32_t chunk_units;   /* 1 KB units per chunk = 4*(kbr + kbh) */
+    int32_t col_idx;       /* -1 or the column copied to col_out */
+    int64_t seg_ld[2];
+    const float* seg_ptr[2];
+    float* out;            /* [M][ldo] fp32 */
+    int64_t ldo;
+    uint8_t* mask;         /* [M][32] ReLU bits or NULL */
+    float* col_out;        /* [M] or NULL */
+    int64_t img_off;       /* byte offset of the layer's first chunk in the image */
+    int64_t bias_off;      /* byte offset of the layer's [nb][32] fp32 biases in the image */
+} nerf_fused_layer;
+
+int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_layers, const void* image, int64_t M,
+                       void* stream);
+
+/* Gather + split packer for the fused image: for i < n, v = srcs[map_src[i] >> 24][map_src[i] & 0xffffff]
+ * (0 if map_src[i] < 0); map_dst[i] >= 0: bf16 element index of hi = bf16(v) (lo = bf16(v - hi)
+ * at +512 elements); map_dst[i] < 0: fp32 word ~map_dst[i] = v.  Up to 64 sources. */
+#define NERF_FUSED_MAX_SRCS 64
+int nerf_fused_pack(const float* const* srcs, int32_t n_srcs, const int32_t* map_src, const int32_t* map_dst,
+                    int64_t n, void* image, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Gaussian activation with a learnable per-channel inverse standard deviation (a8, GARF
  * field MLPs): GaussActivation / GaussAct, garf/gaussian.py:8-63 (copy: barf/gaussian.py).
  * v_n = inv_std_n^2 + 1e-6;  y[m,n] = exp((-(z*z)) * v_n)  over z [M][N] (row stride ld_z).

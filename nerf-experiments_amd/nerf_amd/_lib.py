@@ -75,6 +75,34 @@ class NerfAdamBatch(ctypes.Structure):
     ]
 
 
+NERF_FUSED_MAX_LAYERS = 16
+NERF_FUSED_MAX_SRCS = 64
+
+
+class NerfFusedLayer(ctypes.Structure):
+    _fields_ = [
+        ("type", c_i32),
+        ("N", c_i32),
+        ("nb", c_i32),
+        ("relu", c_i32),
+        ("nseg", c_i32),
+        ("seg_kb", c_i32 * 2),
+        ("seg_k", c_i32 * 2),
+        ("seg_rd", c_i32 * 2),
+        ("seg_rows", c_i32 * 2),
+        ("chunk_units", c_i32),
+        ("col_idx", c_i32),
+        ("seg_ld", c_i64 * 2),
+        ("seg_ptr", c_vp * 2),
+        ("out", c_vp),
+        ("ldo", c_i64),
+        ("mask", c_vp),
+        ("col_out", c_vp),
+        ("img_off", c_i64),
+        ("bias_off", c_i64),
+    ]
+
+
 # name -> (restype, argtypes)
 _SIGNATURES = {
     "nerf_abi_version": (c_i32, []),
@@ -109,6 +137,8 @@ _SIGNATURES = {
                                    c_i64, c_i32, c_vp, c_i64, c_vp]),
     "nerf_linear_wgrad_x3": (c_i32, [c_vp, c_i64, c_i32, ctypes.POINTER(NerfSeg), c_i32, c_i64, c_vp, c_sz, c_vp]),
     "nerf_pack_weight_x3": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
+    "nerf_mlp_fused_fwd": (c_i32, [ctypes.POINTER(NerfFusedLayer), c_i32, c_vp, c_i64, c_vp]),
+    "nerf_fused_pack": (c_i32, [ctypes.POINTER(c_vp), c_i32, c_vp, c_vp, c_i64, c_vp, c_vp]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES.keys())

@@ -24,6 +24,7 @@ import torch
 import torch.nn as nn
 
 from . import kernels as K
+from . import mlp_fused
 from ._lib import (NERF_EPI_ACCUM, NERF_EPI_BIAS, NERF_EPI_MASK, NERF_EPI_MASKBITS, NERF_EPI_MASKOUT,
                    NERF_EPI_RELU)
 
@@ -41,6 +42,9 @@ def matmul_precision() -> str:
 
 
 PRECISION_OVERRIDE: str | None = None
+
+# test hook: when a list, every MLPFunction.forward appends (layer outputs, ReLU mask bits)
+CAPTURE: list | None = None
 
 
 @dataclass
@@ -155,6 +159,7 @@ class MLPPlan:
         self.outputs = outputs
         self.column_outputs = list(column_outputs)
         self.device = None
+        self.fused = {}            # device -> mlp_fused.FusedForward
         self.consumed = [False] * len(layers)
         for lp in layers:
             for s in lp.sources:
@@ -198,37 +203,54 @@ class MLPFunction(torch.autograd.Function):
         acts: list[torch.Tensor] = []
         masks: list[torch.Tensor | None] = []
         pre: list[torch.Tensor] = []
-        for idx, lp in enumerate(plan.layers):
-            lp.pack(prec)
-            segs = []
-            for s in lp.sources:
-                t, rd = _src_tensor(s, pos, dirs, acts, dir_rd)
-                segs.append((t, s.k_seg, rd))
-            out = torch.empty(M, lp.out_ld, device=pos.device, dtype=torch.float32)
-            # Gaussian layers: the GEMM writes the pre-activation z (kept for the backward),
-            # nerf_gauss_act_fwd then writes exp(-z^2 v) into the layer's output
-            target = torch.empty_like(out) if lp.gauss is not None else out
-            epi = NERF_EPI_BIAS | (NERF_EPI_RELU if lp.relu else 0)
-            mask = None
-            if lp.relu and plan.consumed[idx] and lp.N <= 256:
-                # the ReLU-backward mask of this output as bits (32 bytes a row): the input-
-                # gradient GEMMs read it instead of the fp32 activation
-                mask = torch.empty(M, 32, device=pos.device, dtype=torch.uint8)
-                epi |= NERF_EPI_MASKOUT
-            if lp.residual >= 0:
-                # out = residual + (x W^T + b): the accumulate epilogue adds onto the copied residual
-                rc = lp.residual_cols
-                target[:, rc:].zero_()
-                target[:, :rc].copy_(acts[lp.residual][:, :rc])
-                epi |= NERF_EPI_ACCUM
-            lp.gemm(prec, segs, M, False, lp.N, lp.module.bias, target, epi, aux=mask)
-            if lp.gauss is not None:
-                K.gauss_act_fwd(target, lp.N, lp.gauss, out)
-                if lp.out_ld > lp.N:
-                    out[:, lp.N:].zero_()
-                pre.append(target)
-            acts.append(out)
-            masks.append(mask)
+        cols = None
+        if prec == "x3" and mlp_fused.eligible(plan, M):
+            # the whole network in one launch (csrc/mlp_fused.hip); same outputs as the loop below
+            fused = plan.fused.get(pos.device)
+            if fused is None:
+                fused = plan.fused[pos.device] = mlp_fused.FusedForward(plan, pos.device)
+            for idx, lp in enumerate(plan.layers):
+                lp.pack(prec)                 # the input-gradient GEMMs of the backward use Wtx
+                acts.append(torch.empty(M, lp.out_ld, device=pos.device, dtype=torch.float32))
+                masks.append(torch.empty(M, 32, device=pos.device, dtype=torch.uint8)
+                             if lp.relu and plan.consumed[idx] and lp.N <= 256 else None)
+            col_t = {li: torch.empty(M, device=pos.device, dtype=torch.float32) for li, _ in plan.column_outputs}
+            fused.run(M, pos, dirs, dir_rd, acts, masks, col_t)
+            cols = tuple(col_t[li] for li, _ in plan.column_outputs)
+        else:
+            for idx, lp in enumerate(plan.layers):
+                lp.pack(prec)
+                segs = []
+                for s in lp.sources:
+                    t, rd = _src_tensor(s, pos, dirs, acts, dir_rd)
+                    segs.append((t, s.k_seg, rd))
+                out = torch.empty(M, lp.out_ld, device=pos.device, dtype=torch.float32)
+                # Gaussian layers: the GEMM writes the pre-activation z (kept for the backward),
+                # nerf_gauss_act_fwd then writes exp(-z^2 v) into the layer's output
+                target = torch.empty_like(out) if lp.gauss is not None else out
+                epi = NERF_EPI_BIAS | (NERF_EPI_RELU if lp.relu else 0)
+                mask = None
+                if lp.relu and plan.consumed[idx] and lp.N <= 256:
+                    # the ReLU-backward mask of this output as bits (32 bytes a row): the input-
+                    # gradient GEMMs read it instead of the fp32 activation
+                    mask = torch.empty(M, 32, device=pos.device, dtype=torch.uint8)
+                    epi |= NERF_EPI_MASKOUT
+                if lp.residual >= 0:
+                    # out = residual + (x W^T + b): the accumulate epilogue adds onto the copied residual
+                    rc = lp.residual_cols
+                    target[:, rc:].zero_()
+                    target[:, :rc].copy_(acts[lp.residual][:, :rc])
+                    epi |= NERF_EPI_ACCUM
+                lp.gemm(prec, segs, M, False, lp.N, lp.module.bias, target, epi, aux=mask)
+                if lp.gauss is not None:
+                    K.gauss_act_fwd(target, lp.N, lp.gauss, out)
+                    if lp.out_ld > lp.N:
+                        out[:, lp.N:].zero_()
+                    pre.append(target)
+                acts.append(out)
+                masks.append(mask)
+        if CAPTURE is not None:
+            CAPTURE.append((list(acts), list(masks)))
         ctx.masks = masks
         ctx.prec = prec
         ctx.plan = plan
@@ -238,7 +260,8 @@ class MLPFunction(torch.autograd.Function):
         ctx.n_pos_cols = pos.shape[1]
         ctx.n_dir_cols = dirs.shape[1] if dirs is not None else 0
         ctx.save_for_backward(pos, dirs if dirs is not None else pos, *acts, *pre)
-        cols = tuple(acts[li][:, c].contiguous() for li, c in plan.column_outputs)
+        if cols is None:
+            cols = tuple(acts[li][:, c].contiguous() for li, c in plan.column_outputs)
         return tuple(acts[i] for i in plan.outputs) + cols
 
     @staticmethod

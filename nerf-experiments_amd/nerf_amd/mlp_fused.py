@@ -1,0 +1,201 @@
+"""Lowering of a field-MLP plan onto the fused forward kernel (csrc/mlp_fused.hip).
+
+``nerf_mlp_fused_fwd`` runs every Linear (+ bias + ReLU) of a NerfModel
+(barf/model_interpolation_architecture.py:96-141) in one launch, keeping each wave's
+activations in registers between layers.  This module decides whether a plan fits the
+kernel, builds the packed weight image (MFMA-fragment order, split hi/lo bf16, biases) and
+the per-layer descriptors, and launches it.  Outputs are exactly those of the layer-by-layer
+forward in mlp.py (every layer's output, the ReLU mask bits, the density column), so the
+backward is unchanged.
+
+Fragment order (mirrors the kernel header): chunk (layer, nb) holds output rows 32 nb .. +31;
+for every 32-deep k-block kb and 16-row half bb, lane l (s = l & 15, g = l >> 4) element j is
+W[32 nb + 16 bb + s][k(kb, g, j)] with
+  k = 32 kb + 16 (j >> 2) + 4 g + (j & 3)          register-fed input (previous layer output)
+  k = seg_offset + 32 kh + 8 g + j                  HBM-fed segment block kh (encodings)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import kernels as K
+
+FUSED_TYPES = {(0, 1): 1, (0, 2): 2, (4, 0): 3, (8, 0): 6, (8, 1): 7, (8, 2): 8}   # (kbr, kbh) -> type
+ENABLED = os.environ.get("NERF_FUSED", "1") != "0"     # A/B switch (bench, tests)
+
+
+def _layer_shape(plan, idx):
+    """(kbr, hbm sources, act source) of layer idx, or None if the kernel cannot run it."""
+    lp = plan.layers[idx]
+    if lp.gauss is not None or lp.residual >= 0:
+        return None
+    acts = [s for s in lp.sources if s.kind == "act"]
+    hbm = [s for s in lp.sources if s.kind != "act"]
+    if idx == 0:
+        if acts:
+            return None
+        kbr = 0
+    else:
+        if len(acts) != 1 or lp.sources[0] is not acts[0] or acts[0].layer != idx - 1:
+            return None
+        if acts[0].k_valid not in (128, 256):
+            return None
+        kbr = acts[0].k_valid // 32
+    if len(hbm) > 2 or any(s.kind not in ("pos", "dir") for s in hbm):
+        return None
+    kbh = sum(s.k_pad // 32 for s in hbm)
+    if (kbr, kbh) not in FUSED_TYPES:
+        return None
+    return kbr, hbm
+
+
+def eligible(plan, M: int) -> bool:
+    if not ENABLED or len(plan.layers) > _lib.NERF_FUSED_MAX_LAYERS or M >= (1 << 30):
+        return False
+    if len(plan.layers) * 2 > _lib.NERF_FUSED_MAX_SRCS:
+        return False
+    cols = {}
+    for li, c in plan.column_outputs:
+        if c % 32 or li in cols:
+            return False
+        cols[li] = c
+    for idx, lp in enumerate(plan.layers):
+        if _layer_shape(plan, idx) is None:
+            return False
+        N = lp.module.out_features
+        if (N + 31) // 32 > 9 or M * lp.out_ld * 4 >= (1 << 31):
+            return False
+        if idx + 1 < len(plan.layers) and plan.layers[idx + 1].sources[0].kind == "act" and N > 288:
+            return False
+    return True
+
+
+class FusedForward:
+    """Packed image + static descriptors of one plan on one device."""
+
+    def __init__(self, plan, device):
+        self.plan = plan
+        self.device = device
+        self.layers = []          # (kbr, kbh, hbm sources, nb, units, img_off, bias_off)
+        shapes = []
+        off = 0
+        for idx, lp in enumerate(plan.layers):
+            kbr, hbm = _layer_shape(plan, idx)
+            kbh = sum(s.k_pad // 32 for s in hbm)
+            nb = (lp.module.out_features + 31) // 32
+            units = 4 * (kbr + kbh)
+            shapes.append((kbr, kbh, hbm, nb, units, off))
+            off += nb * units * 1024
+        src_codes, dst_codes = [], []
+        for idx, lp in enumerate(plan.layers):
+            kbr, kbh, hbm, nb, units, img_off = shapes[idx]
+            self.layers.append((kbr, kbh, hbm, nb, units, img_off, off))
+            s, d = self._maps(idx, lp, kbr, hbm, nb, units, img_off, off)
+            src_codes.append(s)
+            dst_codes.append(d)
+            off += nb * 128
+        self.image_bytes = off
+        self.image = torch.zeros(off // 2, dtype=torch.bfloat16, device=device)
+        self.map_src = torch.from_numpy(np.concatenate(src_codes).astype(np.int32)).to(device)
+        self.map_dst = torch.from_numpy(np.concatenate(dst_codes).astype(np.int32)).to(device)
+        self.version = None
+
+    @staticmethod
+    def _maps(idx, lp, kbr, hbm, nb, units, off, bias_off):
+        """Gather map of one layer: source codes (tensor << 24 | element, -1 = 0) and
+        destinations (bf16 index of hi, or ~fp32 word for raw bias words)."""
+        N, K_orig = lp.module.out_features, lp.module.in_features
+        tw, tb = 2 * idx, 2 * idx + 1
+        # original weight column offsets of the sources (plan order, k_valid wide)
+        orig = {}
+        o = 0
+        for s in lp.sources:
+            orig[id(s)] = o
+            o += s.k_valid
+        lane = np.arange(64)
+        srow, grp = lane & 15, lane >> 4
+        j = np.arange(8)
+        kb_total = kbr + sum(s.k_pad // 32 for s in hbm)
+        col = np.full((kb_total, 64, 8), -1, dtype=np.int64)       # weight column per (kb, lane, j)
+        for kb in range(kbr):
+            col[kb] = 32 * kb + 16 * (j[None, :] >> 2) + 4 * grp[:, None] + (j[None, :] & 3)
+        kb = kbr
+        for s in hbm:
+            for kh in range(s.k_pad // 32):
+                local = 32 * kh + 8 * grp[:, None] + j[None, :]
+                col[kb] = np.where(local < s.k_valid, orig[id(s)] + local, -1)
+                kb += 1
+        srcs, dsts = [], []
+        for c in range(nb):
+            base = off + c * units * 1024
+            for bb in range(2):
+                n = 32 * c + 16 * bb + srow                          # [64]
+                nn = np.broadcast_to(n[None, :, None], col.shape)
+                valid = (col >= 0) & (nn < N)
+                code = np.where(valid, (tw << 24) + nn * K_orig + col, -1)
+                dst = (base + np.arange(kb_total)[:, None, None] * 4096 + bb * 2048) // 2 + \
+                    lane[None, :, None] * 8 + j[None, None, :]
+                srcs.append(code.reshape(-1))
+                dsts.append(np.broadcast_to(dst, col.shape).reshape(-1))
+            nbias = 32 * c + np.arange(32)
+            srcs.append(np.where(nbias < N, (tb << 24) + nbias, -1))
+            dsts.append(~(bias_off // 4 + nbias))
+        return np.concatenate(srcs), np.concatenate(dsts)
+
+    def pack(self):
+        ps = []
+        for lp in self.plan.layers:
+            ps += [lp.module.weight, lp.module.bias]
+        ver = tuple((p._version, p.data_ptr()) for p in ps)
+        if ver == self.version:
+            return
+        arr = (ctypes.c_void_p * len(ps))(*[p.data_ptr() for p in ps])
+        st = _lib.load().nerf_fused_pack(arr, len(ps), self.map_src.data_ptr(), self.map_dst.data_ptr(),
+                                         self.map_src.numel(), self.image.data_ptr(), K._stream(self.device))
+        _lib.check(st, "nerf_fused_pack")
+        self.version = ver
+
+    def run(self, M: int, pos: torch.Tensor, dirs: torch.Tensor | None, dir_rd: int, acts, masks, col_outs):
+        """Launch on the current stream.  acts[l]: [M, out_ld] fp32, masks[l]: [M, 32] uint8 or
+        None, col_outs: {layer: [M] fp32}."""
+        self.pack()
+        L = len(self.plan.layers)
+        descs = (_lib.NerfFusedLayer * L)()
+        flops = 0.0
+        for idx, lp in enumerate(self.plan.layers):
+            kbr, kbh, hbm, nb, units, off, bias_off = self.layers[idx]
+            d = descs[idx]
+            d.type = FUSED_TYPES[(kbr, kbh)]
+            d.N = lp.module.out_features
+            d.nb = nb
+            d.relu = 1 if lp.relu else 0
+            d.nseg = len(hbm)
+            for si, s in enumerate(hbm):
+                t = pos if s.kind == "pos" else dirs
+                d.seg_kb[si] = s.k_pad // 32
+                d.seg_k[si] = s.k_seg
+                d.seg_rd[si] = 1 if s.kind == "pos" else dir_rd
+                d.seg_rows[si] = t.shape[0]
+                d.seg_ld[si] = t.stride(0)
+                d.seg_ptr[si] = t.data_ptr()
+            d.chunk_units = units
+            d.col_idx = -1
+            d.out = acts[idx].data_ptr()
+            d.ldo = acts[idx].stride(0)
+            d.mask = masks[idx].data_ptr() if masks[idx] is not None else None
+            if idx in col_outs:
+                d.col_out = col_outs[idx].data_ptr()
+                d.col_idx = dict(self.plan.column_outputs)[idx]
+            d.img_off = off
+            d.bias_off = bias_off
+            flops += 2.0 * M * lp.module.out_features * lp.module.in_features
+        end = K.TIMER.bracket("mlp_fused_fwd", flops) if K.TIMER is not None else None
+        st = _lib.load().nerf_mlp_fused_fwd(descs, L, self.image.data_ptr(), M, K._stream(self.device))
+        if end is not None:
+            end.record()
+        _lib.check(st, "nerf_mlp_fused_fwd")

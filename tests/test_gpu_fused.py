@@ -1,0 +1,134 @@
+"""Fused field-MLP forward (csrc/mlp_fused.hip, one launch for the whole NerfModel) against
+the layer-by-layer split-precision path it replaces (mlp.py, pinned to the reference's golden
+vectors by test_gpu_parity.py) on the same inputs, and against the CPU oracle on a subset.
+
+Every layer output (these are the backward's saved activations), the density column and the
+ReLU mask bits are compared.  Tolerance: 1e-4 of the layer's max |value| (both paths form each
+product with ~2^-17 relative error, in different summation orders); mask bits must agree
+wherever the activation is not within 1e-5 of the max of zero.  Sizes: BASELINE's 4096 x 64
+samples, a ragged M (not a multiple of the 64-sample tile), the per-ray direction rows of the
+ray-mode encoder, and one-tile batches."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import nerf_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    import nerf_amd
+    nerf_amd._lib.load()
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision("high")
+    yield
+    torch.set_float32_matmul_precision(prev)
+
+
+def _model(name):
+    from nerf_amd import BarfPositionalEncoding, FourierFeatures, NerfModel
+    torch.manual_seed(0)
+    if name == "n2v":
+        return NerfModel(4, 256, True, True, 2, FourierFeatures(10, 2 * math.pi), FourierFeatures(4, 1.0))
+    return NerfModel(4, 256, True, False, 2, BarfPositionalEncoding(10, 10.0, 0, 1, True, 1.0),
+                     BarfPositionalEncoding(4, 4.0, 0, 1, True, 1.0))
+
+
+def _run(model, pos_pe, dir_pe, rd, fused):
+    from nerf_amd import mlp, mlp_fused
+    from nerf_amd.mlp import MLPFunction
+    plan = model._get_plan()
+    saved = mlp_fused.ENABLED
+    mlp_fused.ENABLED = fused
+    mlp.CAPTURE = []
+    try:
+        outs = MLPFunction.apply(plan, pos_pe.shape[0], pos_pe, dir_pe, rd, *plan.params())
+        torch.cuda.synchronize()
+        acts, masks = mlp.CAPTURE[0]
+    finally:
+        mlp_fused.ENABLED = saved
+        mlp.CAPTURE = None
+    assert len(acts) == len(plan.layers)
+    return outs, acts, masks, plan
+
+
+@pytest.mark.parametrize("name,M,rd", [("n2v", 4096 * 64, 64), ("n2v", 1000, 1), ("barf", 4096 * 8 + 37, 1),
+                                       ("barf", 64, 64), ("n2v", 3 * 64 + 5, 1)])
+def test_fused_forward_matches_layerwise(name, M, rd):
+    from nerf_amd import mlp_fused
+    model = _model(name).to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(11)
+    pd = model.position_encoder.output_dim
+    dd = model.direction_encoder.output_dim
+    pos_pe = torch.zeros(M, (pd + 31) // 32 * 32, device=DEV)
+    pos_pe[:, :pd] = torch.rand(M, pd, device=DEV, generator=g) * 2 - 1
+    nd = (M + rd - 1) // rd
+    dir_pe = torch.zeros(nd, (dd + 31) // 32 * 32, device=DEV)
+    dir_pe[:, :dd] = torch.rand(nd, dd, device=DEV, generator=g) * 2 - 1
+    plan = model._get_plan()
+    plan.to_device(torch.device(DEV))
+    assert mlp_fused.eligible(plan, M)
+    o_ref, a_ref, m_ref, _ = _run(model, pos_pe, dir_pe, rd, False)
+    o_fus, a_fus, m_fus, _ = _run(model, pos_pe, dir_pe, rd, True)
+    assert len(o_ref) == len(o_fus)
+    errs = []
+    for li, (x, y) in enumerate(zip(a_ref, a_fus)):
+        n = plan.layers[li].N
+        scale = max(1.0, x[:, :n].abs().max().item())
+        err = (x[:, :n] - y[:, :n]).abs().max().item()
+        bad = ((x[:, :n] - y[:, :n]).abs() > 1e-4 * scale).nonzero()
+        errs.append((li, err, scale, bad[:4].tolist(), int(bad.shape[0])))
+    for li, err, scale, bad, nbad in errs:
+        assert err <= 1e-4 * scale, errs
+        # padding columns of the output rows are zero in the fused path
+        if y.shape[1] > n:
+            assert (y[:, n:] == 0).all()
+    widths = [plan.layers[i].N for i in plan.outputs] + [1] * len(plan.column_outputs)
+    for x, y, n in zip(o_ref, o_fus, widths):
+        x, y = x.reshape(x.shape[0], -1)[:, :n], y.reshape(y.shape[0], -1)[:, :n]   # padding columns: unspecified
+        scale = max(1.0, x.abs().max().item())
+        assert (x - y).abs().max().item() <= 1e-4 * scale
+    for li, (ma, mb) in enumerate(zip(m_ref, m_fus)):
+        assert (ma is None) == (mb is None)
+        if ma is None:
+            continue
+        n = plan.layers[li].N
+        bits_a = np.unpackbits(ma.cpu().numpy(), axis=1, bitorder="little")
+        bits_b = np.unpackbits(mb.cpu().numpy(), axis=1, bitorder="little")
+        # bit b of word 2e+h <-> column 4(32h+b)+e
+        cols = np.empty(256, dtype=np.int64)
+        for w in range(8):
+            e, h = w // 2, w % 2
+            for b in range(32):
+                cols[32 * w + b] = 4 * (32 * h + b) + e
+        act = a_ref[li][:, :n].cpu().numpy()
+        near0 = np.abs(act) <= 1e-5 * max(1.0, np.abs(act).max())
+        valid = cols < n
+        diff = (bits_a != bits_b)[:, valid] & ~near0[:, cols[valid]]
+        assert not diff.any(), (li, int(diff.sum()))
+
+
+def test_fused_forward_vs_oracle_subset():
+    """Fused NerfModel forward (n2v config) against the CPU oracle on 512 rows."""
+    model = _model("n2v")
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    model = model.to(DEV)
+    g = torch.Generator().manual_seed(5)
+    M = 64 * 512
+    x = torch.rand(M, 3, generator=g) * 2 - 1
+    d = torch.nn.functional.normalize(torch.randn(M, 3, generator=g), dim=1)
+    from nerf_amd import mlp_fused
+    assert mlp_fused.ENABLED
+    dens, rgb = model(x.to(DEV), d.to(DEV), None, None, None)
+    idx = torch.arange(0, M, 61)
+    pe = O.fourier_features(x[idx], 10, 2 * math.pi)
+    de = O.fourier_features(d[idx], 4, 1.0)
+    od, oc = O.nerf_model_forward(sd, pe, de, 2, 4, True, True)
+    assert (dens.cpu()[idx] - od).abs().max().item() < 2e-4
+    assert (rgb.cpu()[idx] - oc).abs().max().item() < 2e-4

@@ -226,3 +226,111 @@ def test_camera_extrinsics_matches_reference(golden):
     np.testing.assert_allclose(m.rotation.grad.numpy(), g["drot"], atol=1e-4, rtol=1e-5)
     np.testing.assert_allclose(m.translation.grad.numpy(), g["dtrans"], atol=1e-5, rtol=1e-6)
     assert len(m.param_groups) == 1
+
+
+def _emulate_fused(plan, fused, image_f64, x_pos, x_dir, dir_rd, relu_floor=True):
+    """Lane-level numpy emulation of csrc/mlp_fused.hip over the packed image for ONE wave of
+    16 samples: B operands built exactly as the kernel's registers (epilogue order), MFMA
+    16x16x32 as D[i][s] += sum_{g,j} A[lane i+16g][j] * B[lane s+16g][j]."""
+    lane = np.arange(64)
+    s_of, g_of = lane & 15, lane >> 4
+    j = np.arange(8)
+    xreg = None                      # [KBMAX, 64 lanes, 8] register-fed B operand
+    outs = []
+    for idx, lp in enumerate(plan.layers):
+        kbr, kbh, hbm, nb, units, off, bias_off = fused.layers[idx]
+        B = []
+        for kb in range(kbr):
+            B.append(xreg[kb])
+        for s in hbm:
+            t = x_pos if s.kind == "pos" else x_dir
+            rd = 1 if s.kind == "pos" else dir_rd
+            for kh in range(s.k_pad // 32):
+                c = 32 * kh + 8 * g_of[:, None] + j[None, :]
+                rows = (s_of // rd)[:, None]
+                B.append(np.where(c < s.k_seg, t[rows, np.minimum(c, t.shape[1] - 1)], 0.0))
+        KB = len(B)
+        N = lp.module.out_features
+        out = np.zeros((16, 32 * nb))
+        for c in range(nb):
+            base = off + c * units * 1024
+            bias = image_f64["raw"][bias_off // 4 + 32 * c + np.arange(32)]
+            for bb in range(2):
+                acc = np.tile(bias[16 * bb:16 * bb + 16][:, None], (1, 16))     # [i rows][s]
+                for kb in range(KB):
+                    h0 = (base + kb * 4096 + bb * 2048) // 2
+                    frag = image_f64["w"][h0 + lane[:, None] * 8 + j[None, :]]   # hi + lo
+                    A = np.zeros((16, 32))
+                    Bm = np.zeros((32, 16))
+                    for g in range(4):
+                        A[:, 8 * g:8 * g + 8] = frag[np.arange(16) + 16 * g]
+                        Bm[8 * g:8 * g + 8, :] = B[kb][np.arange(16) + 16 * g].T
+                    acc += A @ Bm
+                out[:, 32 * c + 16 * bb:32 * c + 16 * bb + 16] = acc.T
+        if lp.relu:
+            out = np.maximum(out, 0.0)
+        outs.append(out[:, :N])
+        # epilogue register order: xout[c] lane (s, g) element j <- row 32c + 16(j>>2) + 4g + (j&3)
+        xreg = np.zeros((8, 64, 8))
+        for c in range(min(nb, 8)):
+            rows = 32 * c + 16 * (j[None, :] >> 2) + 4 * g_of[:, None] + (j[None, :] & 3)
+            xreg[c] = out[s_of[:, None], rows]
+    return outs
+
+
+@pytest.mark.parametrize("name", ["barf", "n2v"])
+def test_fused_forward_image_emulation(name):
+    """The packed image + lane permutations of the fused MLP forward reproduce NerfModel's
+    forward (emulated on CPU; the kernel itself is checked by the GPU tests)."""
+    from nerf_amd import mlp_fused
+    from nerf_amd.mlp import nerf_model_plan
+    m = _models()[name]
+    pd, dd = m.position_encoder.output_dim, m.direction_encoder.output_dim
+    plan, z_last, head = nerf_model_plan(m.n_segments, m.model_segments, m.model_color, m.hidden_dim, pd, dd,
+                                         m.delayed_direction, m.delayed_density)
+    plan.to_device(torch.device("cpu"))
+    assert mlp_fused.eligible(plan, 4096)
+    fused = mlp_fused.FusedForward(plan, torch.device("cpu"))
+    # pack in numpy exactly as nerf_fused_pack does
+    ps = []
+    for lp in plan.layers:
+        ps += [lp.module.weight.detach().double().numpy().ravel(), lp.module.bias.detach().double().numpy().ravel()]
+    src = fused.map_src.numpy().astype(np.int64)
+    dst = fused.map_dst.numpy().astype(np.int64)
+    vals = np.zeros(src.shape[0])
+    for t in range(len(ps)):
+        sel = (src >= 0) & ((src >> 24) == t)
+        vals[sel] = ps[t][src[sel] & 0xffffff]
+    w = np.zeros(fused.image_bytes // 2)
+    raw = np.zeros(fused.image_bytes // 4)
+    hi = torch.from_numpy(vals).float().bfloat16().double().numpy()
+    lo = torch.from_numpy(vals - hi).float().bfloat16().double().numpy()
+    fr = dst >= 0
+    w[dst[fr]] = hi[fr] + lo[fr]
+    raw[~dst[~fr]] = vals[~fr]
+    g = torch.Generator().manual_seed(3)
+    S = 16
+    x_pos = torch.rand(16, pd, generator=g).double().numpy() * 2 - 1
+    x_dir = torch.rand(1, dd, generator=g).double().numpy() * 2 - 1
+    x_pos = np.pad(x_pos, ((0, 0), (0, (-pd) % 4)))
+    x_dir = np.pad(x_dir, ((0, 0), (0, (-dd) % 4)))
+    outs = _emulate_fused(plan, fused, {"w": w, "raw": raw}, x_pos, x_dir, S)
+    # reference: the Linear stack in fp64
+    acts = []
+    for idx, lp in enumerate(plan.layers):
+        parts = []
+        for s in lp.sources:
+            if s.kind == "act":
+                parts.append(acts[s.layer][:, :s.k_valid])
+            elif s.kind == "pos":
+                parts.append(x_pos[:, :s.k_valid])
+            else:
+                parts.append(np.repeat(x_dir[:, :s.k_valid], 16, axis=0))
+        x = np.concatenate(parts, axis=1)
+        y = x @ lp.module.weight.detach().double().numpy().T + lp.module.bias.detach().double().numpy()
+        if lp.relu:
+            y = np.maximum(y, 0.0)
+        acts.append(y)
+    for idx in range(len(plan.layers)):
+        err = np.abs(outs[idx] - acts[idx]).max()
+        assert err <= 1e-4 * max(1.0, np.abs(acts[idx]).max()), (idx, err)
