@@ -39,7 +39,6 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 
 constexpr int SLOT_BYTES = 40 * 1024;      // largest chunk: 10 k-blocks x 4 KB
 constexpr int NSLOT = 2;
-constexpr int STAGE_BYTES = 16 * 128;      // per wave: 16 sample rows x 32 fp32 output columns
 constexpr int XO_BYTES = 8 * 2048;         // per wave: the next layer's B operand, [kb][hi|lo][lane] 16 B
 constexpr int BIAS_LDS = 12 * 1024;        // all biases of the network ([layer][nb][32] fp32), copied once
 constexpr int WG = 256;                    // 4 waves, one per SIMD (up to 512 registers each)
@@ -124,10 +123,8 @@ struct Ctx {
     // repeats per tile, so the next chunk is d_off; layer fields are only read when it changes
     int d_off, d_kb, d_left, d_layer;
     int d_remaining;      // chunks still to issue
-    char* stage;          // this wave's LDS transpose buffer for the output stores
     char* xo;             // this wave's LDS image of the next layer's B operand
     const char* bias;     // LDS copy of the biases
-    int tile0;            // first sample row of the current tile
     // the current layer's register-fed input (B operand)
     bf16x8 xh[KBMAX], xl[KBMAX];
 };
@@ -170,21 +167,12 @@ struct LayerState {
     int sample, col_idx;
     unsigned sample_off;  // sample * 4 (OOB past M)
     unsigned row_off;     // byte offset of this lane's sample row (OOB past M; direct stores)
-    unsigned st_off[2];   // byte offsets of the two rows this lane stores (transposed stores)
     int64_t ldo;
     __amdgpu_buffer_rsrc_t ro, rm, rc;
     int bias_lds;         // LDS byte offset of the layer's biases (+128 per chunk; >= 128)
     unsigned mw[2];       // ReLU mask words 2g, 2g + 1 of this lane's sample row, filled chunk by chunk
 };
 
-#ifdef NERF_STORE_NOP
-#define NERF_AFTER_STORE() asm volatile("s_nop 4" ::: "memory")
-#else
-#define NERF_AFTER_STORE() (void)0
-#endif
-#ifndef NERF_STORE_TRANSPOSED
-#define NERF_STORE_TRANSPOSED 0
-#endif
 
 // Epilogue of chunk nbc (output rows 32 nbc .. +31, accumulator blocks v0 / v1, biases b0 / b1):
 // bias + ReLU, stores and the next layer's B-operand registers xo.  Straight-line code in four
@@ -205,40 +193,15 @@ __device__ __forceinline__ void chunk_epilogue(Ctx& c, LayerState& st, int nbc, 
             v1[r] = __builtin_bit_cast(float, max(__builtin_bit_cast(int, v1[r] + b1[r]), st.floor_i));
         }
         const int colok = nbc >= 0 ? (int)st.ldo : 0;
-#if NERF_STORE_TRANSPOSED
-        // transpose through the wave's LDS stage so that every store writes whole 128-byte row
-        // segments (16-byte slot q of row s lives at slot q ^ (s & 7): conflict-free both ways)
-        const int s_ = c.lane & 15;
-        *reinterpret_cast<f4*>(c.stage + s_ * 128 + ((g ^ (s_ & 7)) << 4)) = v0;
-        *reinterpret_cast<f4*>(c.stage + s_ * 128 + (((4 + g) ^ (s_ & 7)) << 4)) = v1;
-        const int p = c.lane & 7, r0 = c.lane >> 3;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int r = r0 + 8 * h;
-            const f4 q = *reinterpret_cast<const f4*>(c.stage + r * 128 + ((p ^ (r & 7)) << 4));
-            const int col = 32 * nbc + 4 * p;
-            const unsigned off = (unsigned)col < (unsigned)colok ? st.st_off[h] + (unsigned)col * 4u : OOB;
-            if (!(NERF_DIAG & 1)) __builtin_amdgcn_raw_buffer_store_b128(q, st.ro, off, 0, 0);
-        }
-#else
-#ifdef NERF_ROW_RECOMP
-        const int m_ = c.tile0 + c.wave * SPW + (int)(__lane_id() & 15);
-        const unsigned row_off = m_ < c.M ? (unsigned)(m_ * (int)st.ldo * 4) : OOB;
-#else
-        const unsigned row_off = st.row_off;
-#endif
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) {
             const int col = 32 * nbc + 16 * bb + 4 * g;
-            const unsigned off = (unsigned)col < (unsigned)colok ? row_off + (unsigned)col * 4u : OOB;   // nbc = -1: col < 0
+            const unsigned off = (unsigned)col < (unsigned)colok ? st.row_off + (unsigned)col * 4u : OOB;   // nbc = -1: col < 0
             if (!(NERF_DIAG & 1)) __builtin_amdgcn_raw_buffer_store_b128(bb ? v1 : v0, st.ro, off, 0, 0);
-            NERF_AFTER_STORE();
         }
-#endif
         const unsigned coff = (g == 0 && st.col_idx == 32 * nbc) ? st.sample_off : OOB;
         if (!(NERF_DIAG & 1)) {
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v0[0]), st.rc, coff, 0, 0);
-            NERF_AFTER_STORE();
             count_vm(c, 3);
         }
     } else if constexpr (PART == 1) {
@@ -251,15 +214,10 @@ __device__ __forceinline__ void chunk_epilogue(Ctx& c, LayerState& st, int nbc, 
             w |= (v1[r] > 0.f ? 1u : 0u) << (8 * r + 4 + g);
         }
     } else if constexpr (PART == 2) {
-#ifdef NERF_MASK_SHFL
-        w |= (unsigned)__shfl_xor((int)w, 16, 64);
-        w |= (unsigned)__shfl_xor((int)w, 32, 64);
-#else
         const auto x16 = __builtin_amdgcn_permlane16_swap(w, w, false, false);   // OR with lane ^ 16
         w = x16[0] | x16[1];
         const auto x32 = __builtin_amdgcn_permlane32_swap(w, w, false, false);   // OR with lane ^ 32
         w = x32[0] | x32[1];
-#endif
         const unsigned byte = ((w >> (8 * g)) & 0xffu) << (8 * (nbc & 3));
         st.mw[0] |= (nbc >= 0 && nbc < 4) ? byte : 0u;
         st.mw[1] |= (nbc >= 4 && nbc < 8) ? byte : 0u;
@@ -290,15 +248,7 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int sample) {
     st.row_ok = sample < c.M;
     st.row_off = st.row_ok ? (unsigned)((int64_t)sample * st.ldo * 4) : OOB;
     st.sample_off = st.row_ok ? (unsigned)(sample * 4) : OOB;
-    {
-        const int m0 = sample - (c.lane & 15);          // the wave's first sample row
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int m = m0 + (c.lane >> 3) + 8 * h;
-            st.st_off[h] = m < c.M ? (unsigned)((int64_t)m * st.ldo * 4) : OOB;
-        }
-        st.mw[0] = st.mw[1] = 0;
-    }
+    st.mw[0] = st.mw[1] = 0;
     st.ro = __builtin_amdgcn_make_buffer_rsrc(LF(fptr_t, out, l), 0, (int)((int64_t)c.M * st.ldo * 4), RSRC_W3);
     uint8_t* mptr = LF(u8ptr_t, mask, l);
     st.rm = __builtin_amdgcn_make_buffer_rsrc(mptr, 0, mptr != nullptr ? c.M * 32 : 0, RSRC_W3);
@@ -338,7 +288,7 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int sample) {
 
     f4 p0 = {}, p1 = {};
     for (int nbc = 0; nbc < st.NB; ++nbc) {
-#if NERF_DIAG || defined(NERF_WAIT_LADDER)
+#if NERF_DIAG
         if (!(NERF_DIAG & 2)) wait_vm(c.after_last);   // this chunk's own DMA share has landed
 #else
         // this chunk's own DMA share has landed: every chunk issues its successor's DMA and then
@@ -369,8 +319,13 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int sample) {
             bf16x8(&f)[4] = (kb & 1) ? fb : fa;
             const bf16x8 bh = kb < KBR ? c.xh[kb < KBR ? kb : 0] : hh[kb < KBR ? 0 : kb - KBR];
             const bf16x8 bl = kb < KBR ? c.xl[kb < KBR ? kb : 0] : hl[kb < KBR ? 0 : kb - KBR];
-            a0 = mfma_x3(f[0], f[1], bh, bl, a0);
-            a1 = mfma_x3(f[2], f[3], bh, bl, a1);
+            // the two accumulators alternate: consecutive MFMAs are independent
+            a0 = mfma16(f[1], bh, a0);
+            a1 = mfma16(f[3], bh, a1);
+            a0 = mfma16(f[0], bl, a0);
+            a1 = mfma16(f[2], bl, a1);
+            a0 = mfma16(f[0], bh, a0);
+            a1 = mfma16(f[2], bh, a1);
             if (kb + 2 < KB) frag(kb + 2, f);
             // the previous chunk's epilogue, one part per stage (all in the last stage if KB < 4)
             if (kb == 0) chunk_epilogue<0>(c, st, ep, p0, p1, w);
@@ -379,24 +334,14 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int sample) {
             if (kb == (KB > 3 ? 3 : KB - 1)) chunk_epilogue<3>(c, st, ep, p0, p1, w);
             __builtin_amdgcn_sched_barrier(0);
         }
-#ifdef NERF_MFMA_NOP
-        // the accumulators stay in AGPRs across these wait states, so no VALU reads them before
-        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(a0), "+a"(a1));
-#endif
         c.cur = slot ^ 1;
         p0 = a0;
         p1 = a1;
     }
     {
-#ifdef NERF_FINAL_NOP
-        asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
-#endif
         unsigned w = 0;
         const int nbc = st.NB - 1;
         chunk_epilogue<0>(c, st, nbc, p0, p1, w);
-#ifdef NERF_FINAL_DRAIN
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
         chunk_epilogue<1>(c, st, nbc, p0, p1, w);
         chunk_epilogue<2>(c, st, nbc, p0, p1, w);
         chunk_epilogue<3>(c, st, nbc, p0, p1, w);
@@ -419,11 +364,7 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int sample) {
 }
 
 __global__ __launch_bounds__(WG, 1) void mlp_fused_fwd_kernel(FusedArgs a) {
-#if NERF_STORE_TRANSPOSED
-    __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT_BYTES + NWAVE * (XO_BYTES + STAGE_BYTES) + BIAS_LDS];
-#else
     __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT_BYTES + NWAVE * XO_BYTES + BIAS_LDS];
-#endif
     Ctx c;
     c.kargs = (kchar_t*)__builtin_amdgcn_kernarg_segment_ptr();
     c.smem = smem;
@@ -431,7 +372,6 @@ __global__ __launch_bounds__(WG, 1) void mlp_fused_fwd_kernel(FusedArgs a) {
     c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     c.xo = smem + NSLOT * SLOT_BYTES + c.wave * XO_BYTES;
     c.bias = smem + NSLOT * SLOT_BYTES + NWAVE * XO_BYTES;
-    c.stage = smem + NSLOT * SLOT_BYTES + NWAVE * XO_BYTES + BIAS_LDS + c.wave * STAGE_BYTES;
     c.bias_base = a.bias_base;
     c.lane = threadIdx.x & 63;
     c.M = a.M;
@@ -461,7 +401,6 @@ __global__ __launch_bounds__(WG, 1) void mlp_fused_fwd_kernel(FusedArgs a) {
     }
     for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
         const int sample = tile * TILE + c.wave * SPW + (c.lane & 15);
-        c.tile0 = tile * TILE;
         for (int l = 0; l < a.n_layers; ++l) {
             switch (LF(int, type, l)) {
                 case 1: fused_layer<0, 1>(c, l, sample); break;
