@@ -286,13 +286,22 @@ def main():
     x3 = matmul_precision() == "x3"
     nt_name = "linear_nt_x3" if x3 else "linear_nt"
     peak = X3_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
-    nt = ks.get(nt_name, {"launches": 0, "flops": 0.0, "ms": 0.0})
+    # the roofline kernel: the MFMA kernel with the most device time per step (the fused field-MLP
+    # forward, the input-gradient GEMMs or the weight-gradient GEMMs)
+    cands = [k for k in ("mlp_fused_fwd", nt_name, "linear_wgrad_x3" if x3 else "linear_wgrad") if k in ks]
+    dom = max(cands, key=lambda k: ks[k]["ms"]) if cands else nt_name
+    nt = ks.get(dom, {"launches": 0, "flops": 0.0, "ms": 0.0})
     nt_avg_ms = nt["ms"] / max(nt["launches"], 1)
     nt_avg_flops = nt["flops"] / max(nt["launches"], 1)
     achieved = (nt_avg_flops / (nt_avg_ms * 1e-3)) / 1e12 if nt_avg_ms > 0 else 0.0
+    dom_desc = {
+        "mlp_fused_fwd": "the whole field-MLP forward in one launch",
+        nt_name: "input-gradient GEMMs",
+        "linear_wgrad_x3": "weight-gradient GEMMs", "linear_wgrad": "weight-gradient GEMMs",
+    }.get(dom, dom)
 
     traffic = None
-    tfile = os.path.join(ROOT, "profiles", f"traffic_{nt_name}.json")
+    tfile = os.path.join(ROOT, "profiles", f"traffic_{dom}.json")
     if args.workload == "n2v" and os.path.exists(tfile):
         with open(tfile) as f:
             traffic = json.load(f).get("bytes_per_launch")
@@ -324,9 +333,9 @@ def main():
                        "rays_per_gpu": wl["rays"], "samples_per_ray": wl["coarse"] + wl["fine"],
                        "coarse_samples": wl["coarse"], "fine_samples": wl["fine"], "global_rays": wl["rays"] * world,
                        "parallelism": f"ray-batch dp{world}" + (" (RCCL all-reduce)" if world > 1 else "")},
-            "roofline": {"kernel": (f"{nt_name} (" + ("3 x bf16 MFMA 32x32x16; peak = bf16 dense / 3"
-                                                       if x3 else "fp32 MFMA 32x32x2")
-                                    + ": forward + input-gradient GEMMs; achieved in algorithmic fp32 GEMM flops)"),
+            "roofline": {"kernel": (f"{dom} (" + ("3 x bf16 MFMA; peak = bf16 dense / 3"
+                                                   if x3 else "fp32 MFMA 32x32x2")
+                                    + f": {dom_desc}; achieved in algorithmic fp32 GEMM flops)"),
                          "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": traffic,
                          "avg_launch_us": nt_avg_ms * 1e3, "avg_flops_per_launch": nt_avg_flops,
