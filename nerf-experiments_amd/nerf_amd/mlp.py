@@ -90,6 +90,8 @@ class LayerPlan:
     Wpx: torch.Tensor | None = None
     Wtx: torch.Tensor | None = None
     packed_version_x3: tuple = ()
+    packed_version_t: tuple = ()
+    packed_version_x3t: tuple = ()
 
     def finalize(self, device):
         self.N = self.module.out_features
@@ -114,26 +116,38 @@ class LayerPlan:
         self.col_map = torch.tensor(cm, dtype=torch.int32, device=device)
         self.Wp = torch.empty(K.pad128(self.N), self.Kp, device=device, dtype=torch.float32)
         self.Wt = torch.empty(K.pad128(self.Kp) + 128, self.ldwt, device=device, dtype=torch.float32)
-        self.packed_version = ()
+        self.packed_version = self.packed_version_t = ()
         self.Wpx = self.Wtx = None
-        self.packed_version_x3 = ()
+        self.packed_version_x3 = self.packed_version_x3t = ()
 
-    def pack(self, precision: str = "fp32"):
+    def pack(self, precision: str = "fp32", forward: bool = True):
+        """Refresh the packed weights whose parameter version changed: the forward layouts (Wp /
+        Wpx; skipped with forward=False, when the fused forward kernel runs the layer) and the
+        transposed ones the input-gradient GEMMs use (Wt / Wtx)."""
         w = self.module.weight
         ver = (w._version, w.data_ptr())
+        x3 = precision == "x3"
         # in split precision the fp32 packs only serve GEMMs with <= 32 output columns: this
         # layer's forward (N <= 32) and the input gradients of sources <= 32 columns wide
-        need_fp32 = precision != "x3" or self.N <= 32 or any(s.k_pad <= 32 for s in self.sources)
-        if need_fp32 and ver != self.packed_version:
-            K.pack_weight(w.detach().contiguous(), self.col_map, self.Kp, self.Wp, self.Wt, self.ldwt)
-            self.packed_version = ver
-        if precision == "x3" and ver != self.packed_version_x3:
-            if self.Wpx is None:
-                dev = self.Wp.device
-                self.Wpx = torch.empty(self.Wp.shape[0], 2 * self.Wp.shape[1], device=dev, dtype=torch.bfloat16)
-                self.Wtx = torch.empty(self.Wt.shape[0], 2 * self.Wt.shape[1], device=dev, dtype=torch.bfloat16)
-            K.pack_weight_x3(w.detach().contiguous(), self.col_map, self.Kp, self.Wpx, self.Wtx, self.ldwt)
-            self.packed_version_x3 = ver
+        p = forward and (not x3 or self.N <= 32) and ver != self.packed_version
+        t = (not x3 or any(s.k_pad <= 32 for s in self.sources)) and ver != self.packed_version_t
+        if p or t:
+            K.pack_weight(w.detach().contiguous(), self.col_map, self.Kp, self.Wp if p else None,
+                          self.Wt if t else None, self.ldwt)
+            self.packed_version = ver if p else self.packed_version
+            self.packed_version_t = ver if t else self.packed_version_t
+        if x3:
+            px = forward and ver != self.packed_version_x3
+            tx = ver != self.packed_version_x3t
+            if px or tx:
+                if self.Wpx is None:
+                    dev = self.Wp.device
+                    self.Wpx = torch.empty(self.Wp.shape[0], 2 * self.Wp.shape[1], device=dev, dtype=torch.bfloat16)
+                    self.Wtx = torch.empty(self.Wt.shape[0], 2 * self.Wt.shape[1], device=dev, dtype=torch.bfloat16)
+                K.pack_weight_x3(w.detach().contiguous(), self.col_map, self.Kp, self.Wpx if px else None,
+                                 self.Wtx if tx else None, self.ldwt)
+                self.packed_version_x3 = ver if px else self.packed_version_x3
+                self.packed_version_x3t = ver if tx else self.packed_version_x3t
 
     def gemm(self, precision: str, segs, M: int, transpose: bool, N: int, bias, out, epi, aux=None,
              row_offset: int = 0):
@@ -210,7 +224,7 @@ class MLPFunction(torch.autograd.Function):
             if fused is None:
                 fused = plan.fused[pos.device] = mlp_fused.FusedForward(plan, pos.device)
             for idx, lp in enumerate(plan.layers):
-                lp.pack(prec)                 # the input-gradient GEMMs of the backward use Wtx
+                lp.pack(prec, forward=False)  # only the input-gradient GEMMs' layouts (Wt / Wtx)
                 acts.append(torch.empty(M, lp.out_ld, device=pos.device, dtype=torch.float32))
                 masks.append(torch.empty(M, 32, device=pos.device, dtype=torch.uint8)
                              if lp.relu and plan.consumed[idx] and lp.N <= 256 else None)
