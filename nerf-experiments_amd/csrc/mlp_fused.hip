@@ -39,12 +39,13 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 
 constexpr int SLOT_BYTES = 40 * 1024;      // largest chunk: 10 k-blocks x 4 KB
 constexpr int NSLOT = 2;
-constexpr int XO_BYTES = 8 * 2048;         // per wave: the next layer's B operand, [kb][hi|lo][lane] 16 B
+constexpr int XO_BYTES = 8 * 2048;         // per wave pair: the next layer's B operand, [kb][hi|lo][lane] 16 B
+constexpr int MX_BYTES = 64 * 8;           // per wave pair: mask-word exchange (the high nibbles)
 constexpr int BIAS_LDS = 12 * 1024;        // all biases of the network ([layer][nb][32] fp32), copied once
-constexpr int WG = 256;                    // 4 waves, one per SIMD (up to 512 registers each)
+constexpr int WG = 512;                    // 8 waves, two per SIMD (<= 256 registers each)
 constexpr int NWAVE = WG / 64;
-constexpr int SPW = 16;                    // samples per wave
-constexpr int TILE = NWAVE * SPW;          // samples per workgroup tile
+constexpr int SPW = 16;                    // samples per wave pair
+constexpr int TILE = NWAVE / 2 * SPW;      // samples per workgroup tile
 constexpr int KBMAX = 8;                   // register-fed 32-deep k-blocks (256 features)
 constexpr unsigned OOB = 0x80000000u;      // buffer offset past every num_records: load 0 / drop store
 constexpr int RSRC_W3 = 0x00020000;
@@ -52,7 +53,7 @@ constexpr int RSRC_W3 = 0x00020000;
 #ifndef NERF_DIAG
 #define NERF_DIAG 0       // timing diagnostics only: 1 no stores, 2 no DMA wait, 4 no barrier, 8 no MFMA
 #endif
-constexpr int EPI_MIN_VM = 3;
+constexpr int EPI_MIN_VM = 2;
 
 struct FusedArgs {
     nerf_fused_layer L[NERF_FUSED_MAX_LAYERS];
@@ -115,15 +116,17 @@ struct Ctx {
     char* smem;
     const char* img;
     int wave, lane, M, n_layers, bias_base;
+    int half;             // which 16-row block of every 32-row chunk this wave computes
     int cur;              // ring slot of the chunk being computed
     // vector-memory ops issued after the newest chunk DMA (= the chunk about to be computed), so
     // s_waitcnt vmcnt(after_last) is exactly its wait
     int after_prev, after_last;
     // DMA cursor: chunks of consecutive layers are contiguous in the image and the stream
     // repeats per tile, so the next chunk is d_off; layer fields are only read when it changes
-    int d_off, d_kb, d_left, d_layer;
+    int d_off, d_units, d_left, d_layer;
     int d_remaining;      // chunks still to issue
-    char* xo;             // this wave's LDS image of the next layer's B operand
+    char* xo;             // the wave pair's LDS image of the next layer's B operand
+    char* mx;             // the wave pair's mask-word exchange
     const char* bias;     // LDS copy of the biases
     // the current layer's register-fed input (B operand)
     bf16x8 xh[KBMAX], xl[KBMAX];
@@ -134,24 +137,23 @@ __device__ __forceinline__ void count_vm(Ctx& c, int n) {
     c.after_last += n;
 }
 
-// LDS-DMA of the next chunk of the stream into ring slot `slot`: each wave copies d_kb of its
-// 4 * d_kb 1 KB units
+// LDS-DMA of the next chunk of the stream into ring slot `slot` (the 8 waves share its 1 KB units)
 __device__ __forceinline__ void issue_dma(Ctx& c, int slot) {
     int cnt = 0;
     if (c.d_remaining > 0) {
-        const char* src = c.img + c.d_off + (c.wave + 0) * 1024 + c.lane * 16;
-        char* dst = c.smem + slot * SLOT_BYTES + c.wave * 1024;
-        for (int q = 0; q < c.d_kb; ++q)
-            __builtin_amdgcn_global_load_lds((glb_void_t*)(src + q * NWAVE * 1024),
-                                             (lds_void_t*)(dst + q * NWAVE * 1024), 16, 0, 0);
-        cnt = c.d_kb;
-        c.d_off += c.d_kb * NWAVE * 1024;
+        const char* src = c.img + c.d_off + c.lane * 16;
+        char* dst = c.smem + slot * SLOT_BYTES;
+        for (int u = c.wave; u < c.d_units; u += NWAVE) {
+            __builtin_amdgcn_global_load_lds((glb_void_t*)(src + u * 1024), (lds_void_t*)(dst + u * 1024), 16, 0, 0);
+            ++cnt;
+        }
+        c.d_off += c.d_units * 1024;
         if (--c.d_left == 0) {
             if (++c.d_layer == c.n_layers) {
                 c.d_layer = 0;
                 c.d_off = 0;
             }
-            c.d_kb = LF(int, chunk_units, c.d_layer) / NWAVE;
+            c.d_units = LF(int, chunk_units, c.d_layer);
             c.d_left = LF(int, nb, c.d_layer);
         }
         --c.d_remaining;
@@ -166,53 +168,41 @@ struct LayerState {
     int floor_i;          // ReLU as an integer max on the fp32 bits: 0, or INT_MIN for no ReLU
     int sample, col_idx;
     unsigned sample_off;  // sample * 4 (OOB past M)
-    unsigned row_off;     // byte offset of this lane's sample row (OOB past M; direct stores)
+    unsigned row_off;     // byte offset of this lane's sample row (OOB past M)
     int64_t ldo;
     __amdgpu_buffer_rsrc_t ro, rm, rc;
     int bias_lds;         // LDS byte offset of the layer's biases (+128 per chunk; >= 128)
-    unsigned mw[2];       // ReLU mask words 2g, 2g + 1 of this lane's sample row, filled chunk by chunk
+    unsigned mw[2];       // ReLU mask words 2g, 2g + 1 of this lane's sample row (this wave's nibbles)
 };
 
-
-// Epilogue of chunk nbc (output rows 32 nbc .. +31, accumulator blocks v0 / v1, biases b0 / b1):
-// bias + ReLU, stores and the next layer's B-operand registers xo.  Straight-line code in four
-// parts (absent outputs are buffer stores with out-of-range offsets, which the hardware drops),
-// placed in the stages of the next chunk so that its VALU work issues in MFMA shadows.
+// Epilogue of this wave's block of chunk nbc (output rows 32 nbc + 16 half .. +15, accumulator v):
+// bias + ReLU, stores, mask bits and the wave pair's B-operand image.  Straight-line code in
+// four parts (absent outputs are buffer stores with out-of-range offsets, which the hardware
+// drops), placed in the stages of the next chunk so that its VALU work issues in MFMA shadows.
+// nbc = -1 (the call in a layer's first chunk) writes nothing visible.
 template <int PART>
-__device__ __forceinline__ void chunk_epilogue(Ctx& c, LayerState& st, int nbc, f4& v0, f4& v1, unsigned& w) {
-    // nbc = -1 (the call in a layer's first chunk) writes nothing visible: stores get
-    // out-of-range offsets, the mask words no byte, the B-operand image its spare slot
+__device__ __forceinline__ void chunk_epilogue(Ctx& c, LayerState& st, int nbc, f4& v, unsigned& w) {
     const int g = c.lane >> 4;
     if constexpr (PART == 0) {
-        const float* bias = reinterpret_cast<const float*>(c.bias + st.bias_lds + 128 * nbc);   // nbc = -1: unused
-        const f4 b0 = *reinterpret_cast<const f4*>(bias + 4 * g);
-        const f4 b1 = *reinterpret_cast<const f4*>(bias + 16 + 4 * g);
+        const f4 b = *reinterpret_cast<const f4*>(c.bias + st.bias_lds + 128 * nbc + 64 * c.half + 16 * g);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            v0[r] = __builtin_bit_cast(float, max(__builtin_bit_cast(int, v0[r] + b0[r]), st.floor_i));
-            v1[r] = __builtin_bit_cast(float, max(__builtin_bit_cast(int, v1[r] + b1[r]), st.floor_i));
-        }
+        for (int r = 0; r < 4; ++r)
+            v[r] = __builtin_bit_cast(float, max(__builtin_bit_cast(int, v[r] + b[r]), st.floor_i));
         const int colok = nbc >= 0 ? (int)st.ldo : 0;
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb) {
-            const int col = 32 * nbc + 16 * bb + 4 * g;
-            const unsigned off = (unsigned)col < (unsigned)colok ? st.row_off + (unsigned)col * 4u : OOB;   // nbc = -1: col < 0
-            if (!(NERF_DIAG & 1)) __builtin_amdgcn_raw_buffer_store_b128(bb ? v1 : v0, st.ro, off, 0, 0);
-        }
-        const unsigned coff = (g == 0 && st.col_idx == 32 * nbc) ? st.sample_off : OOB;
+        const int col = 32 * nbc + 16 * c.half + 4 * g;
+        const unsigned off = (unsigned)col < (unsigned)colok ? st.row_off + (unsigned)col * 4u : OOB;   // nbc = -1: col < 0
+        const unsigned coff = (c.half == 0 && g == 0 && st.col_idx == 32 * nbc) ? st.sample_off : OOB;
         if (!(NERF_DIAG & 1)) {
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v0[0]), st.rc, coff, 0, 0);
-            count_vm(c, 3);
+            __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), st.rc, coff, 0, 0);
+            count_vm(c, 2);
         }
     } else if constexpr (PART == 1) {
         // NERF_EPI_MASKOUT layout: column 32 nb + 16 bb + 4 g + r is bit 4 bb + g of byte (nb & 3)
         // of word 2 r + (nb >> 2) of the row; lane group g keeps the byte of r = g
         w = 0;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            w |= (v0[r] > 0.f ? 1u : 0u) << (8 * r + g);
-            w |= (v1[r] > 0.f ? 1u : 0u) << (8 * r + 4 + g);
-        }
+        for (int r = 0; r < 4; ++r) w |= (v[r] > 0.f ? 1u : 0u) << (8 * r + 4 * c.half + g);
     } else if constexpr (PART == 2) {
         const auto x16 = __builtin_amdgcn_permlane16_swap(w, w, false, false);   // OR with lane ^ 16
         w = x16[0] | x16[1];
@@ -222,20 +212,21 @@ __device__ __forceinline__ void chunk_epilogue(Ctx& c, LayerState& st, int nbc, 
         st.mw[0] |= (nbc >= 0 && nbc < 4) ? byte : 0u;
         st.mw[1] |= (nbc >= 4 && nbc < 8) ? byte : 0u;
     } else {
-        // the next layer's B operand, k-block nbc (rows 32 nbc .. +31), into the wave's LDS image
-        // (read back into registers at the end of the layer)
-        const f8 x = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-        bf16x8 h, lo;
-        split8(x, h, lo);
+        // the next layer's B operand, k-block nbc: elements j < 4 are block 0 (this pair's
+        // half-0 wave), j >= 4 block 1 -> 8 bytes of each lane's 16-byte hi and lo slots
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        const bf16x4 h = __builtin_convertvector(v, bf16x4);
+        const bf16x4 lo = __builtin_convertvector(v - __builtin_convertvector(h, f4), bf16x4);
         if (nbc >= 0 && nbc < KBMAX) {
-            *reinterpret_cast<bf16x8*>(c.xo + nbc * 2048 + c.lane * 16) = h;
-            *reinterpret_cast<bf16x8*>(c.xo + nbc * 2048 + 1024 + c.lane * 16) = lo;
+            *reinterpret_cast<bf16x4*>(c.xo + nbc * 2048 + c.lane * 16 + 8 * c.half) = h;
+            *reinterpret_cast<bf16x4*>(c.xo + nbc * 2048 + 1024 + c.lane * 16 + 8 * c.half) = lo;
         }
     }
 }
 
-// one layer: runtime loop over its 32-row output chunks; k-blocks unrolled (KBR register-fed,
-// KBH HBM-fed).  Reads c.xh/c.xl, leaves the next layer's input there.
+// one layer: runtime loop over its 32-row output chunks (this wave: one 16-row block of each);
+// k-blocks unrolled (KBR register-fed, KBH HBM-fed).  Reads c.xh/c.xl, leaves the next layer's
+// input there.
 template <int KBR, int KBH>
 __device__ __forceinline__ void fused_layer(Ctx& c, int l, int sample) {
     constexpr int KB = KBR + KBH;
@@ -286,26 +277,27 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int sample) {
         for (int kh = 0; kh < KBH; ++kh) split8(raw[kh], hh[kh], hl[kh]);
     }
 
-    f4 p0 = {}, p1 = {};
+    f4 p = {};
     for (int nbc = 0; nbc < st.NB; ++nbc) {
 #if NERF_DIAG
-        if (!(NERF_DIAG & 2)) wait_vm(c.after_last);   // this chunk's own DMA share has landed
+        if (!(NERF_DIAG & 2)) wait_vm(c.after_last);
 #else
         // this chunk's own DMA share has landed: every chunk issues its successor's DMA and then
-        // at least EPI_MIN_VM vector-memory ops (2 bias loads, 3 epilogue stores; more at layer
-        // boundaries, which only makes this wait stricter), so a constant count is exact or safe
+        // at least EPI_MIN_VM vector-memory ops (the epilogue stores; more at layer boundaries,
+        // which only makes this wait stricter), so a constant count is exact or safe
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EPI_MIN_VM) : "memory");
 #endif
         if (!(NERF_DIAG & 4)) barrier();               // ... and everyone else's; the other slot is free
         const int slot = c.cur;
-        const char* S = c.smem + slot * SLOT_BYTES + c.lane * 16;
-        // explicit software pipeline: the fragments of k-block kb + 2 are read while kb's six
+        // this wave's 16-row block of the chunk: [kb][block][hi 1 KB | lo 1 KB]
+        const char* S = c.smem + slot * SLOT_BYTES + c.half * 2048 + c.lane * 16;
+        // explicit software pipeline: the fragments of k-block kb + 2 are read while kb's three
         // MFMAs run; sched_barriers pin the stages.  The previous chunk's epilogue covers the
         // latency of the first reads and fills the MFMA shadows of the first stages.
-        bf16x8 fa[4], fb[4];
-        auto frag = [&](int kb, bf16x8 (&f)[4]) __attribute__((always_inline)) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) f[q] = *reinterpret_cast<const bf16x8*>(S + kb * 4096 + q * 1024);
+        bf16x8 fa[2], fb[2];
+        auto frag = [&](int kb, bf16x8 (&f)[2]) __attribute__((always_inline)) {
+            f[0] = *reinterpret_cast<const bf16x8*>(S + kb * 4096);
+            f[1] = *reinterpret_cast<const bf16x8*>(S + kb * 4096 + 1024);
         };
         frag(0, fa);
         if (KB > 1) frag(1, fb);
@@ -313,65 +305,63 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int sample) {
         __builtin_amdgcn_sched_barrier(0);            // keep the DMA ahead of every other vmem op (vmcnt)
         unsigned w = 0;
         const int ep = nbc - 1;                        // the previous chunk (-1: none)
-        f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+        f4 a = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
-            bf16x8(&f)[4] = (kb & 1) ? fb : fa;
+            bf16x8(&f)[2] = (kb & 1) ? fb : fa;
             const bf16x8 bh = kb < KBR ? c.xh[kb < KBR ? kb : 0] : hh[kb < KBR ? 0 : kb - KBR];
             const bf16x8 bl = kb < KBR ? c.xl[kb < KBR ? kb : 0] : hl[kb < KBR ? 0 : kb - KBR];
-            // the two accumulators alternate: consecutive MFMAs are independent
-            a0 = mfma16(f[1], bh, a0);
-            a1 = mfma16(f[3], bh, a1);
-            a0 = mfma16(f[0], bl, a0);
-            a1 = mfma16(f[2], bl, a1);
-            a0 = mfma16(f[0], bh, a0);
-            a1 = mfma16(f[2], bh, a1);
+            a = mfma_x3(f[0], f[1], bh, bl, a);
             if (kb + 2 < KB) frag(kb + 2, f);
             // the previous chunk's epilogue, one part per stage (all in the last stage if KB < 4)
-            if (kb == 0) chunk_epilogue<0>(c, st, ep, p0, p1, w);
-            if (kb == (KB > 1 ? 1 : 0)) chunk_epilogue<1>(c, st, ep, p0, p1, w);
-            if (kb == (KB > 2 ? 2 : KB - 1)) chunk_epilogue<2>(c, st, ep, p0, p1, w);
-            if (kb == (KB > 3 ? 3 : KB - 1)) chunk_epilogue<3>(c, st, ep, p0, p1, w);
+            if (kb == 0) chunk_epilogue<0>(c, st, ep, p, w);
+            if (kb == (KB > 1 ? 1 : 0)) chunk_epilogue<1>(c, st, ep, p, w);
+            if (kb == (KB > 2 ? 2 : KB - 1)) chunk_epilogue<2>(c, st, ep, p, w);
+            if (kb == (KB > 3 ? 3 : KB - 1)) chunk_epilogue<3>(c, st, ep, p, w);
             __builtin_amdgcn_sched_barrier(0);
         }
         c.cur = slot ^ 1;
-        p0 = a0;
-        p1 = a1;
+        p = a;
     }
     {
         unsigned w = 0;
         const int nbc = st.NB - 1;
-        chunk_epilogue<0>(c, st, nbc, p0, p1, w);
-        chunk_epilogue<1>(c, st, nbc, p0, p1, w);
-        chunk_epilogue<2>(c, st, nbc, p0, p1, w);
-        chunk_epilogue<3>(c, st, nbc, p0, p1, w);
+        chunk_epilogue<0>(c, st, nbc, p, w);
+        chunk_epilogue<1>(c, st, nbc, p, w);
+        chunk_epilogue<2>(c, st, nbc, p, w);
+        chunk_epilogue<3>(c, st, nbc, p, w);
     }
-    // the next layer's input: the B operand image back into registers
+    // the pair's halves meet: the half-1 wave hands its mask nibbles over, then both read the
+    // next layer's operand image
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    if (c.half == 1) *reinterpret_cast<u2*>(c.mx + c.lane * 8) = u2{st.mw[0], st.mw[1]};
+    barrier();
+    if (c.half == 0) {
+        const u2 o = *reinterpret_cast<const u2*>(c.mx + c.lane * 8);
+        const unsigned off = st.row_ok ? (unsigned)(sample * 32 + 8 * g) : OOB;
+        if (!(NERF_DIAG & 1)) {
+            __builtin_amdgcn_raw_buffer_store_b64(u2{st.mw[0] | o.x, st.mw[1] | o.y}, st.rm, off, 0, 0);
+            count_vm(c, 1);
+        }
+    }
 #pragma unroll
     for (int kb = 0; kb < KBMAX; ++kb) {
         c.xh[kb] = *reinterpret_cast<const bf16x8*>(c.xo + kb * 2048 + c.lane * 16);
         c.xl[kb] = *reinterpret_cast<const bf16x8*>(c.xo + kb * 2048 + 1024 + c.lane * 16);
     }
-    // the layer's ReLU mask bits: lane (s, g) holds words 2g, 2g + 1 of row s (8 bytes)
-    {
-        const unsigned off = st.row_ok ? (unsigned)(sample * 32 + 8 * g) : OOB;
-        typedef unsigned u2 __attribute__((ext_vector_type(2)));
-        if (!(NERF_DIAG & 1)) {
-            __builtin_amdgcn_raw_buffer_store_b64(u2{st.mw[0], st.mw[1]}, st.rm, off, 0, 0);
-            count_vm(c, 1);
-        }
-    }
 }
 
 __global__ __launch_bounds__(WG, 1) void mlp_fused_fwd_kernel(FusedArgs a) {
-    __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT_BYTES + NWAVE * XO_BYTES + BIAS_LDS];
+    __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT_BYTES + NWAVE / 2 * (XO_BYTES + MX_BYTES) + BIAS_LDS];
     Ctx c;
     c.kargs = (kchar_t*)__builtin_amdgcn_kernarg_segment_ptr();
     c.smem = smem;
     c.img = a.img;
     c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    c.xo = smem + NSLOT * SLOT_BYTES + c.wave * XO_BYTES;
-    c.bias = smem + NSLOT * SLOT_BYTES + NWAVE * XO_BYTES;
+    c.half = c.wave & 1;
+    c.xo = smem + NSLOT * SLOT_BYTES + (c.wave >> 1) * XO_BYTES;
+    c.mx = smem + NSLOT * SLOT_BYTES + NWAVE / 2 * XO_BYTES + (c.wave >> 1) * MX_BYTES;
+    c.bias = smem + NSLOT * SLOT_BYTES + NWAVE / 2 * (XO_BYTES + MX_BYTES);
     c.bias_base = a.bias_base;
     c.lane = threadIdx.x & 63;
     c.M = a.M;
@@ -382,7 +372,7 @@ __global__ __launch_bounds__(WG, 1) void mlp_fused_fwd_kernel(FusedArgs a) {
     for (int l = 0; l < a.n_layers; ++l) per_tile += LF(int, nb, l);
     c.d_layer = 0;
     c.d_off = 0;
-    c.d_kb = LF(int, chunk_units, 0) / NWAVE;
+    c.d_units = LF(int, chunk_units, 0);
     c.d_left = LF(int, nb, 0);
     c.d_remaining = my_tiles * per_tile;
     c.cur = 0;
@@ -400,7 +390,7 @@ __global__ __launch_bounds__(WG, 1) void mlp_fused_fwd_kernel(FusedArgs a) {
         c.xl[kb] = bf16x8{};
     }
     for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
-        const int sample = tile * TILE + c.wave * SPW + (c.lane & 15);
+        const int sample = tile * TILE + (c.wave >> 1) * SPW + (c.lane & 15);
         for (int l = 0; l < a.n_layers; ++l) {
             switch (LF(int, type, l)) {
                 case 1: fused_layer<0, 1>(c, l, sample); break;
