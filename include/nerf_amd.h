@@ -286,6 +286,9 @@ int nerf_pack_weight_x3(const float* W, int32_t N, int32_t K_orig, const int32_t
  * segments (kbh blocks in all)]; type = 3*(kbr/4) + kbh with kbr in {0, 4, 8}, kbh in {0, 1, 2}.  out[m, n] for n < ldo
  * (columns >= N are written as 0), ReLU mask bits as NERF_EPI_MASKOUT (N <= 256), column
  * col_idx (a multiple of 32) additionally into col_out[m].  Buffers: byte extents < 2^31.
+ * The same launch runs the input-gradient chain of the backward (layers in reverse, images of
+ * W^T, no bias, mask_in instead of ReLU): each step's output is the previous layer's
+ * pre-activation gradient, kept in registers for the next step and stored for the weight gradients.
  * ------------------------------------------------------------------------- */
 #define NERF_FUSED_MAX_LAYERS 16
 typedef struct nerf_fused_layer {
@@ -308,6 +311,8 @@ typedef struct nerf_fused_layer {
     float* col_out;        /* [M] or NULL */
     int64_t img_off;       /* byte offset of the layer's first chunk in the image */
     int64_t bias_off;      /* byte offset of the layer's [nb][32] fp32 biases in the image */
+    const uint8_t* mask_in;/* NULL, or [M][32] ReLU bits (NERF_EPI_MASKOUT layout) multiplied into the
+                              output (the input-gradient chain: dL/dz_{l-1} = (dL/dz_l W_l) * (z_{l-1} > 0)) */
 } nerf_fused_layer;
 
 int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_layers, const void* image, int64_t M,

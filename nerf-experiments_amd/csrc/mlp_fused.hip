@@ -68,6 +68,7 @@ typedef __attribute__((address_space(4))) const char kchar_t;
 typedef float* fptr_t;
 typedef const float* cfptr_t;
 typedef uint8_t* u8ptr_t;
+typedef const uint8_t* cu8ptr_t;
 // layer fields are read from the kernel-argument segment by scalar loads (indexing the by-value
 // argument with a runtime layer index would make hipcc copy it to scratch)
 #define LF(T, f, l)                                                                                          \
@@ -173,6 +174,8 @@ struct LayerState {
     __amdgpu_buffer_rsrc_t ro, rm, rc;
     int bias_lds;         // LDS byte offset of the layer's biases (+128 per chunk; >= 128)
     unsigned mw[2];       // ReLU mask words 2g, 2g + 1 of this lane's sample row (this wave's nibbles)
+    bool mask_in;         // multiply the output by the ReLU bits min (input-gradient chain)
+    unsigned mi[8];       // this lane's sample row of those bits
 };
 
 // Epilogue of this wave's block of chunk nbc (output rows 32 nbc + 16 half .. +15, accumulator v):
@@ -188,6 +191,16 @@ __device__ __forceinline__ void chunk_epilogue(Ctx& c, LayerState& st, int nbc, 
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             v[r] = __builtin_bit_cast(float, max(__builtin_bit_cast(int, v[r] + b[r]), st.floor_i));
+        if (st.mask_in) {
+            // column 32 nbc + 16 half + 4 g + r: bit 4 half + g of byte (nbc & 3) of word 2 r + (nbc >> 2)
+            const int sh = 8 * (nbc & 3) + 4 * c.half + g;
+            const bool hi = nbc >= 4;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const unsigned word = hi ? st.mi[2 * r + 1] : st.mi[2 * r];
+                v[r] = ((word >> sh) & 1u) ? v[r] : 0.f;
+            }
+        }
         const int colok = nbc >= 0 ? (int)st.ldo : 0;
         const int col = 32 * nbc + 16 * c.half + 4 * g;
         const unsigned off = (unsigned)col < (unsigned)colok ? st.row_off + (unsigned)col * 4u : OOB;   // nbc = -1: col < 0
@@ -247,6 +260,21 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int sample) {
     st.col_idx = cptr != nullptr ? LF(int, col_idx, l) : -1;
     st.rc = __builtin_amdgcn_make_buffer_rsrc(cptr, 0, cptr ? c.M * 4 : 0, RSRC_W3);
     st.bias_lds = (int)LF(int64_t, bias_off, l) - c.bias_base + 128;
+    {
+        const uint8_t* mi = LF(cu8ptr_t, mask_in, l);
+        st.mask_in = mi != nullptr;
+        if (st.mask_in) {
+            const __amdgpu_buffer_rsrc_t rmi =
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(mi), 0, c.M * 32, RSRC_W3);
+            const unsigned off = st.row_ok ? (unsigned)(sample * 32) : OOB;
+            typedef unsigned u4 __attribute__((ext_vector_type(4)));
+            const u4 w0 = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rmi, off, 0, 0));
+            const u4 w1 = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rmi, off + 16, 0, 0));
+            st.mi[0] = w0.x; st.mi[1] = w0.y; st.mi[2] = w0.z; st.mi[3] = w0.w;
+            st.mi[4] = w1.x; st.mi[5] = w1.y; st.mi[6] = w1.z; st.mi[7] = w1.w;
+            count_vm(c, 2);
+        }
+    }
 
     // ---- HBM-fed input blocks (encodings): lane (s, g) of block kh holds columns 32 kh + 8 g .. +7
     bf16x8 hh[KBH > 0 ? KBH : 1], hl[KBH > 0 ? KBH : 1];

@@ -100,6 +100,7 @@ class NerfFusedLayer(ctypes.Structure):
         ("col_out", c_vp),
         ("img_off", c_i64),
         ("bias_off", c_i64),
+        ("mask_in", c_vp),
     ]
 
 

@@ -174,6 +174,7 @@ class MLPPlan:
         self.column_outputs = list(column_outputs)
         self.device = None
         self.fused = {}            # device -> mlp_fused.FusedForward
+        self.fused_dgrad = {}      # device -> mlp_fused.FusedInputGrad
         self.consumed = [False] * len(layers)
         for lp in layers:
             for s in lp.sources:
@@ -213,6 +214,7 @@ class MLPFunction(torch.autograd.Function):
         # outputs the caller never uses get None gradients instead of materialised zeros
         # (NerfModel with delayed density never reads z_last: a 268 MB memset + clone per step)
         ctx.set_materialize_grads(False)
+        ctx.fused_forward = False
         prec = matmul_precision()
         acts: list[torch.Tensor] = []
         masks: list[torch.Tensor | None] = []
@@ -231,6 +233,7 @@ class MLPFunction(torch.autograd.Function):
             col_t = {li: torch.empty(M, device=pos.device, dtype=torch.float32) for li, _ in plan.column_outputs}
             fused.run(M, pos, dirs, dir_rd, acts, masks, col_t)
             cols = tuple(col_t[li] for li, _ in plan.column_outputs)
+            ctx.fused_forward = True
         else:
             for idx, lp in enumerate(plan.layers):
                 lp.pack(prec)
@@ -310,6 +313,20 @@ class MLPFunction(torch.autograd.Function):
         ddir = None
         layer_grads: list[list[torch.Tensor]] = [[] for _ in range(L)]
 
+        # the input-gradient chain in one launch (csrc/mlp_fused.hip): every dY[l], l < L-1, from
+        # the head gradient through the stored ReLU bits, when nothing else feeds the backward
+        chain = (ctx.fused_forward and not need_pos and not need_dir and not plan.column_outputs
+                 and all(dY[i] is None for i in range(L - 1)) and dY[L - 1] is not None
+                 and mlp_fused.dgrad_eligible(plan, M))
+        if chain:
+            fd = plan.fused_dgrad.get(dev)
+            if fd is None:
+                fd = plan.fused_dgrad[dev] = mlp_fused.FusedInputGrad(plan, dev)
+            g_head = dY[L - 1]
+            for l in range(L - 1):
+                dY[l] = torch.empty(M, plan.layers[l].out_ld, device=dev, dtype=torch.float32)
+            fd.run(M, g_head, dY, ctx.masks)
+
         # one workspace sized for the largest weight-gradient launch
         ws_bytes = 0
         for lp in plan.layers:
@@ -360,6 +377,8 @@ class MLPFunction(torch.autograd.Function):
             K.linear_wgrad_reduce(M, N4, lp.Kp, lp.N, workspace, lp.col_map, gW, gb)
             layer_grads[li] = [gW, gb] + ([gs] if gs is not None else [])
             # ---- input gradients
+            if chain:
+                continue
             a_seg = [(dZ, lp.out_ld, 1)]
             for s, koff in zip(lp.sources, lp.koffs):
                 if s.kind == "act":

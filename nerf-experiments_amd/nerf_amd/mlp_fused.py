@@ -199,3 +199,149 @@ class FusedForward:
         if end is not None:
             end.record()
         _lib.check(st, "nerf_mlp_fused_fwd")
+
+
+# ---------------------------------------------------------------------------------------------
+# Input-gradient chain of the backward on the same kernel: steps l = L-1 .. 1, step l maps the
+# gradient w.r.t. layer l's output (dL/dz_l, B operand) through W_l^T to the gradient w.r.t. its
+# register-fed input, times the ReLU bits of layer l-1 (mask_in) = dL/dz_{l-1}.  The chain starts
+# from the head gradient in HBM; every step's output is stored for the weight gradients.
+# ---------------------------------------------------------------------------------------------
+def dgrad_eligible(plan, M: int) -> bool:
+    """NerfModel plans whose backward needs only the register-fed chain (no encoding gradients,
+    no column outputs, a single head output gradient): checked further by the caller."""
+    if not ENABLED or not eligible(plan, M) or plan.column_outputs:
+        return False
+    L = len(plan.layers)
+    for l in range(1, L):
+        lp = plan.layers[l]
+        act = lp.sources[0]
+        if act.kind != "act" or act.layer != l - 1 or act.k_valid not in (128, 256):
+            return False
+        if l < L - 1 and lp.N not in (128, 256):
+            return False
+        if l == L - 1 and lp.N > 32:
+            return False
+        if plan.layers[l - 1].relu and plan.layers[l - 1].N > 256:
+            return False
+    return True
+
+
+class FusedInputGrad:
+    """Packed W^T image + static step table of the input-gradient chain of one plan."""
+
+    runs = 0                      # launches so far (tests check the chain actually ran)
+
+    def __init__(self, plan, device):
+        self.plan = plan
+        self.device = device
+        L = len(plan.layers)
+        self.steps = []           # (layer l, kbr, kbh, n_out, nb, units, img_off, bias_off)
+        shapes = []
+        off = 0
+        for l in range(L - 1, 0, -1):
+            lp = plan.layers[l]
+            kbr, kbh = (0, 1) if l == L - 1 else (lp.N // 32, 0)
+            n_out = lp.sources[0].k_valid
+            nb = n_out // 32
+            units = 4 * (kbr + kbh)
+            shapes.append((l, kbr, kbh, n_out, nb, units, off))
+            off += nb * units * 1024
+        src_codes, dst_codes = [], []
+        for (l, kbr, kbh, n_out, nb, units, img_off) in shapes:
+            self.steps.append((l, kbr, kbh, n_out, nb, units, img_off, off))
+            s, d = self._maps(plan.layers[l], l, kbr, kbh, nb, units, img_off, off)
+            src_codes.append(s)
+            dst_codes.append(d)
+            off += nb * 128
+        self.image_bytes = off
+        self.image = torch.zeros(off // 2, dtype=torch.bfloat16, device=device)
+        self.map_src = torch.from_numpy(np.concatenate(src_codes).astype(np.int32)).to(device)
+        self.map_dst = torch.from_numpy(np.concatenate(dst_codes).astype(np.int32)).to(device)
+        self.version = None
+
+    @staticmethod
+    def _maps(lp, l, kbr, kbh, nb, units, off, bias_off):
+        """A fragment (row i = input feature k of layer l, column = its output n) = W_l[n][k];
+        n permuted like the previous step's accumulator layout when register-fed, natural when
+        it is the head gradient read from HBM; biases zero."""
+        N, K_orig = lp.module.out_features, lp.module.in_features
+        lane = np.arange(64)
+        srow, grp = lane & 15, lane >> 4
+        j = np.arange(8)
+        kb_total = kbr + kbh
+        nidx = np.full((kb_total, 64, 8), -1, dtype=np.int64)
+        for kb in range(kbr):
+            nidx[kb] = 32 * kb + 16 * (j[None, :] >> 2) + 4 * grp[:, None] + (j[None, :] & 3)
+        for kh in range(kbh):
+            local = 32 * kh + 8 * grp[:, None] + j[None, :]
+            nidx[kbr + kh] = np.where(local < N, local, -1)
+        k_valid = lp.sources[0].k_valid
+        srcs, dsts = [], []
+        for c in range(nb):
+            base = off + c * units * 1024
+            for bb in range(2):
+                k = 32 * c + 16 * bb + srow
+                kk = np.broadcast_to(k[None, :, None], nidx.shape)
+                valid = (nidx >= 0) & (nidx < N) & (kk < k_valid)
+                code = np.where(valid, ((2 * l) << 24) + nidx * K_orig + kk, -1)
+                dst = (base + np.arange(kb_total)[:, None, None] * 4096 + bb * 2048) // 2 + \
+                    lane[None, :, None] * 8 + j[None, None, :]
+                srcs.append(code.reshape(-1))
+                dsts.append(np.broadcast_to(dst, nidx.shape).reshape(-1))
+            srcs.append(np.full(32, -1))
+            dsts.append(~(bias_off // 4 + 32 * c + np.arange(32)))
+        return np.concatenate(srcs), np.concatenate(dsts)
+
+    def pack(self):
+        ps = []
+        for lp in self.plan.layers:
+            ps += [lp.module.weight, lp.module.bias]
+        ver = tuple((p._version, p.data_ptr()) for p in ps)
+        if ver == self.version:
+            return
+        arr = (ctypes.c_void_p * len(ps))(*[p.data_ptr() for p in ps])
+        st = _lib.load().nerf_fused_pack(arr, len(ps), self.map_src.data_ptr(), self.map_dst.data_ptr(),
+                                         self.map_src.numel(), self.image.data_ptr(), K._stream(self.device))
+        _lib.check(st, "nerf_fused_pack")
+        self.version = ver
+
+    def run(self, M: int, g_head: torch.Tensor, dY, masks):
+        """g_head: [M, ld] gradient of the last layer's output; fills dY[l] ([M, out_ld] fp32) for
+        l = L-2 .. 0 on the current stream."""
+        self.pack()
+        S = len(self.steps)
+        descs = (_lib.NerfFusedLayer * S)()
+        flops = 0.0
+        for i, (l, kbr, kbh, n_out, nb, units, img_off, bias_off) in enumerate(self.steps):
+            lp = self.plan.layers[l]
+            d = descs[i]
+            d.type = FUSED_TYPES[(kbr, kbh)]
+            d.N = n_out
+            d.nb = nb
+            d.relu = 0
+            d.nseg = 1 if kbh else 0
+            if kbh:
+                d.seg_kb[0] = 1
+                d.seg_k[0] = (lp.N + 3) // 4 * 4
+                d.seg_rd[0] = 1
+                d.seg_rows[0] = g_head.shape[0]
+                d.seg_ld[0] = g_head.stride(0)
+                d.seg_ptr[0] = g_head.data_ptr()
+            d.chunk_units = units
+            d.col_idx = -1
+            d.out = dY[l - 1].data_ptr()
+            d.ldo = dY[l - 1].stride(0)
+            d.mask = None
+            d.col_out = None
+            d.img_off = img_off
+            d.bias_off = bias_off
+            mk = masks[l - 1] if self.plan.layers[l - 1].relu else None
+            d.mask_in = mk.data_ptr() if mk is not None else None
+            flops += 2.0 * M * lp.module.out_features * n_out
+        end = K.TIMER.bracket("mlp_fused_dgrad", flops) if K.TIMER is not None else None
+        st = _lib.load().nerf_mlp_fused_fwd(descs, S, self.image.data_ptr(), M, K._stream(self.device))
+        if end is not None:
+            end.record()
+        _lib.check(st, "nerf_mlp_fused_fwd (input-gradient chain)")
+        FusedInputGrad.runs += 1
