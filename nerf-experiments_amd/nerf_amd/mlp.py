@@ -315,17 +315,27 @@ class MLPFunction(torch.autograd.Function):
 
         # the input-gradient chain in one launch (csrc/mlp_fused.hip): every dY[l], l < L-1, from
         # the head gradient through the stored ReLU bits, when nothing else feeds the backward
-        chain = (ctx.fused_forward and not need_pos and not need_dir and not plan.column_outputs
+        # (a column output's gradient joins the chain as one more k-block and is added to its
+        # layer's stored gradient below, as in the layer-by-layer path)
+        chain = (ctx.fused_forward and not need_pos and not need_dir
                  and all(dY[i] is None for i in range(L - 1)) and dY[L - 1] is not None
+                 and all(len(col_grads[li]) == 1 for li, _ in plan.column_outputs)
                  and mlp_fused.dgrad_eligible(plan, M))
         if chain:
             fd = plan.fused_dgrad.get(dev)
             if fd is None:
                 fd = plan.fused_dgrad[dev] = mlp_fused.FusedInputGrad(plan, dev)
             g_head = dY[L - 1]
+            g_cols = {}
+            for li, _ in plan.column_outputs:
+                g4 = torch.zeros(M, 4, device=dev, dtype=torch.float32)
+                g4[:, 0] = col_grads[li][0][1].reshape(-1)
+                g_cols[li] = g4
             for l in range(L - 1):
                 dY[l] = torch.empty(M, plan.layers[l].out_ld, device=dev, dtype=torch.float32)
-            fd.run(M, g_head, dY, ctx.masks)
+                if plan.layers[l].out_ld > 256 and plan.layers[l].N > 256:
+                    dY[l][:, 256:].zero_()    # the chain fills the register-fed 256 columns
+            fd.run(M, g_head, dY, ctx.masks, g_cols)
 
         # one workspace sized for the largest weight-gradient launch
         ws_bytes = 0

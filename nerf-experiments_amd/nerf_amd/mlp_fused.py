@@ -208,17 +208,23 @@ class FusedForward:
 # from the head gradient in HBM; every step's output is stored for the weight gradients.
 # ---------------------------------------------------------------------------------------------
 def dgrad_eligible(plan, M: int) -> bool:
-    """NerfModel plans whose backward needs only the register-fed chain (no encoding gradients,
-    no column outputs, a single head output gradient): checked further by the caller."""
-    if not ENABLED or not eligible(plan, M) or plan.column_outputs:
+    """NerfModel plans whose backward needs only the register-fed chain (no encoding gradients;
+    the caller checks that and which outputs carry gradients).  A column output is allowed on a
+    257-wide layer at column 256 (the density of NerfModel without delayed density): its gradient
+    enters the chain as one HBM-fed k-block."""
+    if not ENABLED or not eligible(plan, M):
         return False
+    cols = dict(plan.column_outputs)
     L = len(plan.layers)
+    for li, c in cols.items():
+        if plan.layers[li].N != 257 or c != 256 or li == L - 1 or plan.layers[li].relu:
+            return False
     for l in range(1, L):
         lp = plan.layers[l]
         act = lp.sources[0]
         if act.kind != "act" or act.layer != l - 1 or act.k_valid not in (128, 256):
             return False
-        if l < L - 1 and lp.N not in (128, 256):
+        if l < L - 1 and not (lp.N in (128, 256) or (l in cols and lp.N == 257)):
             return False
         if l == L - 1 and lp.N > 32:
             return False
@@ -239,9 +245,11 @@ class FusedInputGrad:
         self.steps = []           # (layer l, kbr, kbh, n_out, nb, units, img_off, bias_off)
         shapes = []
         off = 0
+        cols = dict(plan.column_outputs)
         for l in range(L - 1, 0, -1):
             lp = plan.layers[l]
-            kbr, kbh = (0, 1) if l == L - 1 else (lp.N // 32, 0)
+            # the head gradient, or a column output's gradient, enters as an HBM-fed k-block
+            kbr, kbh = (0, 1) if l == L - 1 else (lp.N // 32, 1 if l in cols else 0)
             n_out = lp.sources[0].k_valid
             nb = n_out // 32
             units = 4 * (kbr + kbh)
@@ -274,7 +282,8 @@ class FusedInputGrad:
         for kb in range(kbr):
             nidx[kb] = 32 * kb + 16 * (j[None, :] >> 2) + 4 * grp[:, None] + (j[None, :] & 3)
         for kh in range(kbh):
-            local = 32 * kh + 8 * grp[:, None] + j[None, :]
+            # HBM-fed gradient columns follow the register-fed ones (natural order)
+            local = 32 * kbr + 32 * kh + 8 * grp[:, None] + j[None, :]
             nidx[kbr + kh] = np.where(local < N, local, -1)
         k_valid = lp.sources[0].k_valid
         srcs, dsts = [], []
@@ -306,9 +315,11 @@ class FusedInputGrad:
         _lib.check(st, "nerf_fused_pack")
         self.version = ver
 
-    def run(self, M: int, g_head: torch.Tensor, dY, masks):
-        """g_head: [M, ld] gradient of the last layer's output; fills dY[l] ([M, out_ld] fp32) for
-        l = L-2 .. 0 on the current stream."""
+    def run(self, M: int, g_head: torch.Tensor, dY, masks, g_cols=None):
+        """g_head: [M, ld] gradient of the last layer's output; g_cols: {layer: [M, 4] buffer whose
+        column 0 is the gradient of the layer's column output}; fills dY[l] ([M, out_ld] fp32,
+        the columns of the register-fed chain) for l = L-2 .. 0 on the current stream."""
+        g_cols = g_cols or {}
         self.pack()
         S = len(self.steps)
         descs = (_lib.NerfFusedLayer * S)()
@@ -322,12 +333,13 @@ class FusedInputGrad:
             d.relu = 0
             d.nseg = 1 if kbh else 0
             if kbh:
+                src = g_head if kbr == 0 else g_cols[l]
                 d.seg_kb[0] = 1
-                d.seg_k[0] = (lp.N + 3) // 4 * 4
+                d.seg_k[0] = (lp.N + 3) // 4 * 4 if kbr == 0 else 4
                 d.seg_rd[0] = 1
-                d.seg_rows[0] = g_head.shape[0]
-                d.seg_ld[0] = g_head.stride(0)
-                d.seg_ptr[0] = g_head.data_ptr()
+                d.seg_rows[0] = src.shape[0]
+                d.seg_ld[0] = src.stride(0)
+                d.seg_ptr[0] = src.data_ptr()
             d.chunk_units = units
             d.col_idx = -1
             d.out = dY[l - 1].data_ptr()

@@ -188,3 +188,53 @@ def test_fused_input_gradient_chain_matches_layerwise(M, rd):
         e_layer = (grads[False][n] - r).abs().max().item() / scale
         e_fused = (grads[True][n] - r).abs().max().item() / scale
         assert e_fused <= 1.25 * e_layer + 1e-3 and e_fused < 2e-2, (n, e_fused, e_layer)
+
+
+def test_fused_input_gradient_chain_density_column():
+    """mip / barf-shaped NerfModel without delayed density: the density column's gradient joins
+    the chain as an HBM-fed k-block; parameter gradients against the layer-by-layer backward and
+    fp64 (tolerance as above)."""
+    from nerf_amd import mlp_fused
+    from nerf_amd.mlp import MLPFunction
+    M, rd = 4096 * 16 + 3, 1
+    g = torch.Generator(device=DEV).manual_seed(9)
+    pos_pe = torch.zeros(M, 64, device=DEV)
+    pos_pe[:, :63] = torch.rand(M, 63, device=DEV, generator=g) * 2 - 1
+    dir_pe = torch.zeros(M, 32, device=DEV)
+    dir_pe[:, :27] = torch.rand(M, 27, device=DEV, generator=g) * 2 - 1
+    w_rgb = torch.randn(M, 3, device=DEV, generator=g)
+    w_sig = torch.randn(M, device=DEV, generator=g)
+    grads = {}
+    for fused in (False, True):
+        model = _model("barf").to(DEV)
+        plan = model._get_plan()
+        saved = mlp_fused.ENABLED
+        mlp_fused.ENABLED = fused
+        runs = mlp_fused.FusedInputGrad.runs
+        try:
+            outs = MLPFunction.apply(plan, M, pos_pe, dir_pe, rd, *plan.params())
+            ((outs[1][:, :3] * w_rgb).sum() + (outs[2] * w_sig).sum()).backward()
+            torch.cuda.synchronize()
+        finally:
+            mlp_fused.ENABLED = saved
+        assert (mlp_fused.FusedInputGrad.runs > runs) == fused
+        grads[fused] = {n: p.grad.detach().double() for n, p in model.named_parameters()}
+    # fp64 reference
+    model = _model("barf").to(DEV).double()
+    plan = model._get_plan()
+    acts = []
+    for lp in plan.layers:
+        parts = []
+        for s in lp.sources:
+            src = acts[s.layer] if s.kind == "act" else (pos_pe.double() if s.kind == "pos" else dir_pe.double())
+            parts.append(src[:, :s.k_valid])
+        y = torch.nn.functional.linear(torch.cat(parts, 1), lp.module.weight, lp.module.bias)
+        acts.append(torch.relu(y) if lp.relu else y)
+    z_last, head = plan.outputs
+    ((acts[head][:, :3] * w_rgb.double()).sum() + (acts[z_last][:, 256] * w_sig.double()).sum()).backward()
+    for n, p in model.named_parameters():
+        r = p.grad.detach()
+        scale = max(r.abs().max().item(), 1e-12)
+        e_layer = (grads[False][n] - r).abs().max().item() / scale
+        e_fused = (grads[True][n] - r).abs().max().item() / scale
+        assert e_fused <= 1.25 * e_layer + 1e-3 and e_fused < 2e-2, (n, e_fused, e_layer)
