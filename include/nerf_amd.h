@@ -294,7 +294,7 @@ int nerf_pack_weight_x3(const float* W, int32_t N, int32_t K_orig, const int32_t
 typedef struct nerf_fused_layer {
     int32_t type;          /* 3*(kbr/4) + kbh */
     int32_t N;             /* output columns */
-    int32_t nb;            /* ceil(N / 32), <= 9 (blocks >= 8 are written, never fed forward) */
+    int32_t nb;            /* ceil(N / 32), <= 16 (chunks >= 8 are written, never fed forward) */
     int32_t relu;
     int32_t nseg;          /* HBM segments, 0..2 */
     int32_t seg_kb[2];     /* 32-column blocks of each segment (sum = kbh) */
@@ -313,6 +313,11 @@ typedef struct nerf_fused_layer {
     int64_t bias_off;      /* byte offset of the layer's [nb][32] fp32 biases in the image */
     const uint8_t* mask_in;/* NULL, or [M][32] ReLU bits (NERF_EPI_MASKOUT layout) multiplied into the
                               output (the input-gradient chain: dL/dz_{l-1} = (dL/dz_l W_l) * (z_{l-1} > 0)) */
+    float* out2;           /* chunks >= n1 (input-gradient chain: the rows of an encoding input) go to
+                              out2[m, 32 (chunk - n1) + ...] (row stride ldo2), unmasked, not fed forward */
+    int64_t ldo2;
+    int32_t n1;            /* chunks written to out (= nb when out2 is unused) */
+    int32_t pad1;
 } nerf_fused_layer;
 
 int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_layers, const void* image, int64_t M,

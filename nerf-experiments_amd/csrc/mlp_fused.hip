@@ -174,6 +174,10 @@ struct LayerState {
     __amdgpu_buffer_rsrc_t ro, rm, rc;
     int bias_lds;         // LDS byte offset of the layer's biases (+128 per chunk; >= 128)
     unsigned mw[2];       // ReLU mask words 2g, 2g + 1 of this lane's sample row (this wave's nibbles)
+    int n1;               // chunks routed to out (fed forward, masked); the rest go to out2
+    unsigned row_off2;    // byte offset of this lane's sample row in out2 (OOB past M)
+    int64_t ldo2;
+    __amdgpu_buffer_rsrc_t ro2;
     bool mask_in;         // multiply the output by the ReLU bits min (input-gradient chain)
     unsigned mi[8];       // this lane's sample row of those bits
 };
@@ -191,7 +195,8 @@ __device__ __forceinline__ void chunk_epilogue(Ctx& c, LayerState& st, int nbc, 
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             v[r] = __builtin_bit_cast(float, max(__builtin_bit_cast(int, v[r] + b[r]), st.floor_i));
-        if (st.mask_in) {
+        const bool sec = nbc >= st.n1;               // an encoding input's rows (chain: out2)
+        if (st.mask_in && !sec) {
             // column 32 nbc + 16 half + 4 g + r: bit 4 half + g of byte (nbc & 3) of word 2 r + (nbc >> 2)
             const int sh = 8 * (nbc & 3) + 4 * c.half + g;
             const bool hi = nbc >= 4;
@@ -201,12 +206,13 @@ __device__ __forceinline__ void chunk_epilogue(Ctx& c, LayerState& st, int nbc, 
                 v[r] = ((word >> sh) & 1u) ? v[r] : 0.f;
             }
         }
-        const int colok = nbc >= 0 ? (int)st.ldo : 0;
-        const int col = 32 * nbc + 16 * c.half + 4 * g;
-        const unsigned off = (unsigned)col < (unsigned)colok ? st.row_off + (unsigned)col * 4u : OOB;   // nbc = -1: col < 0
+        const int colok = nbc >= 0 ? (int)(sec ? st.ldo2 : st.ldo) : 0;
+        const int col = 32 * (sec ? nbc - st.n1 : nbc) + 16 * c.half + 4 * g;
+        const unsigned off = (unsigned)col < (unsigned)colok ? (sec ? st.row_off2 : st.row_off) + (unsigned)col * 4u
+                                                             : OOB;   // nbc = -1: col < 0
         const unsigned coff = (c.half == 0 && g == 0 && st.col_idx == 32 * nbc) ? st.sample_off : OOB;
         if (!(NERF_DIAG & 1)) {
-            __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(v, sec ? st.ro2 : st.ro, off, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), st.rc, coff, 0, 0);
             count_vm(c, 2);
         }
@@ -230,7 +236,7 @@ __device__ __forceinline__ void chunk_epilogue(Ctx& c, LayerState& st, int nbc, 
         typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
         const bf16x4 h = __builtin_convertvector(v, bf16x4);
         const bf16x4 lo = __builtin_convertvector(v - __builtin_convertvector(h, f4), bf16x4);
-        if (nbc >= 0 && nbc < KBMAX) {
+        if (nbc >= 0 && nbc < KBMAX && nbc < st.n1) {
             *reinterpret_cast<bf16x4*>(c.xo + nbc * 2048 + c.lane * 16 + 8 * c.half) = h;
             *reinterpret_cast<bf16x4*>(c.xo + nbc * 2048 + 1024 + c.lane * 16 + 8 * c.half) = lo;
         }
@@ -260,6 +266,13 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int sample) {
     st.col_idx = cptr != nullptr ? LF(int, col_idx, l) : -1;
     st.rc = __builtin_amdgcn_make_buffer_rsrc(cptr, 0, cptr ? c.M * 4 : 0, RSRC_W3);
     st.bias_lds = (int)LF(int64_t, bias_off, l) - c.bias_base + 128;
+    {
+        float* o2 = LF(fptr_t, out2, l);
+        st.n1 = o2 != nullptr ? LF(int, n1, l) : st.NB;
+        st.ldo2 = o2 != nullptr ? LF(int64_t, ldo2, l) : 0;
+        st.ro2 = __builtin_amdgcn_make_buffer_rsrc(o2, 0, o2 ? (int)((int64_t)c.M * st.ldo2 * 4) : 0, RSRC_W3);
+        st.row_off2 = st.row_ok ? (unsigned)((int64_t)sample * st.ldo2 * 4) : OOB;
+    }
     {
         const uint8_t* mi = LF(cu8ptr_t, mask_in, l);
         st.mask_in = mi != nullptr;
@@ -488,14 +501,18 @@ extern "C" int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_laye
         const int kbr = (L.type / 3) * 4, kbh = L.type % 3;
         NERF_REQUIRE(L.type == 1 || L.type == 2 || L.type == 3 || L.type == 6 || L.type == 7 || L.type == 8);
         NERF_REQUIRE((l == 0) == (kbr == 0));                  // only the first layer has no register input
-        NERF_REQUIRE(L.N >= 1 && L.nb == (L.N + 31) / 32 && L.nb <= 9);
+        NERF_REQUIRE(L.N >= 1 && L.nb == (L.N + 31) / 32 && L.nb <= 16);
         NERF_REQUIRE(L.chunk_units == 4 * (kbr + kbh));
         NERF_REQUIRE(L.bias_off >= 0 && L.bias_off % 16 == 0);
-        NERF_REQUIRE(L.out != nullptr && aligned16(L.out) && L.ldo >= L.N && L.ldo % 4 == 0);
+        // with a second output only the first n1 chunks land in out (columns past ldo are dropped)
+        NERF_REQUIRE(L.out != nullptr && aligned16(L.out) && L.ldo % 4 == 0 &&
+                     L.ldo >= (L.out2 != nullptr ? (32 * L.n1 < L.N ? 32 * L.n1 : L.N) : L.N));
         NERF_REQUIRE(M * L.ldo * 4 < ((int64_t)1 << 31));
         NERF_REQUIRE(L.mask == nullptr || (L.N <= 256 && M * 32 < ((int64_t)1 << 31)));
         NERF_REQUIRE(L.col_out == nullptr || (L.col_idx >= 0 && L.col_idx % 32 == 0 && L.col_idx < L.N));
         NERF_REQUIRE(L.img_off >= 0 && L.img_off % 1024 == 0);
+        NERF_REQUIRE(L.out2 == nullptr || (aligned16(L.out2) && L.ldo2 % 4 == 0 && L.ldo2 > 0 && L.n1 >= 0 &&
+                                           L.n1 <= L.nb && M * L.ldo2 * 4 < ((int64_t)1 << 31)));
         NERF_REQUIRE(L.nseg >= 0 && L.nseg <= 2);
         int kbs = 0;
         for (int s = 0; s < L.nseg; ++s) {
@@ -508,7 +525,8 @@ extern "C" int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_laye
         NERF_REQUIRE(kbs == kbh);
         if (l > 0) {
             const nerf_fused_layer& P = layers[l - 1];
-            NERF_REQUIRE(kbr <= (P.nb < 8 ? P.nb : 8));  // fed blocks exist in the previous output
+            const int pn = P.out2 != nullptr ? P.n1 : P.nb;
+            NERF_REQUIRE(kbr <= (pn < 8 ? pn : 8));      // fed blocks exist in the previous output
         }
         a.L[l] = L;
         if (L.nseg < 2) {

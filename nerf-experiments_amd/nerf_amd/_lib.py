@@ -101,6 +101,10 @@ class NerfFusedLayer(ctypes.Structure):
         ("img_off", c_i64),
         ("bias_off", c_i64),
         ("mask_in", c_vp),
+        ("out2", c_vp),
+        ("ldo2", c_i64),
+        ("n1", c_i32),
+        ("pad1", c_i32),
     ]
 
 

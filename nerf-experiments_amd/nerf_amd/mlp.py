@@ -317,14 +317,16 @@ class MLPFunction(torch.autograd.Function):
         # the head gradient through the stored ReLU bits, when nothing else feeds the backward
         # (a column output's gradient joins the chain as one more k-block and is added to its
         # layer's stored gradient below, as in the layer-by-layer path)
-        chain = (ctx.fused_forward and not need_pos and not need_dir
+        chain = (ctx.fused_forward
                  and all(dY[i] is None for i in range(L - 1)) and dY[L - 1] is not None
                  and all(len(col_grads[li]) == 1 for li, _ in plan.column_outputs)
-                 and mlp_fused.dgrad_eligible(plan, M))
+                 and mlp_fused.dgrad_eligible(plan, M)
+                 and mlp_fused.FusedInputGrad.layout(plan, need_pos, need_dir) is not None)
         if chain:
-            fd = plan.fused_dgrad.get(dev)
+            key = (dev, bool(need_pos), bool(need_dir))
+            fd = plan.fused_dgrad.get(key)
             if fd is None:
-                fd = plan.fused_dgrad[dev] = mlp_fused.FusedInputGrad(plan, dev)
+                fd = plan.fused_dgrad[key] = mlp_fused.FusedInputGrad(plan, dev, need_pos, need_dir)
             g_head = dY[L - 1]
             g_cols = {}
             for li, _ in plan.column_outputs:
@@ -335,7 +337,19 @@ class MLPFunction(torch.autograd.Function):
                 dY[l] = torch.empty(M, plan.layers[l].out_ld, device=dev, dtype=torch.float32)
                 if plan.layers[l].out_ld > 256 and plan.layers[l].N > 256:
                     dY[l][:, 256:].zero_()    # the chain fills the register-fed 256 columns
-            fd.run(M, g_head, dY, ctx.masks, g_cols)
+            # encoding-input gradients (pose refinement): one buffer per step that produces them
+            x_out = {}
+            for (l, _, _, _, x, *_rest) in fd.steps:
+                if x is not None:
+                    x_out[l] = torch.empty(M, x.k_pad, device=dev, dtype=torch.float32)
+            fd.run(M, g_head, dY, ctx.masks, g_cols, x_out)
+            for (l, _, _, _, x, *_rest) in fd.steps:
+                if x is None:
+                    continue
+                if x.kind == "pos":
+                    dpos = x_out[l] if dpos is None else dpos.add_(x_out[l])
+                else:
+                    ddir = x_out[l] if ddir is None else ddir.add_(x_out[l])
 
         # one workspace sized for the largest weight-gradient launch
         ws_bytes = 0

@@ -238,27 +238,48 @@ class FusedInputGrad:
 
     runs = 0                      # launches so far (tests check the chain actually ran)
 
-    def __init__(self, plan, device):
-        self.plan = plan
-        self.device = device
+    @staticmethod
+    def layout(plan, need_pos: bool, need_dir: bool):
+        """Steps (layer l, kbr, kbh, n1 chained chunks, extra source or None) of the chain, or None
+        if the plan needs encoding gradients the kernel cannot route (at most one encoding input
+        per layer may need its gradient, written to the step's second output)."""
         L = len(plan.layers)
-        self.steps = []           # (layer l, kbr, kbh, n_out, nb, units, img_off, bias_off)
-        shapes = []
-        off = 0
         cols = dict(plan.column_outputs)
+
+        def extra(lp):
+            xs = [s for s in lp.sources[1:] if (s.kind == "pos" and need_pos) or (s.kind == "dir" and need_dir)]
+            return xs
+        steps = []
         for l in range(L - 1, 0, -1):
             lp = plan.layers[l]
-            # the head gradient, or a column output's gradient, enters as an HBM-fed k-block
             kbr, kbh = (0, 1) if l == L - 1 else (lp.N // 32, 1 if l in cols else 0)
-            n_out = lp.sources[0].k_valid
-            nb = n_out // 32
+            xs = extra(lp)
+            if len(xs) > 1:
+                return None
+            steps.append((l, kbr, kbh, lp.sources[0].k_valid // 32, xs[0] if xs else None))
+        lp0 = plan.layers[0]
+        xs = [s for s in lp0.sources if (s.kind == "pos" and need_pos) or (s.kind == "dir" and need_dir)]
+        if len(xs) > 1 or (xs and lp0.N not in (128, 256)):
+            return None
+        if xs:
+            steps.append((0, lp0.N // 32, 0, 0, xs[0]))
+        return steps
+
+    def __init__(self, plan, device, need_pos: bool = False, need_dir: bool = False):
+        self.plan = plan
+        self.device = device
+        self.steps = []           # (l, kbr, kbh, n1, extra, n_out, nb, units, img_off, bias_off)
+        shapes = []
+        off = 0
+        for (l, kbr, kbh, n1, x) in self.layout(plan, need_pos, need_dir):
+            nb = n1 + (x.k_pad // 32 if x is not None else 0)
             units = 4 * (kbr + kbh)
-            shapes.append((l, kbr, kbh, n_out, nb, units, off))
+            shapes.append((l, kbr, kbh, n1, x, nb, units, off))
             off += nb * units * 1024
         src_codes, dst_codes = [], []
-        for (l, kbr, kbh, n_out, nb, units, img_off) in shapes:
-            self.steps.append((l, kbr, kbh, n_out, nb, units, img_off, off))
-            s, d = self._maps(plan.layers[l], l, kbr, kbh, nb, units, img_off, off)
+        for (l, kbr, kbh, n1, x, nb, units, img_off) in shapes:
+            self.steps.append((l, kbr, kbh, n1, x, 32 * nb, nb, units, img_off, off))
+            s, d = self._maps(plan.layers[l], l, kbr, kbh, n1, x, nb, units, img_off, off)
             src_codes.append(s)
             dst_codes.append(d)
             off += nb * 128
@@ -269,10 +290,11 @@ class FusedInputGrad:
         self.version = None
 
     @staticmethod
-    def _maps(lp, l, kbr, kbh, nb, units, off, bias_off):
+    def _maps(lp, l, kbr, kbh, n1, x, nb, units, off, bias_off):
         """A fragment (row i = input feature k of layer l, column = its output n) = W_l[n][k];
         n permuted like the previous step's accumulator layout when register-fed, natural when
-        it is the head gradient read from HBM; biases zero."""
+        it is an HBM-fed gradient (head output, density column); rows of chunks >= n1 are the
+        columns of the encoding input x; biases zero."""
         N, K_orig = lp.module.out_features, lp.module.in_features
         lane = np.arange(64)
         srow, grp = lane & 15, lane >> 4
@@ -285,14 +307,24 @@ class FusedInputGrad:
             # HBM-fed gradient columns follow the register-fed ones (natural order)
             local = 32 * kbr + 32 * kh + 8 * grp[:, None] + j[None, :]
             nidx[kbr + kh] = np.where(local < N, local, -1)
-        k_valid = lp.sources[0].k_valid
+        orig = {}
+        o = 0
+        for s_ in lp.sources:
+            orig[id(s_)] = o
+            o += s_.k_valid
+        act_valid = lp.sources[0].k_valid if lp.sources[0].kind == "act" else 0
         srcs, dsts = [], []
         for c in range(nb):
             base = off + c * units * 1024
             for bb in range(2):
-                k = 32 * c + 16 * bb + srow
-                kk = np.broadcast_to(k[None, :, None], nidx.shape)
-                valid = (nidx >= 0) & (nidx < N) & (kk < k_valid)
+                if c < n1:
+                    k = 32 * c + 16 * bb + srow
+                    kcol = np.where(k < act_valid, k, -1)
+                else:
+                    local = 32 * (c - n1) + 16 * bb + srow
+                    kcol = np.where(local < x.k_valid, orig[id(x)] + local, -1)
+                kk = np.broadcast_to(kcol[None, :, None], nidx.shape)
+                valid = (nidx >= 0) & (nidx < N) & (kk >= 0)
                 code = np.where(valid, ((2 * l) << 24) + nidx * K_orig + kk, -1)
                 dst = (base + np.arange(kb_total)[:, None, None] * 4096 + bb * 2048) // 2 + \
                     lane[None, :, None] * 8 + j[None, None, :]
@@ -315,16 +347,18 @@ class FusedInputGrad:
         _lib.check(st, "nerf_fused_pack")
         self.version = ver
 
-    def run(self, M: int, g_head: torch.Tensor, dY, masks, g_cols=None):
+    def run(self, M: int, g_head: torch.Tensor, dY, masks, g_cols=None, x_out=None):
         """g_head: [M, ld] gradient of the last layer's output; g_cols: {layer: [M, 4] buffer whose
-        column 0 is the gradient of the layer's column output}; fills dY[l] ([M, out_ld] fp32,
-        the columns of the register-fed chain) for l = L-2 .. 0 on the current stream."""
+        column 0 is the gradient of the layer's column output}; x_out: {layer: [M, k_pad] buffer for
+        the gradient of the layer's encoding input}.  Fills dY[l] ([M, out_ld] fp32, the columns of
+        the register-fed chain) for l = L-2 .. 0 on the current stream."""
         g_cols = g_cols or {}
+        x_out = x_out or {}
         self.pack()
         S = len(self.steps)
         descs = (_lib.NerfFusedLayer * S)()
         flops = 0.0
-        for i, (l, kbr, kbh, n_out, nb, units, img_off, bias_off) in enumerate(self.steps):
+        for i, (l, kbr, kbh, n1, x, n_out, nb, units, img_off, bias_off) in enumerate(self.steps):
             lp = self.plan.layers[l]
             d = descs[i]
             d.type = FUSED_TYPES[(kbr, kbh)]
@@ -342,14 +376,23 @@ class FusedInputGrad:
                 d.seg_ptr[0] = src.data_ptr()
             d.chunk_units = units
             d.col_idx = -1
-            d.out = dY[l - 1].data_ptr()
-            d.ldo = dY[l - 1].stride(0)
+            if l >= 1:
+                d.out = dY[l - 1].data_ptr()
+                d.ldo = dY[l - 1].stride(0)
+                mk = masks[l - 1] if self.plan.layers[l - 1].relu else None
+                d.mask_in = mk.data_ptr() if mk is not None else None
+            else:                                      # the last step only produces encoding gradients
+                d.out = x_out[l].data_ptr()
+                d.ldo = x_out[l].stride(0)
+                d.mask_in = None
             d.mask = None
             d.col_out = None
+            if x is not None:
+                d.out2 = x_out[l].data_ptr()
+                d.ldo2 = x_out[l].stride(0)
+                d.n1 = n1
             d.img_off = img_off
             d.bias_off = bias_off
-            mk = masks[l - 1] if self.plan.layers[l - 1].relu else None
-            d.mask_in = mk.data_ptr() if mk is not None else None
             flops += 2.0 * M * lp.module.out_features * n_out
         end = K.TIMER.bracket("mlp_fused_dgrad", flops) if K.TIMER is not None else None
         st = _lib.load().nerf_mlp_fused_fwd(descs, S, self.image.data_ptr(), M, K._stream(self.device))
