@@ -226,7 +226,8 @@ class MLPFunction(torch.autograd.Function):
             if fused is None:
                 fused = plan.fused[pos.device] = mlp_fused.FusedForward(plan, pos.device)
             for idx, lp in enumerate(plan.layers):
-                lp.pack(prec, forward=False)  # only the input-gradient GEMMs' layouts (Wt / Wtx)
+                # no packing here: the backward packs the input-gradient layouts (Wt / Wtx) only
+                # if it runs the layer-by-layer GEMMs instead of the fused chain
                 acts.append(torch.empty(M, lp.out_ld, device=pos.device, dtype=torch.float32))
                 masks.append(torch.empty(M, 32, device=pos.device, dtype=torch.uint8)
                              if lp.relu and plan.consumed[idx] and lp.N <= 256 else None)
@@ -403,6 +404,7 @@ class MLPFunction(torch.autograd.Function):
             # ---- input gradients
             if chain:
                 continue
+            lp.pack(ctx.prec, forward=False)
             a_seg = [(dZ, lp.out_ld, 1)]
             for s, koff in zip(lp.sources, lp.koffs):
                 if s.kind == "act":
