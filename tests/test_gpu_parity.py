@@ -339,7 +339,11 @@ def _split_bf16(W):
 @pytest.mark.parametrize("M,N,ks,rd", [(1000, 256, (256, 64), (1, 1)), (777, 257, (256,), (1,)),
                                        (4096, 128, (256, 32), (1, 64)), (300, 4, (128,), (1,)),
                                        (129, 300, (32, 32, 64), (1, 3, 1)), (1000, 128, (4,), (1,)),
-                                       (333, 20, (260, 12), (1, 7)), (70000, 256, (256,), (1,))])
+                                       (333, 20, (260, 12), (1, 7)), (70000, 256, (256,), (1,)),
+                                       # one 256 x 256 weight-gradient tile (LDS-DMA kernel): ragged
+                                       # splits, per-ray rows, fewer chunks than ring slots
+                                       (5003, 256, (200, 24), (1, 7)), (777, 200, (128, 60), (1, 3)),
+                                       (50, 256, (256,), (1,)), (10, 160, (64,), (1,))])
 def test_linear_x3_fwd_wgrad(M, N, ks, rd):
     """3 x bf16 split-precision GEMMs (hi*hi + hi*lo + lo*hi, fp32 accumulate).
 
