@@ -117,7 +117,7 @@ def build_workload(name: str, device, rank: int):
 
         def loss_fn():
             return ren.training_loss(o, d, pw, target)[0]
-        return ren, [ren], opt, loss_fn
+        return ren, [ren], opt, loss_fn, lambda: ren(o, d, pw)
     if name == "mip":
         torch.manual_seed(0)
         pos = IntegratedBarfFourierFeatures(10, 10, 1.28, 6.4, True, 1.0, True)
@@ -131,7 +131,7 @@ def build_workload(name: str, device, rank: int):
 
         def loss_fn():
             return ren.training_loss(o, d, pw, target)[0]
-        return ren, [ren], opt, loss_fn
+        return ren, [ren], opt, loss_fn, lambda: ren(o, d, pw)
     if name == "barf":
         torch.manual_seed(0)
         pos = BarfPositionalEncoding(10, 10.0, 0, 1, True, 1.0)
@@ -150,7 +150,11 @@ def build_workload(name: str, device, rank: int):
         def loss_fn():
             o2, d2, _, _ = extr(img, o, d)
             return ren.training_loss(o2, d2, pw, target)[0]
-        return ren, [ren, extr], opt, loss_fn
+
+        def render_fn():
+            o2, d2, _, _ = extr(img, o, d)
+            return ren(o2, d2, pw)
+        return ren, [ren, extr], opt, loss_fn, render_fn
     raise ValueError(name)
 
 
@@ -216,6 +220,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="n2v", choices=tuple(WORKLOADS))
+    ap.add_argument("--mode", default="train", choices=("train", "render"),
+                    help="train: forward + backward + all-reduce + Adam per step (the headline metric); "
+                         "render: the forward pass only, without autograd (BASELINE.json's render metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--matmul-precision", default="high", choices=("highest", "high", "medium"),
@@ -242,11 +249,16 @@ def main():
     nerf_amd._lib.load()
 
     wl = WORKLOADS[args.workload]
-    ren, modules, opt, loss_fn = build_workload(args.workload, device, rank)
+    ren, modules, opt, loss_fn, render_fn = build_workload(args.workload, device, rank)
     allreduce = GradAllReduce([p for m in modules for p in m.parameters()])
     torch.manual_seed(1234 + rank)
+    render = args.mode == "render"
 
     def step():
+        if render:
+            with torch.no_grad():
+                rgb, _ = render_fn()
+            return rgb.mean()
         opt.zero_grad(set_to_none=True)
         loss = loss_fn()
         loss.backward()
@@ -317,7 +329,8 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": "ray-samples/sec (coarse+fine), training step",
+            "metric": ("ray-samples/sec (coarse+fine), render (forward only)" if render
+                       else "ray-samples/sec (coarse+fine), training step"),
             "value": value,
             "unit": "ray-samples/s",
             "n_gpus": world,
@@ -352,10 +365,11 @@ def main():
                             "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["ms"] > 0 else 0.0,
                             "gbs": (v["bytes"] / (v["ms"] * 1e-3) / 1e9) if v["ms"] > 0 else 0.0}
                         for k, v in ks.items()},
-            "mlp_tflops_per_step": flops_per_sample(ren) * samples_per_gpu / (elapsed / args.steps) / 1e12,
-            "final_loss": final_loss,
+            "mlp_tflops_per_step": (flops_per_sample(ren) / (3.0 if render else 1.0)) * samples_per_gpu
+                                   / (elapsed / args.steps) / 1e12,
+            ("mean_rgb" if render else "final_loss"): final_loss,
         }
-        if world == 1 and not args.no_cpu_baseline and args.workload == "n2v":
+        if world == 1 and not args.no_cpu_baseline and args.workload == "n2v" and not render:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(out), flush=True)
     if dist is not None:

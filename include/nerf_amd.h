@@ -305,7 +305,7 @@ typedef struct nerf_fused_layer {
     int32_t col_idx;       /* -1 or the column copied to col_out */
     int64_t seg_ld[2];
     const float* seg_ptr[2];
-    float* out;            /* [M][ldo] fp32 */
+    float* out;            /* [M][ldo] fp32; NULL with ldo 0 drops the layer's stores */
     int64_t ldo;
     uint8_t* mask;         /* [M][32] ReLU bits or NULL */
     float* col_out;        /* [M] or NULL */

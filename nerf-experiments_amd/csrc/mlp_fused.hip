@@ -504,9 +504,11 @@ extern "C" int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_laye
         NERF_REQUIRE(L.N >= 1 && L.nb == (L.N + 31) / 32 && L.nb <= 16);
         NERF_REQUIRE(L.chunk_units == 4 * (kbr + kbh));
         NERF_REQUIRE(L.bias_off >= 0 && L.bias_off % 16 == 0);
-        // with a second output only the first n1 chunks land in out (columns past ldo are dropped)
-        NERF_REQUIRE(L.out != nullptr && aligned16(L.out) && L.ldo % 4 == 0 &&
-                     L.ldo >= (L.out2 != nullptr ? (32 * L.n1 < L.N ? 32 * L.n1 : L.N) : L.N));
+        // with a second output only the first n1 chunks land in out (columns past ldo are dropped);
+        // a null out (ldo 0) drops the layer's stores (inference keeps only the exposed outputs)
+        NERF_REQUIRE((L.out == nullptr && L.ldo == 0) ||
+                     (L.out != nullptr && aligned16(L.out) && L.ldo % 4 == 0 &&
+                      L.ldo >= (L.out2 != nullptr ? (32 * L.n1 < L.N ? 32 * L.n1 : L.N) : L.N)));
         NERF_REQUIRE(M * L.ldo * 4 < ((int64_t)1 << 31));
         NERF_REQUIRE(L.mask == nullptr || (L.N <= 256 && M * 32 < ((int64_t)1 << 31)));
         NERF_REQUIRE(L.col_out == nullptr || (L.col_idx >= 0 && L.col_idx % 32 == 0 && L.col_idx < L.N));

@@ -175,6 +175,7 @@ class MLPPlan:
         self.device = None
         self.fused = {}            # device -> mlp_fused.FusedForward
         self.fused_dgrad = {}      # device -> mlp_fused.FusedInputGrad
+        self.infer = False         # set per call by MLPFunction.apply: no autograd graph is recorded
         self.consumed = [False] * len(layers)
         for lp in layers:
             for s in lp.sources:
@@ -208,6 +209,12 @@ def _src_tensor(src: Source, pos, dirs, acts, dir_rd):
 
 
 class MLPFunction(torch.autograd.Function):
+    @classmethod
+    def apply(cls, plan: MLPPlan, *args):
+        # grad mode is off inside forward (and needs_input_grad ignores it): note it for forward
+        plan.infer = not torch.is_grad_enabled()
+        return super().apply(plan, *args)
+
     @staticmethod
     def forward(ctx, plan: MLPPlan, M: int, pos: torch.Tensor, dirs: torch.Tensor | None, dir_rd: int, *params):
         plan.to_device(pos.device)
@@ -225,12 +232,16 @@ class MLPFunction(torch.autograd.Function):
             fused = plan.fused.get(pos.device)
             if fused is None:
                 fused = plan.fused[pos.device] = mlp_fused.FusedForward(plan, pos.device)
+            # without autograd (rendering) only the exposed outputs are stored: the kernel drops
+            # the other layers' stores and the ReLU bits (11 x 268 MB less HBM traffic at M = 2^18)
+            keep_all = not getattr(plan, "infer", False)
             for idx, lp in enumerate(plan.layers):
                 # no packing here: the backward packs the input-gradient layouts (Wt / Wtx) only
                 # if it runs the layer-by-layer GEMMs instead of the fused chain
-                acts.append(torch.empty(M, lp.out_ld, device=pos.device, dtype=torch.float32))
+                acts.append(torch.empty(M, lp.out_ld, device=pos.device, dtype=torch.float32)
+                            if keep_all or idx in plan.outputs else None)
                 masks.append(torch.empty(M, 32, device=pos.device, dtype=torch.uint8)
-                             if lp.relu and plan.consumed[idx] and lp.N <= 256 else None)
+                             if keep_all and lp.relu and plan.consumed[idx] and lp.N <= 256 else None)
             col_t = {li: torch.empty(M, device=pos.device, dtype=torch.float32) for li, _ in plan.column_outputs}
             fused.run(M, pos, dirs, dir_rd, acts, masks, col_t)
             cols = tuple(col_t[li] for li, _ in plan.column_outputs)
@@ -277,7 +288,10 @@ class MLPFunction(torch.autograd.Function):
         ctx.has_dirs = dirs is not None
         ctx.n_pos_cols = pos.shape[1]
         ctx.n_dir_cols = dirs.shape[1] if dirs is not None else 0
-        ctx.save_for_backward(pos, dirs if dirs is not None else pos, *acts, *pre)
+        if any(a is None for a in acts):
+            ctx.save_for_backward(pos)     # no backward can run (no input needed a gradient)
+        else:
+            ctx.save_for_backward(pos, dirs if dirs is not None else pos, *acts, *pre)
         if cols is None:
             cols = tuple(acts[li][:, c].contiguous() for li, c in plan.column_outputs)
         return tuple(acts[i] for i in plan.outputs) + cols

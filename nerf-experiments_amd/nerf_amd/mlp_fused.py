@@ -161,8 +161,8 @@ class FusedForward:
         self.version = ver
 
     def run(self, M: int, pos: torch.Tensor, dirs: torch.Tensor | None, dir_rd: int, acts, masks, col_outs):
-        """Launch on the current stream.  acts[l]: [M, out_ld] fp32, masks[l]: [M, 32] uint8 or
-        None, col_outs: {layer: [M] fp32}."""
+        """Launch on the current stream.  acts[l]: [M, out_ld] fp32 or None (not stored),
+        masks[l]: [M, 32] uint8 or None, col_outs: {layer: [M] fp32}."""
         self.pack()
         L = len(self.plan.layers)
         descs = (_lib.NerfFusedLayer * L)()
@@ -185,8 +185,9 @@ class FusedForward:
                 d.seg_ptr[si] = t.data_ptr()
             d.chunk_units = units
             d.col_idx = -1
-            d.out = acts[idx].data_ptr()
-            d.ldo = acts[idx].stride(0)
+            # a layer without a tensor (inference: not an exposed output) has its stores dropped
+            d.out = acts[idx].data_ptr() if acts[idx] is not None else None
+            d.ldo = acts[idx].stride(0) if acts[idx] is not None else 0
             d.mask = masks[idx].data_ptr() if masks[idx] is not None else None
             if idx in col_outs:
                 d.col_out = col_outs[idx].data_ptr()

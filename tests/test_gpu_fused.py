@@ -94,6 +94,12 @@ def test_fused_forward_matches_layerwise(name, M, rd):
         x, y = x.reshape(x.shape[0], -1)[:, :n], y.reshape(y.shape[0], -1)[:, :n]   # padding columns: unspecified
         scale = max(1.0, x.abs().max().item())
         assert (x - y).abs().max().item() <= 1e-4 * scale
+    # inference (no autograd): the kernel stores only the exposed outputs; same bits
+    from nerf_amd.mlp import MLPFunction
+    with torch.no_grad():
+        o_inf = MLPFunction.apply(plan, M, pos_pe, dir_pe, rd, *plan.params())
+    for x, y, n in zip(o_fus, o_inf, widths):
+        assert torch.equal(x.reshape(x.shape[0], -1)[:, :n], y.reshape(y.shape[0], -1)[:, :n])
     for li, (ma, mb) in enumerate(zip(m_ref, m_fus)):
         assert (ma is None) == (mb is None)
         if ma is None:
