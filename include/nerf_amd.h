@@ -372,6 +372,27 @@ typedef struct nerf_adam_batch {
 } nerf_adam_batch;
 int nerf_adam_step(const nerf_adam_batch* batch, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * On-device training-batch feed.  Replaces, for one batch of dataset
+ * indices, ImagePoseDataset.__getitem__ (barf/dataset.py:613-637) over the dataset's
+ * precomputed rays (_get_directions_meshgrid :417-451, _meshgrid_to_world :453-481,
+ * _apply_noise :512-557), the DataLoader's collation, and
+ * ImagePoseDataModule.get_blurred_pixel_colors (barf/data_module.py:276-367).
+ *   indices [B] int64: dataset index = image * H*W + row * W + col (the sampler's order)
+ *   c2w [n_img][4][4]; noise_rot [n_img][3][3] / noise_trans [n_img][3] or NULL
+ *   images [n_img][H][W][n_sigma][3] fp32 (blur levels, most blurred first)
+ * Outputs ([B][3] unless noted; NULL skips): o_raw, d_raw, o_noisy + d_noisy (together),
+ * colors_raw [B][n_sigma][3], colors_pair [B][2][3] = (blurred, original) with
+ * blur_mode 1: (last, last), 2: (level 0, last), 3: (level lo * coef_lo + level hi * coef_hi,
+ * last); img_idx [B] int64.  status (device int32, caller-zeroed): bit 0 = an index was out
+ * of range (that ray reads index 0).
+ * ------------------------------------------------------------------------- */
+int nerf_ray_batch(const int64_t* indices, int64_t B, int32_t H, int32_t W, float focal,
+                   const float* c2w, const float* noise_rot, const float* noise_trans, int32_t n_img,
+                   const float* images, int32_t n_sigma, int32_t blur_mode, int32_t blur_lo, int32_t blur_hi,
+                   float coef_lo, float coef_hi, float* o_raw, float* o_noisy, float* d_raw, float* d_noisy,
+                   float* colors_raw, float* colors_pair, int64_t* img_idx, int32_t* status, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

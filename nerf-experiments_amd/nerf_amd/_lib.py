@@ -128,6 +128,8 @@ _SIGNATURES = {
                                      c_i64, c_i32, c_vp, c_vp, c_i32, c_vp]),
     "nerf_encode_rays": (c_i32, [ctypes.POINTER(NerfPEParams), c_vp, c_i64, c_vp, c_i64, c_vp]),
     "nerf_adam_step": (c_i32, [ctypes.POINTER(NerfAdamBatch), c_vp]),
+    "nerf_ray_batch": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_f, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_i32, c_i32,
+                               c_i32, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "nerf_gauss_act_workspace": (c_sz, [c_i64, c_i32]),
     "nerf_gauss_act_fwd": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp]),
     "nerf_gauss_act_bwd": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_i32,

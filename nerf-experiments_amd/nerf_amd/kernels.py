@@ -130,6 +130,34 @@ def sample_uniform(n_rays: int, samples_per_ray: int, near: float, far: float, s
     return t0, t1
 
 
+def ray_batch(indices: torch.Tensor, H: int, W: int, focal: float, c2w: torch.Tensor, noise_rot, noise_trans,
+              images: torch.Tensor, blur: tuple[int, int, int, float, float] | None, want_raw_colors: bool,
+              status: torch.Tensor):
+    """nerf_ray_batch: (o_raw, o_noisy, d_raw, d_noisy, colors_raw or None, colors_pair or None, img_idx).
+    blur = (mode, lo, hi, coef_lo, coef_hi) or None (no pair output)."""
+    dev = indices.device
+    B = indices.shape[0]
+    n_img, n_sigma = c2w.shape[0], images.shape[-2]
+    for name, t in (("indices", indices), ("c2w", c2w), ("images", images)):
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+    if indices.dtype != torch.int64 or images.shape[:3] != (n_img, H, W) or images.shape[-1] != 3:
+        raise ValueError("indices int64 [B]; images [n_img, H, W, n_sigma, 3]")
+    f = dict(device=dev, dtype=torch.float32)
+    o_raw, d_raw = torch.empty(B, 3, **f), torch.empty(B, 3, **f)
+    o_noisy, d_noisy = torch.empty(B, 3, **f), torch.empty(B, 3, **f)
+    craw = torch.empty(B, n_sigma, 3, **f) if want_raw_colors else None
+    cpair = torch.empty(B, 2, 3, **f) if blur is not None else None
+    img_idx = torch.empty(B, device=dev, dtype=torch.int64)
+    mode, lo, hi, ca, cb = blur if blur is not None else (0, 0, 0, 0.0, 0.0)
+    st = _lib.load().nerf_ray_batch(_ptr(indices), B, H, W, focal, _ptr(c2w), _ptr(noise_rot), _ptr(noise_trans),
+                                    n_img, _ptr(images), n_sigma, mode, lo, hi, ca, cb, _ptr(o_raw), _ptr(o_noisy),
+                                    _ptr(d_raw), _ptr(d_noisy), _ptr(craw), _ptr(cpair), _ptr(img_idx),
+                                    _ptr(status), _stream(dev))
+    _lib.check(st, "nerf_ray_batch")
+    return o_raw, o_noisy, d_raw, d_noisy, craw, cpair, img_idx
+
+
 def resample_pdf(t_coarse: torch.Tensor, weights: torch.Tensor, dist_coarse: torch.Tensor, n_samples: int,
                  mode: int, near: float, far: float, seed: int, counter: int, status: torch.Tensor | None = None):
     for name, t in (("t_coarse", t_coarse), ("weights", weights), ("distances_coarse", dist_coarse)):

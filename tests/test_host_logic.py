@@ -334,3 +334,37 @@ def test_fused_forward_image_emulation(name):
     for idx in range(len(plan.layers)):
         err = np.abs(outs[idx] - acts[idx]).max()
         assert err <= 1e-4 * max(1.0, np.abs(acts[idx]).max()), (idx, err)
+
+
+def test_ray_feed_epoch_order_matches_torch_dataloader():
+    """DeviceRayFeed's shuffled index order is the reference DataLoader's (shuffle=True with a
+    seeded generator, data_module.py:202-209), epoch after epoch, whatever the batch size."""
+    from torch.utils.data import DataLoader, Dataset
+
+    from nerf_amd.ray_feed import dataloader_epoch_order
+
+    class _Idx(Dataset):
+        def __len__(self):
+            return 77
+
+        def __getitem__(self, i):
+            return i
+
+    for kw in (dict(batch_size=8), dict(batch_size=8, drop_last=True), dict(batch_size=77)):
+        dl = DataLoader(_Idx(), shuffle=True, generator=torch.Generator().manual_seed(5), **kw)
+        g = torch.Generator().manual_seed(5)
+        for _ in range(3):
+            got = torch.cat(list(dl))
+            want = dataloader_epoch_order(77, g)
+            assert torch.equal(got, want[:len(got)])
+
+
+def test_ray_feed_blur_selection():
+    """get_blurred_pixel_colors' case split (data_module.py:324-365)."""
+    from nerf_amd.ray_feed import blur_selection
+    sig = [8.0, 4.0, 2.0, 0.0]
+    assert blur_selection(sig, 0.1)[0] == 1
+    assert blur_selection(sig, 8.0)[0] == 2
+    mode, lo, hi, a, b = blur_selection(sig, 3.0)
+    assert (mode, lo, hi) == (3, 1, 2)
+    assert abs(a - (3.0 - 2.0) / (4.0 - 2.0 + 1e-8)) < 1e-12 and abs(a + b - 1) < 1e-12
