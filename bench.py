@@ -94,6 +94,46 @@ def synthetic_batch_lego(n_rays: int, seed: int, device, image_size: int):
     return o.to(device), d.to(device), pw.to(device), target.to(device), img.to(device)
 
 
+def lookat_c2w(n_views: int, radius: float, seed: int) -> torch.Tensor:
+    """[n, 4, 4] camera-to-world matrices of cameras on the upper hemisphere at `radius` looking at
+    the origin (camera looks down -z, y up: the Blender convention of barf/dataset.py:417-451)."""
+    g = torch.Generator().manual_seed(seed)
+    u = torch.rand(n_views, 2, generator=g)
+    theta = u[:, 0] * 2 * math.pi
+    z = u[:, 1] * 0.9 + 0.1
+    r = torch.sqrt(1 - z * z)
+    back = torch.stack((r * torch.cos(theta), r * torch.sin(theta), z), dim=1)
+    right = torch.nn.functional.normalize(torch.linalg.cross(torch.tensor([0.0, 0.0, 1.0]).expand_as(back), back),
+                                          dim=1)
+    up = torch.linalg.cross(back, right)
+    c2w = torch.zeros(n_views, 4, 4)
+    c2w[:, :3, 0], c2w[:, :3, 1], c2w[:, :3, 2] = right, up, back
+    c2w[:, :3, 3] = back * radius
+    c2w[:, 3, 3] = 1
+    return c2w
+
+
+def device_feed(name: str, device, rank: int, batch_size: int):
+    """DeviceRayFeed over 100 synthetic views (procedural colours of each pixel's ray direction)
+    at the workload's scene scale; the feed assembles every step's batch on the GPU."""
+    from nerf_amd.ray_feed import DeviceRayFeed
+    size, radius = (400, 0.168) if name == "n2v" else ((800, 4.03) if name == "mip" else (400, 4.03))
+    focal = size / 2 / math.tan(0.6911112 / 2)
+    c2w = lookat_c2w(100, radius, 77)
+    images = torch.zeros(100, size, size, 1, 3, device=device)
+    feed = DeviceRayFeed(images, c2w, focal, batch_size, rotation_noise_sigma=0.15 if name == "barf" else 0.0,
+                         translation_noise_sigma=0.15 if name == "barf" else 0.0, noise_seed=0,
+                         dataloader_seed=rank, device=device)
+    n = 100 * size * size
+    flat = images.view(n, 3)
+    for s in range(0, n, 1 << 22):
+        idx = torch.arange(s, min(n, s + (1 << 22)), device=device)
+        d = feed.batch(idx)[2]
+        flat[s:s + idx.shape[0]] = 0.5 + 0.5 * torch.sin(torch.stack((3 * d[:, 0], 5 * d[:, 1] + 1, 7 * d[:, 2] + 2),
+                                                                     dim=1))
+    return feed
+
+
 def build_model(device):
     from nerf_amd import FourierFeatures, NerfInterpolation, NerfModel
     torch.manual_seed(0)
@@ -104,8 +144,15 @@ def build_model(device):
     return ren
 
 
-def build_workload(name: str, device, rank: int):
-    """(renderer, extra modules, step closure factory inputs) for one workload."""
+def _feed_stream(feed):
+    """Endless batches: epoch after epoch of the feed's shuffled order."""
+    while True:
+        yield from feed.epoch()
+
+
+def build_workload(name: str, device, rank: int, feed: bool = False):
+    """(renderer, extra modules, optimizer, loss closure, render closure) for one workload; with
+    feed=True every step draws a fresh batch from the on-device ray feed."""
     from nerf_amd import (BarfPositionalEncoding, FusedAdam, IntegratedBarfFourierFeatures, NerfInterpolation,
                           NerfModel)
     from nerf_amd.model_camera_extrinsics import CameraExtrinsics
@@ -114,6 +161,17 @@ def build_workload(name: str, device, rank: int):
         ren = build_model(device)
         o, d, pw, target = synthetic_batch(w["rays"], 1000 + rank, device)
         opt = ren.configure_optimizers()["optimizer"]
+        if feed:
+            nxt = _feed_stream(device_feed(name, device, rank, w["rays"]))
+
+            def loss_fn():
+                o_, _, d_, _, c_, _, pw_ = next(nxt)
+                return ren.training_loss(o_, d_, pw_, c_[:, -1])[0]
+
+            def render_fn():
+                o_, _, d_, _, _, _, pw_ = next(nxt)
+                return ren(o_, d_, pw_)
+            return ren, [ren], opt, loss_fn, render_fn
 
         def loss_fn():
             return ren.training_loss(o, d, pw, target)[0]
@@ -128,6 +186,17 @@ def build_workload(name: str, device, rank: int):
                                 w["coarse"]).to(device)
         o, d, pw, target, _ = synthetic_batch_lego(w["rays"], 1000 + rank, device, 800)
         opt = ren.configure_optimizers()["optimizer"]
+        if feed:
+            nxt = _feed_stream(device_feed(name, device, rank, w["rays"]))
+
+            def loss_fn():
+                o_, _, d_, _, c_, _, pw_ = next(nxt)
+                return ren.training_loss(o_, d_, pw_, c_[:, -1])[0]
+
+            def render_fn():
+                o_, _, d_, _, _, _, pw_ = next(nxt)
+                return ren(o_, d_, pw_)
+            return ren, [ren], opt, loss_fn, render_fn
 
         def loss_fn():
             return ren.training_loss(o, d, pw, target)[0]
@@ -146,6 +215,21 @@ def build_workload(name: str, device, rank: int):
         groups = [{"params": list(g["parameters"]), "lr": g["learning_rate_start"], "weight_decay": g["weight_decay"]}
                   for g in ren.param_groups + extr.param_groups]
         opt = FusedAdam(groups, eps=1e-5)
+
+        if feed:
+            nxt = _feed_stream(device_feed(name, device, rank, w["rays"]))
+
+            def loss_fn():
+                # noisy poses refined by the per-image extrinsics (model_barf.py's training input)
+                _, o_, _, d_, c_, i_, pw_ = next(nxt)
+                o2, d2, _, _ = extr(i_, o_, d_)
+                return ren.training_loss(o2, d2, pw_, c_[:, -1])[0]
+
+            def render_fn():
+                _, o_, _, d_, _, i_, pw_ = next(nxt)
+                o2, d2, _, _ = extr(i_, o_, d_)
+                return ren(o2, d2, pw_)
+            return ren, [ren, extr], opt, loss_fn, render_fn
 
         def loss_fn():
             o2, d2, _, _ = extr(img, o, d)
@@ -223,6 +307,9 @@ def main():
     ap.add_argument("--mode", default="train", choices=("train", "render"),
                     help="train: forward + backward + all-reduce + Adam per step (the headline metric); "
                          "render: the forward pass only, without autograd (BASELINE.json's render metric)")
+    ap.add_argument("--feed", default="device", choices=("device", "fixed"),
+                    help="device: every step draws a fresh shuffled batch from 100 synthetic views through "
+                         "the on-device ray feed (nerf_ray_batch); fixed: one resident batch reused")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--matmul-precision", default="high", choices=("highest", "high", "medium"),
@@ -249,7 +336,7 @@ def main():
     nerf_amd._lib.load()
 
     wl = WORKLOADS[args.workload]
-    ren, modules, opt, loss_fn, render_fn = build_workload(args.workload, device, rank)
+    ren, modules, opt, loss_fn, render_fn = build_workload(args.workload, device, rank, args.feed == "device")
     allreduce = GradAllReduce([p for m in modules for p in m.parameters()])
     torch.manual_seed(1234 + rank)
     render = args.mode == "render"
@@ -343,7 +430,10 @@ def main():
             "dtype": "fp32",
             "matmul": ("3xbf16 split MFMA (hi*hi+hi*lo+lo*hi, fp32 accumulate)" if x3 else "fp32 MFMA"),
             "matmul_precision": args.matmul_precision,
-            "data": "synthetic Lego-shaped rays/targets, random-init weights (torch.manual_seed(0))",
+            "data": ("synthetic: 100 procedural views at Lego scale, a fresh shuffled batch per step from the "
+                     "on-device ray feed; random-init weights (torch.manual_seed(0))" if args.feed == "device" else
+                     "synthetic Lego-shaped rays/targets (one resident batch), random-init weights "
+                     "(torch.manual_seed(0))"),
             "config": {"workload": wl["config"], "workload_key": args.workload,
                        "rays_per_gpu": wl["rays"], "samples_per_ray": wl["coarse"] + wl["fine"],
                        "coarse_samples": wl["coarse"], "fine_samples": wl["fine"], "global_rays": wl["rays"] * world,

@@ -90,10 +90,13 @@ class DeviceRayFeed:
         self.camera_to_worlds = camera_to_worlds.to(self.device, th.float32).contiguous()
         self.focal_length = float(focal_length)
         self.pixel_width = th.tensor(1 / self.focal_length)
+        self.batch_size = int(batch_size)
+        # the collated per-ray pixel widths, resident (a per-batch host->device copy of a pageable
+        # tensor would drain the stream)
+        self._pixel_widths = self.pixel_width.to(self.device).repeat(self.batch_size)
         rot, trans = pose_noise(self.n_images, rotation_noise_sigma, translation_noise_sigma, noise_seed)
         self.noise_rotation = rot.to(self.device, th.float32).contiguous()
         self.noise_translation = trans.to(self.device, th.float32).contiguous()
-        self.batch_size = int(batch_size)
         self.drop_last = drop_last
         self.generator = th.Generator().manual_seed(dataloader_seed)
         self.status = th.zeros(1, dtype=th.int32, device=self.device)
@@ -108,7 +111,8 @@ class DeviceRayFeed:
         o_raw, o_n, d_raw, d_n, craw, cpair, img_idx = K.ray_batch(
             indices, self.H, self.W, self.focal_length, self.camera_to_worlds, self.noise_rotation,
             self.noise_translation, self.images, blur, sigma is None, self.status)
-        pw = self.pixel_width.to(self.device).expand(indices.shape[0])
+        B = indices.shape[0]
+        pw = self._pixel_widths[:B] if B <= self.batch_size else self.pixel_width.to(self.device).repeat(B)
         return o_raw, o_n, d_raw, d_n, (cpair if sigma is not None else craw), img_idx, pw
 
     def epoch(self, sigma: float | None = None):
