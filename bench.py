@@ -390,10 +390,17 @@ def main():
     cands = [k for k in ("mlp_fused_fwd", "mlp_fused_dgrad", nt_name, "linear_wgrad_x3" if x3 else "linear_wgrad")
              if k in ks]
     dom = max(cands, key=lambda k: ks[k]["ms"]) if cands else nt_name
-    nt = ks.get(dom, {"launches": 0, "flops": 0.0, "ms": 0.0})
+    nt = ks.get(dom, {"launches": 0, "flops": 0.0, "bytes": 0.0, "ms": 0.0})
     nt_avg_ms = nt["ms"] / max(nt["launches"], 1)
     nt_avg_flops = nt["flops"] / max(nt["launches"], 1)
+    nt_avg_bytes = nt["bytes"] / max(nt["launches"], 1)
     achieved = (nt_avg_flops / (nt_avg_ms * 1e-3)) / 1e12 if nt_avg_ms > 0 else 0.0
+    # which roof binds: algorithmic FLOPs per algorithmic byte against the ridge point of the MFMA
+    # peak and HBM (e.g. the weight gradients: 53 flop/B < 105 at split precision -> HBM-bound)
+    intensity = nt_avg_flops / nt_avg_bytes if nt_avg_bytes > 0 else float("inf")
+    ridge = peak * 1e12 / (HBM_PEAK_GBS * 1e9)
+    hbm_bound = intensity < ridge
+    achieved_gbs = nt_avg_bytes / (nt_avg_ms * 1e-3) / 1e9 if nt_avg_ms > 0 else 0.0
     dom_desc = {
         "mlp_fused_fwd": "the whole field-MLP forward in one launch",
         "mlp_fused_dgrad": "the backward's input-gradient chain in one launch",
@@ -440,10 +447,19 @@ def main():
                        "parallelism": f"ray-batch dp{world}" + (" (RCCL all-reduce)" if world > 1 else "")},
             "roofline": {"kernel": (f"{dom} (" + ("3 x bf16 MFMA; peak = bf16 dense / 3"
                                                    if x3 else "fp32 MFMA 32x32x2")
-                                    + f": {dom_desc}; achieved in algorithmic fp32 GEMM flops)"),
-                         "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": traffic,
+                                    + f": {dom_desc}; algorithmic fp32 GEMM flops and algorithmic bytes, "
+                                    "bound = the lower roof at this kernel's arithmetic intensity)"),
+                         "bound": "hbm" if hbm_bound else "mfma",
+                         "achieved": achieved_gbs if hbm_bound else achieved,
+                         "peak": HBM_PEAK_GBS if hbm_bound else peak,
+                         "unit": "GB/s" if hbm_bound else "TFLOP/s",
+                         "frac": achieved_gbs / HBM_PEAK_GBS if hbm_bound else achieved / peak,
+                         "traffic": traffic,
+                         "arithmetic_intensity": intensity, "ridge": ridge,
+                         "achieved_tflops": achieved, "peak_tflops": peak,
+                         "attainable_tflops": min(peak, intensity * HBM_PEAK_GBS * 1e9 / 1e12),
                          "avg_launch_us": nt_avg_ms * 1e3, "avg_flops_per_launch": nt_avg_flops,
+                         "avg_bytes_per_launch": nt_avg_bytes,
                          "launches_per_step": nt["launches"] / args.steps},
             "roofline_hbm": {"kernel": "encode_fwd + composite_fwd + composite_bwd (positional encoding and "
                                        "alpha compositing; algorithmic bytes per launch)",

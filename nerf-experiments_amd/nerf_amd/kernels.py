@@ -340,11 +340,17 @@ def make_segs(segs: Sequence[tuple[torch.Tensor, int, int]]):
     return arr
 
 
+def _segs_bytes(segs, M: int) -> float:
+    """Algorithmic bytes of a segmented fp32 operand: every row of every segment read once."""
+    return sum(4.0 * k * ((M + rd - 1) // rd) for _, k, rd in segs)
+
+
 def linear_fwd(segs, M: int, W: torch.Tensor, ldw: int, N: int, bias: torch.Tensor | None, out: torch.Tensor,
                epilogue: int, aux: torch.Tensor | None = None, w_row_offset: int = 0) -> None:
     arr = make_segs(segs)
     wptr = W.data_ptr() + w_row_offset * ldw * 4
-    end = TIMER.bracket("linear_nt", 2.0 * M * N * ldw) if TIMER is not None else None
+    end = TIMER.bracket("linear_nt", 2.0 * M * N * ldw, _segs_bytes(segs, M) + 4.0 * M * N + 4.0 * N * ldw) \
+        if TIMER is not None else None
     st = _lib.load().nerf_linear_fwd(arr, len(segs), M, wptr, ldw, N, _ptr(bias), _ptr(out), out.stride(0),
                                      epilogue, _ptr(aux), aux.stride(0) if aux is not None else 0,
                                      _stream(out.device))
@@ -356,7 +362,9 @@ def linear_fwd(segs, M: int, W: torch.Tensor, ldw: int, N: int, bias: torch.Tens
 def linear_wgrad(dY: torch.Tensor, N4: int, segs, M: int, workspace: torch.Tensor) -> None:
     arr = make_segs(segs)
     kt = sum(k for _, k, _ in segs)
-    end = TIMER.bracket("linear_wgrad", 2.0 * M * N4 * kt) if TIMER is not None else None
+    # algorithmic bytes: dY and X read once, dW written once (the split-M slabs are the kernel's)
+    end = TIMER.bracket("linear_wgrad", 2.0 * M * N4 * kt, 4.0 * M * N4 + _segs_bytes(segs, M) + 4.0 * N4 * kt) \
+        if TIMER is not None else None
     st = _lib.load().nerf_linear_wgrad(_ptr(dY), dY.stride(0), N4, arr, len(segs), M, _ptr(workspace),
                                        workspace.numel() * workspace.element_size(), _stream(dY.device))
     if end is not None:
@@ -381,7 +389,8 @@ def linear_fwd_x3(segs, M: int, Wx: torch.Tensor, ldw: int, N: int, bias: torch.
     weights of nerf_pack_weight_x3 ([rows][ldw/32][hi 32 | lo 32] bf16)."""
     arr = make_segs(segs)
     off = w_row_offset * ldw * 2 * 2
-    end = TIMER.bracket("linear_nt_x3", 2.0 * M * N * ldw) if TIMER is not None else None
+    end = TIMER.bracket("linear_nt_x3", 2.0 * M * N * ldw, _segs_bytes(segs, M) + 4.0 * M * N + 4.0 * N * ldw) \
+        if TIMER is not None else None
     st = _lib.load().nerf_linear_fwd_x3(arr, len(segs), M, Wx.data_ptr() + off, ldw, N, _ptr(bias), _ptr(out),
                                         out.stride(0), epilogue, _ptr(aux), aux.stride(0) if aux is not None else 0,
                                         _stream(out.device))
@@ -393,7 +402,9 @@ def linear_fwd_x3(segs, M: int, Wx: torch.Tensor, ldw: int, N: int, bias: torch.
 def linear_wgrad_x3(dY: torch.Tensor, N4: int, segs, M: int, workspace: torch.Tensor) -> None:
     arr = make_segs(segs)
     kt = sum(k for _, k, _ in segs)
-    end = TIMER.bracket("linear_wgrad_x3", 2.0 * M * N4 * kt) if TIMER is not None else None
+    # algorithmic bytes: dY and X read once, dW written once (the split-M slabs are the kernel's)
+    end = TIMER.bracket("linear_wgrad_x3", 2.0 * M * N4 * kt, 4.0 * M * N4 + _segs_bytes(segs, M) + 4.0 * N4 * kt) \
+        if TIMER is not None else None
     st = _lib.load().nerf_linear_wgrad_x3(_ptr(dY), dY.stride(0), N4, arr, len(segs), M, _ptr(workspace),
                                           workspace.numel() * workspace.element_size(), _stream(dY.device))
     if end is not None:

@@ -167,6 +167,7 @@ class FusedForward:
         L = len(self.plan.layers)
         descs = (_lib.NerfFusedLayer * L)()
         flops = 0.0
+        nbytes = 0.0
         for idx, lp in enumerate(self.plan.layers):
             kbr, kbh, hbm, nb, units, off, bias_off = self.layers[idx]
             d = descs[idx]
@@ -195,7 +196,12 @@ class FusedForward:
             d.img_off = off
             d.bias_off = bias_off
             flops += 2.0 * M * lp.module.out_features * lp.module.in_features
-        end = K.TIMER.bracket("mlp_fused_fwd", flops) if K.TIMER is not None else None
+            # algorithmic bytes: HBM-fed encodings read, stored outputs / mask bits / columns written
+            nbytes += sum(4.0 * d.seg_k[si] * d.seg_rows[si] for si in range(d.nseg))
+            nbytes += (4.0 * M * acts[idx].shape[1] if acts[idx] is not None else 0.0) \
+                + (32.0 * M if masks[idx] is not None else 0.0) + (4.0 * M if idx in col_outs else 0.0)
+        end = K.TIMER.bracket("mlp_fused_fwd", flops, nbytes + self.image.numel() * self.image.element_size()) \
+            if K.TIMER is not None else None
         st = _lib.load().nerf_mlp_fused_fwd(descs, L, self.image.data_ptr(), M, K._stream(self.device))
         if end is not None:
             end.record()
@@ -359,6 +365,7 @@ class FusedInputGrad:
         S = len(self.steps)
         descs = (_lib.NerfFusedLayer * S)()
         flops = 0.0
+        nbytes = 0.0
         for i, (l, kbr, kbh, n1, x, n_out, nb, units, img_off, bias_off) in enumerate(self.steps):
             lp = self.plan.layers[l]
             d = descs[i]
@@ -395,7 +402,11 @@ class FusedInputGrad:
             d.img_off = img_off
             d.bias_off = bias_off
             flops += 2.0 * M * lp.module.out_features * n_out
-        end = K.TIMER.bracket("mlp_fused_dgrad", flops) if K.TIMER is not None else None
+            # algorithmic bytes: HBM-fed gradients and ReLU bits read, dY / encoding gradients written
+            nbytes += (4.0 * d.seg_k[0] * d.seg_rows[0] if kbh else 0.0) + (32.0 * M if d.mask_in else 0.0)
+            nbytes += 4.0 * M * min(d.ldo, n_out) + (4.0 * M * d.ldo2 if x is not None else 0.0)
+        end = K.TIMER.bracket("mlp_fused_dgrad", flops, nbytes + self.image.numel() * self.image.element_size()) \
+            if K.TIMER is not None else None
         st = _lib.load().nerf_mlp_fused_fwd(descs, S, self.image.data_ptr(), M, K._stream(self.device))
         if end is not None:
             end.record()
