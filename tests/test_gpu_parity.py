@@ -151,13 +151,15 @@ def test_render_rays_golden_and_grad(golden, S, magic):
     np.testing.assert_allclose(col.grad.cpu().numpy(), co.grad.numpy(), atol=2e-6, rtol=0)
 
 
-def test_composite_raw_heads_fused_activation():
-    """act = 1: softplus(thr 8) / sigmoid applied in-kernel on strided raw head buffers."""
+@pytest.mark.parametrize("width,S", [(32, 128), (4, 128), (4, 64), (4, 100), (4, 257)])
+def test_composite_raw_heads_fused_activation(width, S):
+    """act = 1: softplus(thr 8) / sigmoid applied in-kernel on strided raw head buffers.
+    width 4 is the [rgb | sigma] head row the kernels load and store as one 16-byte access."""
     from nerf_amd.model_interpolation import composite_raw
     from nerf_amd.model_interpolation_architecture import RawHeads
     torch.manual_seed(1)
-    B, S = 50, 128
-    head = (torch.randn(B * S, 32) * 3)
+    B = 50
+    head = (torch.randn(B * S, width) * 3)
     head[:, 4:] = 0
     dist = torch.rand(B, S) * 0.05
     hd = head.to(DEV).requires_grad_(True)

@@ -99,8 +99,9 @@ def bench_composite(B, S):
     gh = torch.zeros_like(head)
     ms_b = time_it(lambda: K.composite_bwd(head[:, 3:], 4, head, 4, dist, B, S, 3.0, 7.0, True, 0.0, g, None,
                                            gh[:, 3:], 4, gh, 4))
+    algo_b = B * S * (16 + 4 + 16) + B * 12
     return {"kernel": "composite", "B": B, "S": S, "fwd_ms": ms, "fwd_GBs_algo": algo / ms / 1e6,
-            "bwd_ms": ms_b}
+            "bwd_ms": ms_b, "bwd_GBs_algo": algo_b / ms_b / 1e6}
 
 
 def bench_encode(B, S):
@@ -128,6 +129,7 @@ def bench_resample(B, Kb, N):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json")
+    ap.add_argument("--hbm", action="store_true", help="only the compositing / encoding kernels")
     ap.add_argument("--only", help="run one shape repeatedly for counter collection: nt256 | nt256mask | wgrad256")
     args = ap.parse_args()
     M = 4096 * 64
@@ -143,6 +145,15 @@ def main():
               "encode": lambda: bench_encode(4096, 64),
               "encode_big": lambda: bench_encode(65536, 128)}[args.only]
         print(json.dumps(fn()))
+        return
+    if args.hbm:  # the HBM-bound kernels at bench size and at sizes where launch latency is amortised
+        res = [bench_composite(4096, 64), bench_composite(65536, 64), bench_composite(65536, 128),
+               bench_composite(262144, 128), bench_encode(4096, 64), bench_encode(65536, 128)]
+        for r in res:
+            print(json.dumps(r))
+        if args.json:
+            with open(args.json, "w") as f:
+                json.dump(res, f, indent=1)
         return
     for x3 in (False, True):
         # forward layers of the bench model
