@@ -26,6 +26,8 @@
 //   MFMA reduction index is the sample index.  A second kernel sums the
 //   slices in a fixed order (deterministic) and scatters into the nn.Linear
 //   gradient layout through a column map.
+#include <cstdlib>
+
 #include "common.h"
 
 using namespace nerf;
@@ -487,8 +489,14 @@ int cu_count() {
 // split-precision kernels and the reduce): enough workgroups for the whole chip even with
 // the 256 x 256 tiles of the split-precision kernel (one workgroup per CU).
 int choose_splits(int64_t M, int tiles) {
+    // NERF_WGRAD_SPLITS (read once) overrides the split count, for split-count experiments
+    static const int64_t split_override = [] {
+        const char* e = getenv("NERF_WGRAD_SPLITS");
+        return e ? (int64_t)atoi(e) : (int64_t)0;
+    }();
     int64_t target = 1024 / (tiles > 0 ? tiles : 1);
     if (target > 256) target = 256;
+    if (split_override > 0) target = split_override;
     if (target < 1) target = 1;
     const int64_t max_splits = (M + TBM - 1) / TBM;
     if (target > max_splits) target = max_splits;

@@ -25,4 +25,15 @@ e.record()
 torch.cuda.synchronize()
 us = s.elapsed_time(e) * 1e3 / n
 print(f"linear_wgrad_x3 256 x 256, M {M}: {us:.1f} us, "
-      f"{2 * M * 1024 / us / 1e3:.0f} GB/s of dY+X")
+      f"{2 * M * 1024 / us / 1e3:.0f} GB/s of dY+X  (NERF_WGRAD_SPLITS={os.environ.get('NERF_WGRAD_SPLITS', 'auto')})")
+# with the fixed-order slab reduction into the nn.Linear layout, as the backward runs it
+col_map = torch.arange(Kd, dtype=torch.int32, device=dev)
+gW = torch.empty(N, Kd, device=dev)
+gb = torch.empty(N, device=dev)
+s.record()
+for _ in range(n):
+    K.linear_wgrad_x3(dY, N, [(X, Kd, 1)], M, ws)
+    K.linear_wgrad_reduce(M, N, Kd, N, ws, col_map, gW, gb)
+e.record()
+torch.cuda.synchronize()
+print(f"  + reduce: {s.elapsed_time(e) * 1e3 / n:.1f} us per layer")
