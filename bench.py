@@ -1,25 +1,23 @@
 #!/usr/bin/env python3
-"""Headline benchmark: NeRF training-step throughput in ray-samples/s.
+"""Headline benchmark: NeRF training-step throughput in ray-samples/s (coarse + fine).
 
-Default workload (BASELINE.json configs[1], the headline line): naive-to-vanilla NeRF at the
-Lego 400x400 setting — per GPU 4096 rays x 64 stratified samples per step, NerfModel with
-n_hidden=4, hidden_dim=256, 2 segments, delayed direction + density, Fourier position encoding
-(L=10, scale 2*pi) and direction encoding (L=4, scale 1), near/far 0.1/0.333, density factor 3*7
-(naive-to-vanilla/main.py:89-102, model_interpolation.py:8,97-125,198-235).  A step is the whole
-training step: t sampling -> encodings -> 12-layer MLP -> compositing -> MSE -> backward ->
-(N>1: RCCL all-reduce of the flat gradient) -> Adam.  Synthetic Lego-shaped rays and target
-colours (no dataset is available offline).
+Default workload (BASELINE.json's metric: "ray-samples/sec (coarse+fine) ... Lego 800²" =
+configs[2]): mip-NeRF masked integrated PE, per GPU 4096 rays x (64 coarse + 128 fine) samples per
+step — stratified coarse t (offset -1) -> IPE -> shared NerfModel (n_hidden 4, width 256, 2 segments,
+delayed direction) -> compositing -> pdf resample (largest remainder) -> fine IPE -> NerfModel ->
+compositing -> MSE(fine) + MSE(coarse) -> backward -> (N>1: RCCL all-reduce) -> Adam
+(barf/model_builders.py:106-195, barf/model_mip.py:85-304, barf/model_interpolation.py:417-526).
+Lego 800x800 pixel width; synthetic Lego-scale rays (no dataset is available offline).
 
 Other BASELINE.json configs as extra workloads (same JSON line, their own `config`):
-  --workload mip   configs[2]: mip-NeRF masked integrated PE, coarse 64 + fine 128 samples through
-                   the pdf resample, one shared NerfModel (barf/model_builders.py:106-195,
-                   model_mip.py), Lego 800x800 pixel width, 4096 rays per GPU
+  --workload n2v   configs[1]: naive-to-vanilla NeRF, Lego 400x400, 4096 rays x 64 stratified samples,
+                   Fourier PE L10/L4, delayed density, density factor 3*7 (naive-to-vanilla/main.py:89-102)
   --workload barf  configs[3]: BARF pose refinement — masked Fourier PE L10/L4 + identity, 128
                    equidistant samples (run_barf.py:150-196), rays refined by per-image so3
                    CameraExtrinsics (100 views) whose gradients come back through the fused
                    ray-mode encoding backward, 4096 rays per GPU
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload n2v|mip|barf]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload mip|n2v|barf]
     (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
 
 Prints ONE JSON line on rank 0 (schema: see DESIGN.md §Measurement).
@@ -249,33 +247,94 @@ def flops_per_sample(ren) -> float:
     return 2.0 * macs * 3.0
 
 
-def cpu_baseline(seconds: float = 15.0):
-    """The CPU oracle (oracle/nerf_oracle.py, PyTorch CPU fp32 — a restatement of the
-    reference's CPU path) running the same training step on a bounded sample."""
+def _cpu_model_name() -> str:
+    cpu_model = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return cpu_model
+
+
+def _cpu_mip_state():
+    """The mip workload's NerfModel (same constructor, same torch.manual_seed(0) init) on the CPU."""
+    from nerf_amd import BarfPositionalEncoding, IntegratedBarfFourierFeatures, NerfModel
+    torch.manual_seed(0)
+    pos = IntegratedBarfFourierFeatures(10, 10, 1.28, 6.4, True, 1.0, True)
+    dirs = BarfPositionalEncoding(4, 4, 1.28, 6.4, True, 1.0)
+    model = NerfModel(4, 256, True, False, 2, pos, dirs, 5e-4, 1e-4, 200000)
+    return model.state_dict()
+
+
+def cpu_baseline(workload: str, seconds: float = 15.0):
+    """The CPU oracle (oracle/nerf_oracle.py, PyTorch CPU fp32 — a restatement of the reference's
+    CPU path, pinned to the reference's own outputs by tests/golden) running the workload's training
+    step on a bounded sample: the same model, encodings, sample counts and loss, B rays per step."""
     from oracle import nerf_oracle as O
     threads = len(os.sched_getaffinity(0))
     threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
     torch.set_num_threads(threads)
-    ren = build_model("cpu")
-    sd = {k: v.clone().requires_grad_(True) for k, v in ren.model_radiance.state_dict().items()}
+    torch.manual_seed(4321)
+    if workload == "mip":
+        sd = {k: v.clone().requires_grad_(True) for k, v in _cpu_mip_state().items() if not k.endswith("alpha")}
+        B, K, S = 1024, WORKLOADS["mip"]["coarse"], WORKLOADS["mip"]["fine"]
+        near, far = 2.0, 8.0
+        o, d, pw, target, _ = synthetic_batch_lego(B, 123, "cpu", 800)
+        pw_rows = pw.view(B, 1)
+        ones10 = torch.ones(10)
+
+        def color(t0, t1, n):
+            pos, dirs = O.compute_positions(o, d, t0, t1, "middle")
+            N = B * n
+            pw_s = pw_rows.repeat(1, n).view(N, 1)
+            pos_pe = O.integrated_pe(pos.reshape(N, 3), dirs.reshape(N, 3), pw_s, t0.reshape(N, 1),
+                                     t1.reshape(N, 1), 10, 1.0, True, True, 0.0, mask=ones10)
+            dir_pe = O.barf_pe(dirs.reshape(N, 3), 4, 4.0, True, 1.0)
+            dens, rgb = O.nerf_model_forward(sd, pos_pe, dir_pe, 2, 4, True, False)
+            return O.render_rays(dens.view(B, n), rgb.view(B, n, 3), t1 - t0, 3.0, 1 / 3)
+
+        def step():
+            interval = (far - near) / K
+            t = O.linspace_t(near, far, K).unsqueeze(0).repeat(B, 1) + torch.rand(B, K) * interval
+            t = t + torch.rand(B, 1) * interval * -1.0          # uniform_sampling_offset_size = -1
+            t0, t1 = O.intervals(t, far)
+            rgb_c, w = color(t0, t1, K)
+            f0, f1, _ = O.sample_t_pdf_weighted_batched(t0, w.detach(), (t1 - t0), S, far)
+            rgb_f, _ = color(f0, f1, S)
+            loss = torch.nn.functional.mse_loss(rgb_f, target) + torch.nn.functional.mse_loss(rgb_c, target)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+        per_step = B * (K + S)
+        desc = (f"training steps of {B} rays x (64 coarse + 128 fine) samples: masked IPE, shared NerfModel "
+                f"fwd+bwd on both passes, pdf resample, Adam")
+    else:
+        ren = build_model("cpu") if workload == "n2v" else None
+        if ren is None:
+            return None
+        sd = {k: v.clone().requires_grad_(True) for k, v in ren.model_radiance.state_dict().items()}
+        B = 1024
+        o, d, pw, target = synthetic_batch(B, 123, "cpu")
+
+        def step():
+            interval = (FAR - NEAR) / SAMPLES
+            t = O.linspace_t(NEAR, FAR, SAMPLES).unsqueeze(0).repeat(B, 1) + torch.rand(B, SAMPLES) * interval
+            t0, t1 = O.intervals(t, FAR)
+            pos, dirs = O.compute_positions(o, d, t0, t1, "middle")
+            pos_pe = O.fourier_features(pos.view(-1, 3), 10, 2 * math.pi)
+            dir_pe = O.fourier_features(dirs.reshape(-1, 3), 4, 1.0)
+            dens, rgb = O.nerf_model_forward(sd, pos_pe, dir_pe, 2, 4, True, True)
+            out, _ = O.render_rays(dens.view(B, SAMPLES), rgb.view(B, SAMPLES, 3), t1 - t0, 3.0, 7.0)
+            loss = torch.nn.functional.mse_loss(out, target)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+        per_step = B * SAMPLES
+        desc = f"training steps of {B} rays x {SAMPLES} samples (Fourier PE, NerfModel fwd+bwd, compositing, Adam)"
     opt = torch.optim.Adam(list(sd.values()), lr=5e-4, eps=1e-5)
-    B = 512
-    o, d, pw, target = synthetic_batch(B, 123, "cpu")
-
-    def step():
-        interval = (FAR - NEAR) / SAMPLES
-        t = O.linspace_t(NEAR, FAR, SAMPLES).unsqueeze(0).repeat(B, 1) + torch.rand(B, SAMPLES) * interval
-        t0, t1 = O.intervals(t, FAR)
-        pos, dirs = O.compute_positions(o, d, t0, t1, "middle")
-        pos_pe = O.fourier_features(pos.view(-1, 3), 10, 2 * math.pi)
-        dir_pe = O.fourier_features(dirs.reshape(-1, 3), 4, 1.0)
-        dens, rgb = O.nerf_model_forward(sd, pos_pe, dir_pe, 2, 4, True, True)
-        out, _ = O.render_rays(dens.view(B, SAMPLES), rgb.view(B, SAMPLES, 3), t1 - t0, 3.0, 7.0)
-        loss = torch.nn.functional.mse_loss(out, target)
-        opt.zero_grad()
-        loss.backward()
-        opt.step()
-
     step()  # warm-up
     n, t_start = 0, time.perf_counter()
     while True:
@@ -284,26 +343,64 @@ def cpu_baseline(seconds: float = 15.0):
         el = time.perf_counter() - t_start
         if el >= seconds or n >= 50:
             break
-    cpu_model = platform.processor() or platform.machine()
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    cpu_model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
-    return {"value": n * B * SAMPLES / el, "unit": "ray-samples/s", "cores": threads, "kind": "port",
-            "sample": f"{n} training steps of {B} rays x {SAMPLES} samples (same model/config, torch CPU fp32, "
-                      f"{el:.1f} s) on {cpu_model}"}
+    return {"value": n * per_step / el, "unit": "ray-samples/s", "cores": threads, "kind": "port",
+            "sample": f"{n} {desc}; oracle/nerf_oracle.py on torch CPU fp32, {el:.1f} s on {_cpu_model_name()}"}
+
+
+def _roofline(ks_fn: dict, x3: bool, steps: int, workload: str):
+    """Roofline object for the MFMA kernel FUNCTION with the most device time in the timed region
+    (launches grouped by HIP kernel function, as rocprofv3 reports them: the fused kernel's forward
+    and input-gradient-chain launches are one entry)."""
+    peak = X3_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
+    mfma_fns = ("mlp_fused_fwd_kernel", "linear_nt_x3_glds_kernel", "linear_nt_x3_kernel", "linear_wgrad_x3_wide_kernel",
+                "linear_wgrad_x3_kernel", "linear_nt_kernel", "linear_wgrad_kernel")
+    cands = [k for k in mfma_fns if k in ks_fn]
+    if not cands:
+        return None
+    dom = max(cands, key=lambda k: ks_fn[k]["ms"])
+    r = ks_fn[dom]
+    n = max(r["launches"], 1)
+    avg_ms, avg_flops, avg_bytes = r["ms"] / n, r["flops"] / n, r["bytes"] / n
+    achieved = avg_flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
+    intensity = avg_flops / avg_bytes if avg_bytes > 0 else float("inf")
+    ridge = peak * 1e12 / (HBM_PEAK_GBS * 1e9)
+    hbm_bound = intensity < ridge
+    achieved_gbs = avg_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", f"traffic_{workload}_{dom}.json")
+    if os.path.exists(tfile):
+        with open(tfile) as f:
+            traffic = json.load(f).get("bytes_per_launch")
+    pmc = None
+    pfile = os.path.join(ROOT, "profiles", f"pmc_{workload}_{dom}.json")
+    if os.path.exists(pfile):
+        with open(pfile) as f:
+            pmc = json.load(f)
+    total_ms = sum(v["ms"] for v in ks_fn.values())
+    return {"kernel": dom, "roles": r["tags"],
+            "precision": "3 x bf16 MFMA; peak = bf16 dense / 3" if x3 else "fp32 MFMA 32x32x2",
+            "bound": "hbm" if hbm_bound else "mfma",
+            "achieved": achieved_gbs if hbm_bound else achieved,
+            "peak": HBM_PEAK_GBS if hbm_bound else peak,
+            "unit": "GB/s" if hbm_bound else "TFLOP/s",
+            "frac": achieved_gbs / HBM_PEAK_GBS if hbm_bound else achieved / peak,
+            "traffic": traffic,
+            "traffic_unit": "bytes per launch (PMC 2*FETCH_SIZE + WRITE_SIZE, gfx950-corrected)",
+            "arithmetic_intensity": intensity, "ridge": ridge,
+            "achieved_tflops": achieved, "peak_tflops": peak,
+            "attainable_tflops": min(peak, intensity * HBM_PEAK_GBS * 1e9 / 1e12),
+            "avg_launch_us": avg_ms * 1e3, "avg_flops_per_launch": avg_flops,
+            "avg_bytes_per_launch": avg_bytes, "launches_per_step": r["launches"] / steps,
+            "share_of_timed_kernel_time": r["ms"] / total_ms if total_ms > 0 else None,
+            "pmc": pmc}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="n2v", choices=tuple(WORKLOADS))
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", default="mip", choices=tuple(WORKLOADS))
     ap.add_argument("--mode", default="train", choices=("train", "render"),
                     help="train: forward + backward + all-reduce + Adam per step (the headline metric); "
                          "render: the forward pass only, without autograd (BASELINE.json's render metric)")
@@ -381,38 +478,10 @@ def main():
     samples_total = samples_per_gpu * world * args.steps
     value = samples_total / elapsed
     ks = timer.summary()
+    ks_fn = timer.summary(by="fn")
     from nerf_amd.mlp import matmul_precision
     x3 = matmul_precision() == "x3"
-    nt_name = "linear_nt_x3" if x3 else "linear_nt"
-    peak = X3_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
-    # the roofline kernel: the MFMA kernel with the most device time per step (the fused field-MLP
-    # forward, the input-gradient GEMMs or the weight-gradient GEMMs)
-    cands = [k for k in ("mlp_fused_fwd", "mlp_fused_dgrad", nt_name, "linear_wgrad_x3" if x3 else "linear_wgrad")
-             if k in ks]
-    dom = max(cands, key=lambda k: ks[k]["ms"]) if cands else nt_name
-    nt = ks.get(dom, {"launches": 0, "flops": 0.0, "bytes": 0.0, "ms": 0.0})
-    nt_avg_ms = nt["ms"] / max(nt["launches"], 1)
-    nt_avg_flops = nt["flops"] / max(nt["launches"], 1)
-    nt_avg_bytes = nt["bytes"] / max(nt["launches"], 1)
-    achieved = (nt_avg_flops / (nt_avg_ms * 1e-3)) / 1e12 if nt_avg_ms > 0 else 0.0
-    # which roof binds: algorithmic FLOPs per algorithmic byte against the ridge point of the MFMA
-    # peak and HBM (e.g. the weight gradients: 53 flop/B < 105 at split precision -> HBM-bound)
-    intensity = nt_avg_flops / nt_avg_bytes if nt_avg_bytes > 0 else float("inf")
-    ridge = peak * 1e12 / (HBM_PEAK_GBS * 1e9)
-    hbm_bound = intensity < ridge
-    achieved_gbs = nt_avg_bytes / (nt_avg_ms * 1e-3) / 1e9 if nt_avg_ms > 0 else 0.0
-    dom_desc = {
-        "mlp_fused_fwd": "the whole field-MLP forward in one launch",
-        "mlp_fused_dgrad": "the backward's input-gradient chain in one launch",
-        nt_name: "input-gradient GEMMs",
-        "linear_wgrad_x3": "weight-gradient GEMMs", "linear_wgrad": "weight-gradient GEMMs",
-    }.get(dom, dom)
-
-    traffic = None
-    tfile = os.path.join(ROOT, "profiles", f"traffic_{dom}.json")
-    if args.workload == "n2v" and os.path.exists(tfile):
-        with open(tfile) as f:
-            traffic = json.load(f).get("bytes_per_launch")
+    roofline = _roofline(ks_fn, x3, args.steps, args.workload)
 
     # HBM roofline of the bandwidth-bound kernels BASELINE.json's north_star names (positional
     # encoding + alpha compositing): algorithmic bytes (kernels.py, per launch) / event-timed duration
@@ -445,22 +514,7 @@ def main():
                        "rays_per_gpu": wl["rays"], "samples_per_ray": wl["coarse"] + wl["fine"],
                        "coarse_samples": wl["coarse"], "fine_samples": wl["fine"], "global_rays": wl["rays"] * world,
                        "parallelism": f"ray-batch dp{world}" + (" (RCCL all-reduce)" if world > 1 else "")},
-            "roofline": {"kernel": (f"{dom} (" + ("3 x bf16 MFMA; peak = bf16 dense / 3"
-                                                   if x3 else "fp32 MFMA 32x32x2")
-                                    + f": {dom_desc}; algorithmic fp32 GEMM flops and algorithmic bytes, "
-                                    "bound = the lower roof at this kernel's arithmetic intensity)"),
-                         "bound": "hbm" if hbm_bound else "mfma",
-                         "achieved": achieved_gbs if hbm_bound else achieved,
-                         "peak": HBM_PEAK_GBS if hbm_bound else peak,
-                         "unit": "GB/s" if hbm_bound else "TFLOP/s",
-                         "frac": achieved_gbs / HBM_PEAK_GBS if hbm_bound else achieved / peak,
-                         "traffic": traffic,
-                         "arithmetic_intensity": intensity, "ridge": ridge,
-                         "achieved_tflops": achieved, "peak_tflops": peak,
-                         "attainable_tflops": min(peak, intensity * HBM_PEAK_GBS * 1e9 / 1e12),
-                         "avg_launch_us": nt_avg_ms * 1e3, "avg_flops_per_launch": nt_avg_flops,
-                         "avg_bytes_per_launch": nt_avg_bytes,
-                         "launches_per_step": nt["launches"] / args.steps},
+            "roofline": roofline,
             "roofline_hbm": {"kernel": "encode_fwd + composite_fwd + composite_bwd (positional encoding and "
                                        "alpha compositing; algorithmic bytes per launch)",
                              "bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -471,12 +525,17 @@ def main():
                             "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["ms"] > 0 else 0.0,
                             "gbs": (v["bytes"] / (v["ms"] * 1e-3) / 1e9) if v["ms"] > 0 else 0.0}
                         for k, v in ks.items()},
+            "kernel_functions": {k: {"launches_per_step": v["launches"] / args.steps,
+                                     "ms_per_step": v["ms"] / args.steps, "roles": v["tags"]}
+                                 for k, v in ks_fn.items()},
             "mlp_tflops_per_step": (flops_per_sample(ren) / (3.0 if render else 1.0)) * samples_per_gpu
                                    / (elapsed / args.steps) / 1e12,
             ("mean_rgb" if render else "final_loss"): final_loss,
         }
-        if world == 1 and not args.no_cpu_baseline and args.workload == "n2v" and not render:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        if world == 1 and not args.no_cpu_baseline and not render:
+            cb = cpu_baseline(args.workload, args.cpu_seconds)
+            if cb is not None:
+                out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

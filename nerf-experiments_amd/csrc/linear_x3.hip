@@ -309,11 +309,7 @@ template <int EPI, int JN>
 __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int ntiles) {
     constexpr int BM = 256, BN = 128 * JN;
     constexpr int ABYTES = BM * 128, WBYTES = BN * 128;
-#ifdef NERF_ROLE_SPLIT
-    constexpr int LW = 4;                       // waves 0..LW-1 issue the DMA, the others the stores
-#else
-    constexpr int LW = 8;
-#endif
+    constexpr int LW = 8;                       // waves issuing the DMA (all; a 4/4 loader/storer split measured slower)
     constexpr int EW = LW == 8 ? 8 : 8 - LW;    // waves running the epilogue's global phase
     constexpr int QA = BM / (8 * LW);           // A DMA instructions per loader wave per chunk (8 rows each)
     constexpr int QW = BN / (8 * LW);           // W DMA instructions per loader wave per chunk
@@ -600,9 +596,7 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         barrier();                      // chunk g visible to every wave
-#ifndef NERF_DIAG_NOCOMPUTE
         compute(as, ws);
-#endif
         barrier();                      // every wave done reading chunk g's stages
         if (++c_chunk == nchunks) {
             epilogue(as, ws);

@@ -49,10 +49,6 @@ constexpr int TILE = NWAVE / 2 * SPW;      // samples per workgroup tile
 constexpr int KBMAX = 8;                   // register-fed 32-deep k-blocks (256 features)
 constexpr unsigned OOB = 0x80000000u;      // buffer offset past every num_records: load 0 / drop store
 constexpr int RSRC_W3 = 0x00020000;
-// vector-memory instructions per chunk for its biases (2 x b128)
-#ifndef NERF_DIAG
-#define NERF_DIAG 0       // timing diagnostics only: 1 no stores, 2 no DMA wait, 4 no barrier, 8 no MFMA
-#endif
 constexpr int EPI_MIN_VM = 2;
 
 struct FusedArgs {
@@ -81,7 +77,6 @@ typedef const uint8_t* cu8ptr_t;
                                                    offsetof(nerf_fused_layer, f) + (size_t)(i) * sizeof(T)))
 
 __device__ __forceinline__ f4 mfma16(bf16x8 a, bf16x8 b, f4 c) {
-    if (NERF_DIAG & 8) return c + a[0] * b[0];
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 // acc += a*b, both operands split hi/lo; small terms first (as linear_x3.hip)
@@ -95,17 +90,6 @@ __device__ __forceinline__ void split8(f8 v, bf16x8& hi, bf16x8& lo) {
     lo = __builtin_convertvector(v - __builtin_convertvector(hi, f8), bf16x8);
 }
 
-// s_waitcnt needs an immediate: n is wave-uniform, so this is a scalar branch ladder (counts
-// above 15 wait for more than necessary, which is always safe)
-__device__ __forceinline__ void wait_vm(int n) {
-    switch (n) {
-#define NERF_W(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-        NERF_W(0) NERF_W(1) NERF_W(2) NERF_W(3) NERF_W(4) NERF_W(5) NERF_W(6) NERF_W(7) NERF_W(8) NERF_W(9)
-        NERF_W(10) NERF_W(11) NERF_W(12) NERF_W(13) NERF_W(14)
-#undef NERF_W
-        default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-    }
-}
 __device__ __forceinline__ void barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -211,11 +195,9 @@ __device__ __forceinline__ void chunk_epilogue(Ctx& c, LayerState& st, int nbc, 
         const unsigned off = (unsigned)col < (unsigned)colok ? (sec ? st.row_off2 : st.row_off) + (unsigned)col * 4u
                                                              : OOB;   // nbc = -1: col < 0
         const unsigned coff = (c.half == 0 && g == 0 && st.col_idx == 32 * nbc) ? st.sample_off : OOB;
-        if (!(NERF_DIAG & 1)) {
-            __builtin_amdgcn_raw_buffer_store_b128(v, sec ? st.ro2 : st.ro, off, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), st.rc, coff, 0, 0);
-            count_vm(c, 2);
-        }
+        __builtin_amdgcn_raw_buffer_store_b128(v, sec ? st.ro2 : st.ro, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), st.rc, coff, 0, 0);
+        count_vm(c, 2);
     } else if constexpr (PART == 1) {
         // NERF_EPI_MASKOUT layout: column 32 nb + 16 bb + 4 g + r is bit 4 bb + g of byte (nb & 3)
         // of word 2 r + (nb >> 2) of the row; lane group g keeps the byte of r = g
@@ -320,15 +302,11 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int sample) {
 
     f4 p = {};
     for (int nbc = 0; nbc < st.NB; ++nbc) {
-#if NERF_DIAG
-        if (!(NERF_DIAG & 2)) wait_vm(c.after_last);
-#else
         // this chunk's own DMA share has landed: every chunk issues its successor's DMA and then
         // at least EPI_MIN_VM vector-memory ops (the epilogue stores; more at layer boundaries,
         // which only makes this wait stricter), so a constant count is exact or safe
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EPI_MIN_VM) : "memory");
-#endif
-        if (!(NERF_DIAG & 4)) barrier();               // ... and everyone else's; the other slot is free
+        barrier();               // ... and everyone else's; the other slot is free
         const int slot = c.cur;
         // this wave's 16-row block of the chunk: [kb][block][hi 1 KB | lo 1 KB]
         const char* S = c.smem + slot * SLOT_BYTES + c.half * 2048 + c.lane * 16;
@@ -380,10 +358,8 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int sample) {
     if (c.half == 0) {
         const u2 o = *reinterpret_cast<const u2*>(c.mx + c.lane * 8);
         const unsigned off = st.row_ok ? (unsigned)(sample * 32 + 8 * g) : OOB;
-        if (!(NERF_DIAG & 1)) {
-            __builtin_amdgcn_raw_buffer_store_b64(u2{st.mw[0] | o.x, st.mw[1] | o.y}, st.rm, off, 0, 0);
-            count_vm(c, 1);
-        }
+        __builtin_amdgcn_raw_buffer_store_b64(u2{st.mw[0] | o.x, st.mw[1] | o.y}, st.rm, off, 0, 0);
+        count_vm(c, 1);
     }
 #pragma unroll
     for (int kb = 0; kb < KBMAX; ++kb) {

@@ -23,27 +23,33 @@ class KernelTimer:
     Events are recorded on the same stream the kernel is launched on (torch's
     current stream, which is the stream passed to the C-ABI), so
     elapsed_time() is the kernel's device duration.  Records (tag, flops, algorithmic
-    HBM bytes, start, end)."""
+    HBM bytes, start, end, kernel function).  ``tag`` names the role of a launch (e.g. the
+    fused forward vs the input-gradient chain); ``fn`` is the HIP kernel function it runs, the
+    name rocprofv3's kernel trace reports, so summary(by="fn") lines up with the rocprof stats."""
 
     def __init__(self):
         self.records = []
 
-    def bracket(self, tag: str, flops: float = 0.0, nbytes: float = 0.0):
+    def bracket(self, tag: str, flops: float = 0.0, nbytes: float = 0.0, fn: str | None = None):
         start = torch.cuda.Event(enable_timing=True)
         end = torch.cuda.Event(enable_timing=True)
         start.record()
-        self.records.append((tag, flops, nbytes, start, end))
+        self.records.append((tag, flops, nbytes, start, end, fn or tag))
         return end
 
-    def summary(self):
+    def summary(self, by: str = "tag"):
         out = {}
-        for tag, flops, nbytes, s, e in self.records:
+        for tag, flops, nbytes, s, e, fn in self.records:
             ms = s.elapsed_time(e)
-            d = out.setdefault(tag, {"launches": 0, "flops": 0.0, "bytes": 0.0, "ms": 0.0})
+            d = out.setdefault(fn if by == "fn" else tag,
+                               {"launches": 0, "flops": 0.0, "bytes": 0.0, "ms": 0.0, "tags": set()})
             d["launches"] += 1
             d["flops"] += flops
             d["bytes"] += nbytes
             d["ms"] += ms
+            d["tags"].add(tag)
+        for d in out.values():
+            d["tags"] = sorted(d["tags"])
         return out
 
 
@@ -89,7 +95,8 @@ def composite_fwd(density: torch.Tensor, density_stride: int, color: torch.Tenso
     w = torch.empty(n_rays, samples_per_ray, device=dev, dtype=torch.float32) if want_weights else None
     n = n_rays * samples_per_ray
     # algorithmic bytes: sigma, rgb, delta in (+ weights out) per sample, rgb out per ray
-    end = TIMER.bracket("composite_fwd", nbytes=n * (20 + (4 if want_weights else 0)) + 12 * n_rays) \
+    end = TIMER.bracket("composite_fwd", nbytes=n * (20 + (4 if want_weights else 0)) + 12 * n_rays,
+                        fn="composite_fwd_kernel") \
         if TIMER is not None else None
     st = _lib.load().nerf_composite_fwd(_ptr(density), density_stride, _ptr(color), color_stride, _ptr(dist),
                                         n_rays, samples_per_ray, scale_a, scale_b, int(act), density_shift,
@@ -109,7 +116,7 @@ def composite_bwd(density, density_stride, color, color_stride, dist, n_rays, sa
     # algorithmic bytes: sigma, rgb, delta (+ dL/dw) in, dL/dsigma, dL/drgb out per sample; dL/drgb in per ray
     nb = n * (20 + (4 if grad_weights is not None else 0) + (4 if grad_density is not None else 0)
               + (12 if grad_color is not None else 0)) + 12 * n_rays
-    end = TIMER.bracket("composite_bwd", nbytes=nb) if TIMER is not None else None
+    end = TIMER.bracket("composite_bwd", nbytes=nb, fn="composite_bwd_kernel") if TIMER is not None else None
     st = _lib.load().nerf_composite_bwd(_ptr(density), density_stride, _ptr(color), color_stride, _ptr(dist),
                                         n_rays, samples_per_ray, scale_a, scale_b, int(act), density_shift,
                                         _ptr(grad_rgb), _ptr(grad_weights), _ptr(grad_density), gd_stride,
@@ -225,7 +232,8 @@ def encode_fwd(params: NerfPEParams, out_dim: int, *, x=None, xdir=None, ray_o=N
         else:
             per_sample += 4 + (4 if (params.query == 1 or params.kind == 1) else 0)
             per_ray = 24 + (4 if params.kind == 1 else 0)
-        end = TIMER.bracket("encode_fwd", nbytes=n_samples * per_sample + n_rays * per_ray)
+        end = TIMER.bracket("encode_fwd", nbytes=n_samples * per_sample + n_rays * per_ray,
+                            fn="encode_fwd_lds_kernel" if ld <= 128 else "encode_fwd_kernel")
     st = _lib.load().nerf_encode_fwd(ctypes.byref(params), _ptr(x), _ptr(xdir), _ptr(ray_o), _ptr(ray_d),
                                      _ptr(t_start), _ptr(t_end), _ptr(pixel_width), n_samples, samples_per_ray,
                                      n_rays, _ptr(out), ld, _stream(out.device))
@@ -349,7 +357,8 @@ def linear_fwd(segs, M: int, W: torch.Tensor, ldw: int, N: int, bias: torch.Tens
                epilogue: int, aux: torch.Tensor | None = None, w_row_offset: int = 0) -> None:
     arr = make_segs(segs)
     wptr = W.data_ptr() + w_row_offset * ldw * 4
-    end = TIMER.bracket("linear_nt", 2.0 * M * N * ldw, _segs_bytes(segs, M) + 4.0 * M * N + 4.0 * N * ldw) \
+    end = TIMER.bracket("linear_nt", 2.0 * M * N * ldw, _segs_bytes(segs, M) + 4.0 * M * N + 4.0 * N * ldw,
+                        fn="linear_nt_kernel") \
         if TIMER is not None else None
     st = _lib.load().nerf_linear_fwd(arr, len(segs), M, wptr, ldw, N, _ptr(bias), _ptr(out), out.stride(0),
                                      epilogue, _ptr(aux), aux.stride(0) if aux is not None else 0,
@@ -363,7 +372,8 @@ def linear_wgrad(dY: torch.Tensor, N4: int, segs, M: int, workspace: torch.Tenso
     arr = make_segs(segs)
     kt = sum(k for _, k, _ in segs)
     # algorithmic bytes: dY and X read once, dW written once (the split-M slabs are the kernel's)
-    end = TIMER.bracket("linear_wgrad", 2.0 * M * N4 * kt, 4.0 * M * N4 + _segs_bytes(segs, M) + 4.0 * N4 * kt) \
+    end = TIMER.bracket("linear_wgrad", 2.0 * M * N4 * kt, 4.0 * M * N4 + _segs_bytes(segs, M) + 4.0 * N4 * kt,
+                        fn="linear_wgrad_kernel") \
         if TIMER is not None else None
     st = _lib.load().nerf_linear_wgrad(_ptr(dY), dY.stride(0), N4, arr, len(segs), M, _ptr(workspace),
                                        workspace.numel() * workspace.element_size(), _stream(dY.device))
@@ -389,7 +399,8 @@ def linear_fwd_x3(segs, M: int, Wx: torch.Tensor, ldw: int, N: int, bias: torch.
     weights of nerf_pack_weight_x3 ([rows][ldw/32][hi 32 | lo 32] bf16)."""
     arr = make_segs(segs)
     off = w_row_offset * ldw * 2 * 2
-    end = TIMER.bracket("linear_nt_x3", 2.0 * M * N * ldw, _segs_bytes(segs, M) + 4.0 * M * N + 4.0 * N * ldw) \
+    end = TIMER.bracket("linear_nt_x3", 2.0 * M * N * ldw, _segs_bytes(segs, M) + 4.0 * M * N + 4.0 * N * ldw,
+                        fn="linear_nt_x3_glds_kernel" if N <= 256 else "linear_nt_x3_kernel") \
         if TIMER is not None else None
     st = _lib.load().nerf_linear_fwd_x3(arr, len(segs), M, Wx.data_ptr() + off, ldw, N, _ptr(bias), _ptr(out),
                                         out.stride(0), epilogue, _ptr(aux), aux.stride(0) if aux is not None else 0,
@@ -403,7 +414,11 @@ def linear_wgrad_x3(dY: torch.Tensor, N4: int, segs, M: int, workspace: torch.Te
     arr = make_segs(segs)
     kt = sum(k for _, k, _ in segs)
     # algorithmic bytes: dY and X read once, dW written once (the split-M slabs are the kernel's)
-    end = TIMER.bracket("linear_wgrad_x3", 2.0 * M * N4 * kt, 4.0 * M * N4 + _segs_bytes(segs, M) + 4.0 * N4 * kt) \
+    # the C side runs one 256 x 256 tile per M split when the layer fits it (nerf_linear_wgrad_x3)
+    kpad = sum(pad32(k) for _, k, _ in segs)
+    wide = (N4 > 128 or kpad > 128) and N4 <= 256 and kpad <= 256
+    end = TIMER.bracket("linear_wgrad_x3", 2.0 * M * N4 * kt, 4.0 * M * N4 + _segs_bytes(segs, M) + 4.0 * N4 * kt,
+                        fn="linear_wgrad_x3_wide_kernel" if wide else "linear_wgrad_x3_kernel") \
         if TIMER is not None else None
     st = _lib.load().nerf_linear_wgrad_x3(_ptr(dY), dY.stride(0), N4, arr, len(segs), M, _ptr(workspace),
                                           workspace.numel() * workspace.element_size(), _stream(dY.device))

@@ -5,8 +5,10 @@ A field MLP (NerfModel, NerfModelINGP, ...) is lowered once into a list of
 the padded position encoding ("pos"), the (per-sample or per-ray) direction
 encoding ("dir") or an earlier layer's output ("act", j) — so the reference's
 ``th.cat`` copies (model_interpolation_architecture.py:111-125) never exist.
-Weights are repacked into the kernels' K-padded layout (and its transpose for
-the input-gradient GEMMs) only when a parameter's version counter changed.
+Weights are repacked into the kernels' K-padded layout (forward) and its transpose
+(input-gradient GEMMs) on every call that uses them: one small gather launch per layer, never
+keyed on the parameter's version counter (``p.data`` updates and fused optimizers do not bump
+it, and a stale pack would silently train on old weights).
 
 ``MLPFunction`` is one autograd node for the whole network:
   forward : one ``nerf_linear_fwd`` launch per layer (bias + ReLU fused), all
@@ -86,12 +88,8 @@ class LayerPlan:
     col_map: torch.Tensor | None = None
     Wp: torch.Tensor | None = None
     Wt: torch.Tensor | None = None
-    packed_version: tuple = ()
     Wpx: torch.Tensor | None = None
     Wtx: torch.Tensor | None = None
-    packed_version_x3: tuple = ()
-    packed_version_t: tuple = ()
-    packed_version_x3t: tuple = ()
 
     def finalize(self, device):
         self.N = self.module.out_features
@@ -116,38 +114,27 @@ class LayerPlan:
         self.col_map = torch.tensor(cm, dtype=torch.int32, device=device)
         self.Wp = torch.empty(K.pad128(self.N), self.Kp, device=device, dtype=torch.float32)
         self.Wt = torch.empty(K.pad128(self.Kp) + 128, self.ldwt, device=device, dtype=torch.float32)
-        self.packed_version = self.packed_version_t = ()
         self.Wpx = self.Wtx = None
-        self.packed_version_x3 = self.packed_version_x3t = ()
 
     def pack(self, precision: str = "fp32", forward: bool = True):
-        """Refresh the packed weights whose parameter version changed: the forward layouts (Wp /
-        Wpx; skipped with forward=False, when the fused forward kernel runs the layer) and the
-        transposed ones the input-gradient GEMMs use (Wt / Wtx)."""
-        w = self.module.weight
-        ver = (w._version, w.data_ptr())
+        """Pack the current weights: the forward layouts (Wp / Wpx) when forward=True, the transposed
+        ones the input-gradient GEMMs use (Wt / Wtx) when forward=False.  Every call packs (no
+        version-keyed cache: see the module docstring)."""
+        w = self.module.weight.detach().contiguous()
         x3 = precision == "x3"
         # in split precision the fp32 packs only serve GEMMs with <= 32 output columns: this
         # layer's forward (N <= 32) and the input gradients of sources <= 32 columns wide
-        p = forward and (not x3 or self.N <= 32) and ver != self.packed_version
-        t = (not x3 or any(s.k_pad <= 32 for s in self.sources)) and ver != self.packed_version_t
+        p = forward and (not x3 or self.N <= 32)
+        t = (not forward) and (not x3 or any(s.k_pad <= 32 for s in self.sources))
         if p or t:
-            K.pack_weight(w.detach().contiguous(), self.col_map, self.Kp, self.Wp if p else None,
-                          self.Wt if t else None, self.ldwt)
-            self.packed_version = ver if p else self.packed_version
-            self.packed_version_t = ver if t else self.packed_version_t
+            K.pack_weight(w, self.col_map, self.Kp, self.Wp if p else None, self.Wt if t else None, self.ldwt)
         if x3:
-            px = forward and ver != self.packed_version_x3
-            tx = ver != self.packed_version_x3t
-            if px or tx:
-                if self.Wpx is None:
-                    dev = self.Wp.device
-                    self.Wpx = torch.empty(self.Wp.shape[0], 2 * self.Wp.shape[1], device=dev, dtype=torch.bfloat16)
-                    self.Wtx = torch.empty(self.Wt.shape[0], 2 * self.Wt.shape[1], device=dev, dtype=torch.bfloat16)
-                K.pack_weight_x3(w.detach().contiguous(), self.col_map, self.Kp, self.Wpx if px else None,
-                                 self.Wtx if tx else None, self.ldwt)
-                self.packed_version_x3 = ver if px else self.packed_version_x3
-                self.packed_version_x3t = ver if tx else self.packed_version_x3t
+            if self.Wpx is None:
+                dev = self.Wp.device
+                self.Wpx = torch.empty(self.Wp.shape[0], 2 * self.Wp.shape[1], device=dev, dtype=torch.bfloat16)
+                self.Wtx = torch.empty(self.Wt.shape[0], 2 * self.Wt.shape[1], device=dev, dtype=torch.bfloat16)
+            K.pack_weight_x3(w, self.col_map, self.Kp, self.Wpx if forward else None,
+                             None if forward else self.Wtx, self.ldwt)
 
     def gemm(self, precision: str, segs, M: int, transpose: bool, N: int, bias, out, epi, aux=None,
              row_offset: int = 0):

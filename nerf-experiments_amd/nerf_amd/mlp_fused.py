@@ -25,6 +25,20 @@ import torch
 from . import _lib
 from . import kernels as K
 
+def _pack_image(f) -> None:
+    """Rebuild a fused image from the plan's current parameters (one gather launch, ~2.6 MB for
+    NerfModel).  Runs before EVERY launch that reads the image: a cache keyed on the parameters'
+    version counters misses ``p.data`` updates and fused optimizers, and would then train on stale
+    weights without any error (in training the weights change every step anyway)."""
+    ps = []
+    for lp in f.plan.layers:
+        ps += [lp.module.weight, lp.module.bias]
+    arr = (ctypes.c_void_p * len(ps))(*[p.detach().contiguous().data_ptr() for p in ps])
+    st = _lib.load().nerf_fused_pack(arr, len(ps), f.map_src.data_ptr(), f.map_dst.data_ptr(), f.map_src.numel(),
+                                     f.image.data_ptr(), K._stream(f.device))
+    _lib.check(st, "nerf_fused_pack")
+
+
 FUSED_TYPES = {(0, 1): 1, (0, 2): 2, (4, 0): 3, (8, 0): 6, (8, 1): 7, (8, 2): 8}   # (kbr, kbh) -> type
 ENABLED = os.environ.get("NERF_FUSED", "1") != "0"     # A/B switch (bench, tests)
 
@@ -103,7 +117,6 @@ class FusedForward:
         self.image = torch.zeros(off // 2, dtype=torch.bfloat16, device=device)
         self.map_src = torch.from_numpy(np.concatenate(src_codes).astype(np.int32)).to(device)
         self.map_dst = torch.from_numpy(np.concatenate(dst_codes).astype(np.int32)).to(device)
-        self.version = None
 
     @staticmethod
     def _maps(idx, lp, kbr, hbm, nb, units, off, bias_off):
@@ -148,17 +161,7 @@ class FusedForward:
         return np.concatenate(srcs), np.concatenate(dsts)
 
     def pack(self):
-        ps = []
-        for lp in self.plan.layers:
-            ps += [lp.module.weight, lp.module.bias]
-        ver = tuple((p._version, p.data_ptr()) for p in ps)
-        if ver == self.version:
-            return
-        arr = (ctypes.c_void_p * len(ps))(*[p.data_ptr() for p in ps])
-        st = _lib.load().nerf_fused_pack(arr, len(ps), self.map_src.data_ptr(), self.map_dst.data_ptr(),
-                                         self.map_src.numel(), self.image.data_ptr(), K._stream(self.device))
-        _lib.check(st, "nerf_fused_pack")
-        self.version = ver
+        _pack_image(self)
 
     def run(self, M: int, pos: torch.Tensor, dirs: torch.Tensor | None, dir_rd: int, acts, masks, col_outs):
         """Launch on the current stream.  acts[l]: [M, out_ld] fp32 or None (not stored),
@@ -200,7 +203,8 @@ class FusedForward:
             nbytes += sum(4.0 * d.seg_k[si] * d.seg_rows[si] for si in range(d.nseg))
             nbytes += (4.0 * M * acts[idx].shape[1] if acts[idx] is not None else 0.0) \
                 + (32.0 * M if masks[idx] is not None else 0.0) + (4.0 * M if idx in col_outs else 0.0)
-        end = K.TIMER.bracket("mlp_fused_fwd", flops, nbytes + self.image.numel() * self.image.element_size()) \
+        end = K.TIMER.bracket("mlp_fused_fwd", flops, nbytes + self.image.numel() * self.image.element_size(),
+                              fn="mlp_fused_fwd_kernel") \
             if K.TIMER is not None else None
         st = _lib.load().nerf_mlp_fused_fwd(descs, L, self.image.data_ptr(), M, K._stream(self.device))
         if end is not None:
@@ -294,7 +298,6 @@ class FusedInputGrad:
         self.image = torch.zeros(off // 2, dtype=torch.bfloat16, device=device)
         self.map_src = torch.from_numpy(np.concatenate(src_codes).astype(np.int32)).to(device)
         self.map_dst = torch.from_numpy(np.concatenate(dst_codes).astype(np.int32)).to(device)
-        self.version = None
 
     @staticmethod
     def _maps(lp, l, kbr, kbh, n1, x, nb, units, off, bias_off):
@@ -342,17 +345,7 @@ class FusedInputGrad:
         return np.concatenate(srcs), np.concatenate(dsts)
 
     def pack(self):
-        ps = []
-        for lp in self.plan.layers:
-            ps += [lp.module.weight, lp.module.bias]
-        ver = tuple((p._version, p.data_ptr()) for p in ps)
-        if ver == self.version:
-            return
-        arr = (ctypes.c_void_p * len(ps))(*[p.data_ptr() for p in ps])
-        st = _lib.load().nerf_fused_pack(arr, len(ps), self.map_src.data_ptr(), self.map_dst.data_ptr(),
-                                         self.map_src.numel(), self.image.data_ptr(), K._stream(self.device))
-        _lib.check(st, "nerf_fused_pack")
-        self.version = ver
+        _pack_image(self)
 
     def run(self, M: int, g_head: torch.Tensor, dY, masks, g_cols=None, x_out=None):
         """g_head: [M, ld] gradient of the last layer's output; g_cols: {layer: [M, 4] buffer whose
@@ -405,7 +398,8 @@ class FusedInputGrad:
             # algorithmic bytes: HBM-fed gradients and ReLU bits read, dY / encoding gradients written
             nbytes += (4.0 * d.seg_k[0] * d.seg_rows[0] if kbh else 0.0) + (32.0 * M if d.mask_in else 0.0)
             nbytes += 4.0 * M * min(d.ldo, n_out) + (4.0 * M * d.ldo2 if x is not None else 0.0)
-        end = K.TIMER.bracket("mlp_fused_dgrad", flops, nbytes + self.image.numel() * self.image.element_size()) \
+        end = K.TIMER.bracket("mlp_fused_dgrad", flops, nbytes + self.image.numel() * self.image.element_size(),
+                              fn="mlp_fused_fwd_kernel") \
             if K.TIMER is not None else None
         st = _lib.load().nerf_mlp_fused_fwd(descs, S, self.image.data_ptr(), M, K._stream(self.device))
         if end is not None:

@@ -207,6 +207,7 @@ class BarfPositionalEncoding(PositionalEncoding):
         self.space_dimensions = space_dimensions
         self.register_buffer("alpha", th.tensor(float(alpha_start)))
         self._alpha_host = float(th.tensor(float(alpha_start), dtype=th.float32))
+        self._alpha_seen = (id(self.alpha), self.alpha._version)
 
     def update_alpha(self, epoch: float) -> None:
         if epoch < self.alpha_increase_start_epoch:
@@ -219,18 +220,31 @@ class BarfPositionalEncoding(PositionalEncoding):
         # device-side buffer kept for state_dict compatibility; fill_ enqueues, never syncs
         self.alpha.fill_(float(alpha))
         self._alpha_host = float(th.tensor(float(alpha), dtype=th.float32))
+        self._alpha_seen = (id(self.alpha), self.alpha._version)
 
     def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
         super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
         key = prefix + "alpha"
         if key in state_dict:
             self._alpha_host = float(state_dict[key].float().cpu())
+            self._alpha_seen = (id(self.alpha), self.alpha._version)
+
+    def _sync_alpha_host(self) -> None:
+        """Refresh the host mirror of alpha after a write that bypassed update_alpha: assigning a new
+        tensor (``enc.alpha = th.tensor(a)``, what the reference's own update_alpha does) or an
+        in-place write (``enc.alpha.fill_(a)``, ``.to()``/``_apply`` moves).  Detected by the buffer's
+        identity and version counter (a host-side check; the device read happens only then)."""
+        cur = (id(self.alpha), self.alpha._version)
+        if cur != self._alpha_seen:
+            self._alpha_host = float(self.alpha.detach().float().cpu())
+            self._alpha_seen = (id(self.alpha), self.alpha._version)
 
     def compute_mask(self, alpha: th.Tensor) -> th.Tensor:
         vals = barf_mask_values(float(alpha), self.levels)
         return th.tensor(vals * self.space_dimensions, device=alpha.device).view(1, -1)
 
     def mask_values(self) -> list[float]:
+        self._sync_alpha_host()
         return barf_mask_values(self._alpha_host, self.levels)
 
     def _pe_params(self, query: int = 1, pw_mode: int = 2):

@@ -41,6 +41,46 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _worker_unused(rank, world, port, q):
+    """A parameter used by one rank only keeps its gradient (mean over ranks); a parameter no rank
+    used ends with grad None on every rank, as with one process."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                        "nerf-experiments_amd"))
+        from nerf_amd.ddp import GradAllReduce
+        a = torch.nn.Parameter(torch.ones(4))
+        b = torch.nn.Parameter(torch.ones(3))       # rank 1 only
+        c = torch.nn.Parameter(torch.ones(2))       # nobody
+        loss = (a * (rank + 1)).sum() + ((b * 2).sum() if rank == 1 else 0)
+        loss.backward()
+        GradAllReduce([a, b, c])()
+        q.put((rank, a.grad.clone(), None if b.grad is None else b.grad.clone(), c.grad is None))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_unused_parameters_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_unused, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {r: (ga, gb, cnone) for r, ga, gb, cnone in (q.get(timeout=120) for _ in range(2))}
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        ga, gb, cnone = res[r]
+        assert torch.allclose(ga, torch.full((4,), 1.5))
+        assert gb is not None and torch.allclose(gb, torch.full((3,), 1.0))
+        assert cnone
+
+
 def test_grad_allreduce_gloo_world2():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -140,6 +140,30 @@ def test_fused_forward_vs_oracle_subset():
     assert (rgb.cpu()[idx] - oc).abs().max().item() < 2e-4
 
 
+@pytest.mark.parametrize("fused", [True, False])
+def test_weight_updates_outside_autograd_reach_the_kernels(fused):
+    """p.data updates do not bump a parameter's version counter; the packed weight images must
+    still follow them: after p.data.add_, the fused and layer-by-layer forwards equal a
+    fresh model built from the updated state_dict."""
+    model = _model("n2v").to(DEV)
+    g = torch.Generator().manual_seed(9)
+    M = 2048
+    pe = torch.rand(M, 64, generator=g).to(DEV)
+    pe[:, 60:] = 0
+    de = torch.rand(M // 64, 32, generator=g).to(DEV)
+    de[:, 24:] = 0
+    _run(model, pe, de, 64, fused)                       # packs the images once
+    with torch.no_grad():
+        for p in model.parameters():
+            p.data.add_(0.01 * torch.randn(p.shape, generator=g).to(DEV))
+    outs, acts, _, _ = _run(model, pe, de, 64, fused)
+    fresh = _model("n2v").to(DEV)
+    fresh.load_state_dict(model.state_dict())
+    outs2, acts2, _, _ = _run(fresh, pe, de, 64, fused)
+    for a, b in zip(acts, acts2):
+        assert torch.equal(a, b)
+
+
 def _fp64_param_grads(pos_pe, dir_pe, rd, w_out):
     """fp64 torch reference of the same NerfModel plan (dense cat + linear + ReLU)."""
     model = _model("n2v").to(DEV).double()

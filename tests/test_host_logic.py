@@ -139,6 +139,20 @@ def test_barf_alpha_schedule_and_state_dict():
     assert enc.output_dim == 63 and enc.padded_dim == 64
 
 
+def test_barf_alpha_direct_writes_refresh_the_mask():
+    """Writes to the registered alpha buffer that bypass update_alpha (assignment, as the reference's
+    own update_alpha does, and in-place fills) must reach the kernel's mask values."""
+    import torch as th
+    from nerf_amd import BarfPositionalEncoding
+    enc = BarfPositionalEncoding(10, 0.0, 2.0, 6.0, True, 1.0)
+    enc.alpha = th.tensor(3.4)
+    assert enc.mask_values() == O.barf_mask(3.4, 10).tolist()
+    enc.alpha.fill_(7.25)
+    assert enc.mask_values() == O.barf_mask(7.25, 10).tolist()
+    enc.update_alpha(100.0)
+    assert enc.mask_values() == O.barf_mask(10.0, 10).tolist()
+
+
 def test_encoder_dims_and_errors():
     from nerf_amd import (FourierFeatures, IdentityPositionalEncoding, IntegratedBarfFourierFeatures,
                           IntegratedFourierFeatures)

@@ -1,16 +1,17 @@
 #!/bin/bash
-# Kernel-trace stats + HBM traffic (FETCH_SIZE, WRITE_SIZE in separate --pmc passes) of the
-# default bench command.  Usage: tools/profile_bench.sh <outdir> [bench args...]
+# Kernel-trace stats + HBM traffic (FETCH_SIZE, WRITE_SIZE in separate --pmc passes) of a bench
+# command.  Usage: tools/profile_bench.sh <outdir> [bench args...]
 set -u
 OUT=${1:?outdir}; shift
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run --output-format csv \
-  -- python3 bench.py --no-cpu-baseline "$@" > "$OUT/stats.log" 2>&1 || { echo "stats pass failed"; exit 1; }
+  -- python3 bench.py --no-cpu-baseline --steps 50 --warmup 10 "$@" > "$OUT/stats.log" 2>&1 \
+  || { echo "stats pass failed"; exit 1; }
 i=0
 for group in "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $group -d "$OUT/bench_p$i" -o run --output-format csv \
+  timeout -s KILL 180 rocprofv3 --kernel-trace --pmc $group -d "$OUT/bench_p$i" -o run --output-format csv \
     -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 "$@" > "$OUT/bench_p$i.log" 2>&1 \
     || { echo "pmc pass $i failed"; exit 1; }
 done
