@@ -19,6 +19,12 @@ Fixtures:
   ipe_grad.npz   integrated encodings: outputs and gradients w.r.t. position and direction
   garf.npz       GARF RadianceNetwork / ProposalNetwork / GaussAct: checksummed init, outputs, gradients
   pose.npz       CameraExtrinsics (BARF pose refinement): refined rays, rotations, parameter gradients
+  pose_render.npz CameraExtrinsics -> NerfInterpolation._compute_color -> backward: rgb and the pose
+                 parameters' gradients through the whole rendering path (BarfModel's training input)
+  mipnerf.npz    mip_NeRF API: IntegratedFourierFeatures (both variance modes), MipNerfModel forward /
+                 gradients, MipNerf coarse+fine forward with injected coarse t
+  feed.npz       ImagePoseDataset rays + __getitem__ (DataLoader collation) + get_blurred_pixel_colors
+                 on a small in-memory image set; the notebook's 4x2 meshgrid known answer
 
     python tests/golden/make_golden.py [pe composite resample model color cos_kat ipe_grad garf pose]
 """
@@ -57,6 +63,15 @@ def _install_stubs():
         m.DatasetOutput = tuple
         m.ImagePoseDataModule = object
         sys.modules[name] = m
+    # dataset.py imports torchvision at module level (used only by its image loader, which the
+    # feed fixture never calls); pytorch_lightning.callbacks for data_module.py
+    sys.modules.setdefault("torchvision", types.ModuleType("torchvision"))
+    cb = types.ModuleType("pytorch_lightning.callbacks")
+    cb.LambdaCallback = object
+    sys.modules["pytorch_lightning.callbacks"] = cb
+    pl.callbacks = cb
+    pl.LightningDataModule = object
+    pl.Trainer = object
 
 
 def _import_from(subdir: str, names: list[str]):
@@ -377,9 +392,126 @@ def gen_pose():
                         R=f32(R), go=f32(go), gd=f32(gd), drot=f32(m.rotation.grad), dtrans=f32(m.translation.grad))
 
 
+def gen_pose_render():
+    """Pose gradients through the whole rendering path, as BarfModel trains them
+    (barf/model_barf.py:29-92): CameraExtrinsics.forward (model_camera_extrinsics.py:77-85) ->
+    NerfInterpolation._compute_color (model_interpolation.py:356-414) on a BARF NerfModel ->
+    backward to the so3 rotation and translation parameters."""
+    pe, mia, mi, ce = _import_from("barf", ["positional_encodings", "model_interpolation_architecture",
+                                            "model_interpolation", "model_camera_extrinsics"])
+    g = th.Generator().manual_seed(10)
+    th.manual_seed(0)
+    model = mia.NerfModel(4, 256, True, False, 2, pe.BarfPositionalEncoding(10, 6.3, 0, 1, True, 1.0),
+                          pe.BarfPositionalEncoding(4, 4.0, 0, 1, True, 1.0))
+    ren = mi.NerfInterpolation(2.0, 8.0, model, 32, "equidistant", -1.0, "middle")
+    extr = ce.CameraExtrinsics(6, 1e-3, 1e-5, 100)
+    with th.no_grad():
+        extr.rotation.copy_(th.randn(6, 3, generator=g) * 0.05)
+        extr.translation.copy_(th.randn(6, 3, generator=g) * 0.05)
+    B, S = 40, 32
+    o = th.randn(B, 3, generator=g)
+    o = o / th.linalg.vector_norm(o, dim=1, keepdim=True) * 4.03
+    d = th.randn(B, 3, generator=g) * 0.3 - o
+    d = d / th.linalg.vector_norm(d, dim=1, keepdim=True)
+    idx = th.randint(0, 6, (B,), generator=g)
+    pw = th.full((B,), 1 / 555.56)
+    t = 2.0 + th.arange(S, dtype=th.float32).unsqueeze(0).repeat(B, 1) * (6.0 / S) \
+        + th.rand(B, 1, generator=g) * (6.0 / S)
+    t0, t1 = ren._get_intervals(t)
+    o2, d2, _, _ = extr.forward(idx, o, d)
+    rgb, w, _ = ren._compute_color(model, t0, t1, o2, d2, pw, B, S)
+    grgb = th.randn(B, 3, generator=g)
+    (rgb * grgb).sum().backward()
+    np.savez_compressed(os.path.join(OUT, "pose_render.npz"), rotation=f32(extr.rotation),
+                        translation=f32(extr.translation), idx=idx.numpy().astype(np.int64), o=f32(o), d=f32(d),
+                        pw=f32(pw), t0=f32(t0), t1=f32(t1), rgb=f32(rgb), w=f32(w), grgb=f32(grgb),
+                        drot=f32(extr.rotation.grad), dtrans=f32(extr.translation.grad))
+
+
+def gen_mipnerf():
+    """The older mip_NeRF directory's API (mip_NeRF/mip_model.py:11-167, model_interpolation.py)."""
+    mm, mi = _import_from("mip_NeRF", ["mip_model", "model_interpolation"])
+    g = th.Generator().manual_seed(11)
+    out = {}
+    N = 256
+    x = th.rand(N, 3, generator=g) * 4 - 2
+    d = th.randn(N, 3, generator=g)
+    d = d / th.linalg.vector_norm(d, dim=1, keepdim=True)
+    t0 = 1.0 + th.rand(N, 1, generator=g) * 4
+    t1 = t0 + th.rand(N, 1, generator=g) * 0.1 + 1e-3
+    pw = 1 / 1111.1
+    out.update({"x": f32(x), "dir": f32(d), "t0": f32(t0), "t1": f32(t1)})
+    for dv in (False, True):
+        out[f"ipe_dv{int(dv)}"] = f32(mm.IntegratedFourierFeatures(10, 2 * th.pi, dv).forward(x, d, t0, t1, pw))
+    th.manual_seed(0)
+    model = mm.MipNerfModel(4, 256, (True, 10, 4), 2, True)
+    for k, v in model.state_dict().items():
+        out[f"model.sdsum.{k}"] = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+    dens, rgb = model.forward(x, d, t0, t1, pw)
+    gd, gc = th.randn(N, generator=g), th.randn(N, 3, generator=g)
+    ((dens * gd).sum() + (rgb * gc).sum()).backward()
+    out.update({"model.density": f32(dens), "model.rgb": f32(rgb), "model.gd": f32(gd), "model.gc": f32(gc)})
+    for k, prm in model.named_parameters():
+        out[f"model.gradsum.{k}"] = np.array([prm.grad.double().sum().item(), prm.grad.double().abs().sum().item()])
+    # coarse (32) + fine (64 more) forward of MipNerf with the coarse t injected (RNG-free)
+    th.manual_seed(0)
+    ren = mm.MipNerf(1.0, 5.0, 96, 4, (True, 32), (True, 10, 4), 2, distribute_variance=True)
+    B = 16
+    o = th.randn(B, 3, generator=g) * 0.1
+    rd = th.randn(B, 3, generator=g)
+    rd = rd / th.linalg.vector_norm(rd, dim=1, keepdim=True)
+    pwb = th.full((B,), 1 / 1111.1)
+    tc = th.sort(1.0 + th.rand(B, 32, generator=g) * 4, dim=1).values
+    ren._sample_t_coarse = lambda batch_size: ren._get_intervals(tc.clone())
+    rgb_f, rgb_c = ren.forward(o, rd, pwb)
+    out.update({"ren.o": f32(o), "ren.d": f32(rd), "ren.pw": f32(pwb), "ren.tc": f32(tc),
+                "ren.rgb_fine": f32(rgb_f), "ren.rgb_coarse": f32(rgb_c)})
+    np.savez_compressed(os.path.join(OUT, "mipnerf.npz"), **out)
+
+
+def gen_feed():
+    """Training-batch assembly (barf/dataset.py:407-481, 514-557, 613-637; data_module.py:276-369)
+    run by the reference on a small in-memory image set (the Lego data is absent), batches collated
+    the way torch's default DataLoader collate stacks __getitem__ tuples."""
+    ds_mod, dm_mod, ce = _import_from("barf", ["dataset", "data_module", "model_camera_extrinsics"])
+    g = th.Generator().manual_seed(12)
+    out = {"kat_meshgrid_4x2": f32(ds_mod.ImagePoseDataset._get_directions_meshgrid(4, 2, 4.0))}
+    n, H, W, sigmas = 3, 7, 5, [8.0, 4.0, 0.0]
+    images = th.rand(n, H, W, len(sigmas), 3, generator=g)
+    R = ce.CameraExtrinsics.so3_to_SO3(th.randn(n, 3, 1, generator=g))
+    c2w = th.zeros(n, 4, 4)
+    c2w[:, :3, :3] = R
+    c2w[:, :3, 3] = th.randn(n, 3, generator=g) * 4
+    c2w[:, 3, 3] = 1
+    focal = W / 2 / np.tan(0.6911112 / 2)
+    ds = ds_mod.ImagePoseDataset.__new__(ds_mod.ImagePoseDataset)
+    meshgrid = ds_mod.ImagePoseDataset._get_directions_meshgrid(H, W, focal)
+    ray_o, ray_d = ds_mod.ImagePoseDataset._meshgrid_to_world(meshgrid, c2w)
+    cam_o, cam_d = ds_mod.ImagePoseDataset._get_cam_origs_and_directions(c2w)
+    cam_on, _, ray_on, ray_dn = ds_mod.ImagePoseDataset._apply_noise(cam_o, cam_d, ray_o, ray_d, 0.1, 0.2, 3)
+    ds.camera_to_worlds, ds.camera_origins, ds.camera_origins_noisy = c2w, cam_o, cam_on
+    ds.ray_directions, ds.ray_directions_noisy = ray_d, ray_dn
+    ds.images, ds.image_batch_size, ds.n_images = images, H * W, n
+    ds.index_to_index = {i: i for i in range(n)}
+    ds.gaussian_blur_sigmas = sigmas
+    ds.pixel_width = th.tensor(1 / focal)
+    idx = th.randperm(n * H * W, generator=g)[:97]
+    items = [ds[int(i)] for i in idx]
+    batch = tuple(th.stack([it[k] for it in items]) for k in range(7))
+    out.update({"images": f32(images), "c2w": f32(c2w), "focal": np.array([focal], np.float32),
+                "sigmas": np.array(sigmas, np.float32), "indices": idx.numpy().astype(np.int64),
+                "o_raw": f32(batch[0]), "o_noisy": f32(batch[1]), "d_raw": f32(batch[2]), "d_noisy": f32(batch[3]),
+                "colors": f32(batch[4]), "img_idx": batch[5].numpy().astype(np.int64), "pw": f32(batch[6])})
+    dm = dm_mod.ImagePoseDataModule.__new__(dm_mod.ImagePoseDataModule)
+    dm.gaussian_blur_sigmas = sigmas
+    for sigma in (0.1, 2.0, 5.0, 8.0):
+        out[f"blur_{sigma}"] = f32(dm.get_blurred_pixel_colors(batch, sigma)[4])
+    np.savez_compressed(os.path.join(OUT, "feed.npz"), **out)
+
+
 GENERATORS = {"pe": gen_pe, "composite": gen_composite, "resample": gen_resample, "model": gen_model,
               "color": gen_color, "cos_kat": gen_cos_kat, "ipe_grad": gen_ipe_grad, "garf": gen_garf,
-              "pose": gen_pose}
+              "pose": gen_pose, "pose_render": gen_pose_render, "mipnerf": gen_mipnerf, "feed": gen_feed}
 
 
 if __name__ == "__main__":

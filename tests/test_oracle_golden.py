@@ -176,3 +176,49 @@ def test_cos_kat():
     for d in range(3):
         blk = c[:, d * 10:(d + 1) * 10]
         np.testing.assert_allclose(blk[:, 1:], 2 * blk[:, :-1] ** 2 - 1, atol=5e-6)
+
+
+def test_feed_oracle_matches_reference_dataset(golden):
+    """oracle.ray_batch / directions_meshgrid (the feed's restatement) against the reference's own
+    ImagePoseDataset + collation + get_blurred_pixel_colors on an in-memory image set, and the
+    notebook's hand-computed 4x2 meshgrid (barf/bug_hunting_with_Lauge.ipynb cell 8)."""
+    g = golden("feed")
+    raw = torch.tensor([[-1 / 8, 3 / 8, -1], [1 / 8, 3 / 8, -1], [-1 / 8, 1 / 8, -1], [1 / 8, 1 / 8, -1],
+                        [-1 / 8, -1 / 8, -1], [1 / 8, -1 / 8, -1], [-1 / 8, -3 / 8, -1], [1 / 8, -3 / 8, -1]])
+    kat = raw / torch.linalg.vector_norm(raw, dim=1, keepdim=True)
+    mg = O.directions_meshgrid(4, 2, 4.0)
+    assert torch.allclose(mg, kat) and torch.equal(mg, t(g["kat_meshgrid_4x2"]))
+    from nerf_amd.ray_feed import pose_noise
+    rot, trans = pose_noise(3, 0.1, 0.2, 3)
+    sigmas = [float(s) for s in g["sigmas"]]
+    idx = torch.from_numpy(g["indices"])
+    base = O.ray_batch(t(g["images"]), t(g["c2w"]), float(g["focal"][0]), idx, rot, trans)
+    for got, key in zip(base, ("o_raw", "o_noisy", "d_raw", "d_noisy", "colors", "img_idx")):
+        assert torch.equal(got, torch.from_numpy(g[key])), key
+    for sigma in (0.1, 2.0, 5.0, 8.0):
+        out = O.ray_batch(t(g["images"]), t(g["c2w"]), float(g["focal"][0]), idx, rot, trans, sigmas, sigma)
+        assert torch.equal(out[4], torch.from_numpy(g[f"blur_{sigma}"])), sigma
+
+
+def test_mipnerf_oracle_variants(golden):
+    g = golden("mipnerf")
+    n = g["x"].shape[0]
+    for dv in (0, 1):
+        y = O.integrated_pe(t(g["x"]), t(g["dir"]), torch.full((n, 1), 1 / 1111.1), t(g["t0"]), t(g["t1"]), 10,
+                            2 * np.pi, False, bool(dv), 0.0)
+        np.testing.assert_allclose(y.numpy(), g[f"ipe_dv{dv}"], atol=1e-6, rtol=0)
+
+
+def test_mipnerf_model_init_matches_reference(golden):
+    from nerf_amd.mip_model import MipNerf, MipNerfModel
+    g = golden("mipnerf")
+    torch.manual_seed(0)
+    model = MipNerfModel(4, 256, (True, 10, 4), 2, True)
+    for k, v in model.state_dict().items():
+        np.testing.assert_allclose([v.double().sum().item(), v.double().abs().sum().item()], g[f"model.sdsum.{k}"],
+                                   rtol=1e-12, atol=1e-9)
+    ren = MipNerf(1.0, 5.0, 96, 4, (True, 32), (True, 10, 4), 2)
+    keys = list(ren.state_dict().keys())
+    assert keys[0].startswith("model_fine.") and any(k.startswith("model_coarse.") for k in keys)
+    assert not any(k.startswith(("model_radiance.", "model_proposal.")) for k in keys)
+    assert ren.model_radiance is ren.model_fine and ren.model_proposal is ren.model_coarse
