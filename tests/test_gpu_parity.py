@@ -460,20 +460,55 @@ def test_nerf_model_golden(golden, name, matmul_precision):
     np.testing.assert_allclose(dens.detach().cpu().numpy(), g[f"{name}.density"], atol=1e-4, rtol=1e-4)
     np.testing.assert_allclose(rgb.detach().cpu().numpy(), g[f"{name}.rgb"], atol=1e-4, rtol=1e-4)
     ((dens * g2d(g[f"{name}.gd"])).sum() + (rgb * g2d(g[f"{name}.gc"])).sum()).backward()
-    # Gradients of the deep first segment pass through ~10 ReLU masks whose pre-activations
-    # sit arbitrarily close to zero, so they are ill-conditioned: in fp64 a 1e-5 relative
-    # perturbation of the weights moves barf's model_segments.0.* gradients by up to 6e-3 of
-    # their max.  The 3 x bf16 GEMMs (~2^-16 per product) get a correspondingly looser bound.
-    tol = 1e-4 if matmul_precision == "highest" else 2e-3
-    np.testing.assert_allclose(pos.grad.cpu().numpy(), g[f"{name}.dpos"], atol=10 * tol, rtol=10 * tol)
-    for k, prm in m.named_parameters():
-        s = g[f"{name}.gradsum.{k}"]
-        gs = prm.grad.double()
-        assert abs(gs.abs().sum().item() - s[1]) <= tol * s[1] + 1e-6, k
-        key = f"{name}.grad.{k}"
-        if key in g:
-            np.testing.assert_allclose(prm.grad.cpu().numpy(), g[key], atol=tol * max(1.0, np.abs(g[key]).max()),
-                                       rtol=10 * tol)
+    if matmul_precision == "highest":
+        tol = 1e-4
+        np.testing.assert_allclose(pos.grad.cpu().numpy(), g[f"{name}.dpos"], atol=10 * tol, rtol=10 * tol)
+        for k, prm in m.named_parameters():
+            s = g[f"{name}.gradsum.{k}"]
+            assert abs(prm.grad.double().abs().sum().item() - s[1]) <= tol * s[1] + 1e-6, k
+            key = f"{name}.grad.{k}"
+            if key in g:
+                np.testing.assert_allclose(prm.grad.cpu().numpy(), g[key],
+                                           atol=tol * max(1.0, np.abs(g[key]).max()), rtol=10 * tol)
+        return
+    # split precision: a per-tensor conditioning bound.  Gradients of the deep first segment pass
+    # ~10 ReLU masks whose pre-activations sit arbitrarily close to zero, so how far ANY finite
+    # precision lands from the exact value differs per tensor.  The CPU oracle (pinned to the
+    # reference by the "highest" branch above and tests/test_oracle_golden.py) gives the exact
+    # (fp64) gradient and the reference's own fp32 error on it; three bf16 products carry <= 2^-15
+    # relative error per product against fp32's 2^-24, so each tensor's error must
+    # stay within 2 x 2^9 x the fp32 error (floored at fp32's well-conditioned 2^-22).
+    exact, fp32 = (_oracle_model_grads(m, name, g, dt) for dt in (torch.float64, torch.float32))
+    got = {k: p.grad.double().cpu() for k, p in m.named_parameters()}
+    got["dpos"] = pos.grad.double().cpu()
+    for k, e in exact.items():
+        scale = e.abs().max().item()
+        if scale == 0:
+            continue
+        fp32_err = (fp32[k].double() - e).abs().max().item() / scale
+        err = (got[k] - e).abs().max().item() / scale
+        assert err <= 2 * 2 ** 9 * max(fp32_err, 2 ** -22), (k, err, fp32_err)
+
+
+def _oracle_model_grads(m, name, g, dtype):
+    """Parameter and position gradients of the golden NerfModel config by the CPU oracle in dtype."""
+    cfg = {"barf": (lambda x: O.barf_pe(x, 10, 10.0, True, 1.0), lambda x: O.barf_pe(x, 4, 4.0, True, 1.0),
+                    2, 4, True, False),
+           "n2v": (lambda x: O.fourier_features(x, 10, 2 * math.pi), lambda x: O.fourier_features(x, 4, 1.0),
+                   2, 4, True, True),
+           "small": (lambda x: O.barf_pe(x, 6, 3.4, True, 1.0), lambda x: O.barf_pe(x, 2, 1.5, False, 1.0),
+                     3, 2, False, False)}[name]
+    pe, de, nseg, nhid, dd, dden = cfg
+    sd = {k: v.detach().cpu().to(dtype).requires_grad_(True) for k, v in m.state_dict().items()
+          if not k.endswith("alpha")}
+    pos = torch.from_numpy(g["pos"]).to(dtype).requires_grad_(True)
+    d = torch.from_numpy(g["dir"]).to(dtype)
+    dens, rgb = O.nerf_model_forward(sd, pe(pos).to(dtype), de(d).to(dtype), nseg, nhid, dd, dden)
+    ((dens * torch.from_numpy(g[f"{name}.gd"]).to(dtype)).sum()
+     + (rgb * torch.from_numpy(g[f"{name}.gc"]).to(dtype)).sum()).backward()
+    out = {k: v.grad.double() for k, v in sd.items()}
+    out["dpos"] = pos.grad.double()
+    return out
 
 
 def test_compute_color_and_forward_golden(golden, matmul_precision):
