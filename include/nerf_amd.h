@@ -20,6 +20,7 @@
  *   - encoding   : FourierFeatures / BarfPositionalEncoding / IntegratedFourierFeatures
  *                  (+ IntegratedBarfFourierFeatures)     barf/positional_encodings.py:28-282
  *                  fused with _compute_positions         barf/model_interpolation.py:288-312
+ *   - hash grid  : INGPTable / INGPEncoding              3d-ingp/model.py:14-121
  *   - linear     : the nn.Linear (addmm) chain of NerfModel.forward
  *                                                        barf/model_interpolation_architecture.py:96-141
  *                  and its autograd backward (dX, dW, db)
@@ -317,7 +318,7 @@ typedef struct nerf_fused_layer {
                               out2[m, 32 (chunk - n1) + ...] (row stride ldo2), unmasked, not fed forward */
     int64_t ldo2;
     int32_t n1;            /* chunks written to out (= nb when out2 is unused) */
-    int32_t pad1;
+    int32_t hbm_off;       /* byte offset of the layer's HBM-fed weight fragments in the image */
 } nerf_fused_layer;
 
 int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_layers, const void* image, int64_t M,
@@ -392,6 +393,44 @@ int nerf_ray_batch(const int64_t* indices, int64_t B, int32_t H, int32_t W, floa
                    const float* images, int32_t n_sigma, int32_t blur_mode, int32_t blur_lo, int32_t blur_hi,
                    float coef_lo, float coef_hi, float* o_raw, float* o_noisy, float* d_raw, float* d_noisy,
                    float* colors_raw, float* colors_pair, int64_t* img_idx, int32_t* status, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Multiresolution hash-grid encoding (a9, config C5): INGPTable / INGPEncoding,
+ * 3d-ingp/model.py:14-121 (restated from SURVEY.md §8(a) a9; parity unpinned).
+ * Per level l with resolution res[l]: x_hat = (x / 8 + 0.5) * res[l]; corners floor(x_hat) +
+ * {0,1}^3; table row = x + (r+1) y + (r+1)^2 z of the corner clipped to [0, r] while (r+1)^3 <=
+ * table_size, else ((x * 1) ^ (y * 2654435761) ^ (z * 805459861)) mod table_size in 64-bit
+ * integers (non-negative remainder); weight prod_d (1 - |x_hat_d - corner_d|) on the unclipped
+ * corner; out[n, l * F + f] = sum over corners k = dx + 2 dy + 4 dz (in that order) of
+ * w_k * table[l][row_k][f].  table: [levels][table_size][features] fp32.
+ * Positions: x [n][3], or (x == NULL) o[ray] + tq * d[ray] with ray = n / samples_per_ray and
+ * tq = t_start[n] (query 0) or (t_start[n] + t_end[n]) / 2 (query 1).
+ * ------------------------------------------------------------------------- */
+#define NERF_HASHGRID_MAX_LEVELS 32
+#define NERF_HASHGRID_MAX_FEATURES 8
+typedef struct nerf_hashgrid_params {
+    int32_t levels;
+    int32_t table_size;
+    int32_t features;
+    int32_t query;
+    int32_t res[NERF_HASHGRID_MAX_LEVELS];
+} nerf_hashgrid_params;
+
+int nerf_hashgrid_fwd(const nerf_hashgrid_params* params, const float* x, const float* ray_o,
+                      const float* ray_d, const float* t_start, const float* t_end, int64_t n_samples,
+                      int32_t samples_per_ray, const float* table, float* out, int64_t out_ld, void* stream);
+
+/* Gradient of sum(out * grad_out) w.r.t. the table (positions get none): every contribution
+ * w * g rounded to a 64-bit fixed-point grid 2^-s chosen from the batch's max |g| (no entry can
+ * overflow) and added with integer atomics, so the result does not depend on their order
+ * (deterministic); then grad_table = acc * 2^-s (+= if accumulate).  A non-finite grad_out gives
+ * NaN.  workspace: nerf_hashgrid_workspace(params) bytes, 256-byte aligned, ZERO on the first call
+ * (every call leaves it zero). */
+size_t nerf_hashgrid_workspace(const nerf_hashgrid_params* params);
+int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float* x, const float* ray_o,
+                      const float* ray_d, const float* t_start, const float* t_end, int64_t n_samples,
+                      int32_t samples_per_ray, const float* grad_out, int64_t g_ld, float* grad_table,
+                      int32_t accumulate, void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,258 @@
+// Multiresolution hash-grid encoding (a9, config C5): INGPTable / INGPEncoding of the
+// reference's 3d-ingp/model.py:14-121, restated from SURVEY.md §8(a) a9 (parity unpinned, see
+// oracle/hashgrid_oracle.py).  Contract in include/nerf_amd.h.
+//
+// Forward: one thread per (sample, level), consecutive threads = consecutive levels of one sample,
+// so a sample's L*F features are written by L adjacent threads as one contiguous row.  Per level:
+// x_hat = (x / 8 + 0.5) * r, the 8 corners floor(x_hat) + {0,1}^3, their table rows (bijective
+// while (r+1)^3 <= T, else the product-xor hash modulo T computed in 64-bit integers exactly as the
+// reference's int64 tensor arithmetic with a non-negative remainder), weights prod_d (1 - |x_hat_d -
+// corner_d|) on the unclipped corner, features summed over the corners in the fixed order
+// k = dx + 2 dy + 4 dz with separate multiplies and adds (no contraction): bit-exact with the oracle.
+//
+// Backward (the table gradient; positions receive none): every contribution w * g is rounded to a
+// 64-bit fixed-point integer at a scale 2^s chosen from the batch's max |g| so that no table entry
+// can overflow, and added with integer atomics; integer addition is associative, so the result is
+// independent of the order in which the atomics land (deterministic, unlike float atomics).
+#include "common.h"
+
+namespace {
+
+struct HashArgs {
+    nerf_hashgrid_params p;
+    const float* x;
+    const float* o;
+    const float* d;
+    const float* t0;
+    const float* t1;
+    int64_t n;
+    int spr;
+};
+
+__device__ __forceinline__ void sample_position(const HashArgs& a, int64_t n, float* p) {
+#pragma clang fp contract(off)
+    if (a.x != nullptr) {
+        p[0] = a.x[n * 3 + 0];
+        p[1] = a.x[n * 3 + 1];
+        p[2] = a.x[n * 3 + 2];
+        return;
+    }
+    const int64_t ray = n / a.spr;
+    const float tq = (a.p.query == 0) ? a.t0[n] : (a.t0[n] + a.t1[n]) / 2.0f;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) p[j] = a.o[ray * 3 + j] + tq * a.d[ray * 3 + j];
+}
+
+struct Corners {
+    int64_t idx[8];
+    float w[8];
+};
+
+__device__ __forceinline__ Corners level_corners(const float* p, int r, int T) {
+#pragma clang fp contract(off)
+    Corners c;
+    float xh[3];
+    long long base[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        xh[j] = (p[j] / 8.0f + 0.5f) * (float)r;
+        base[j] = (long long)floorf(xh[j]);
+    }
+    const bool bij = (long long)(r + 1) * (r + 1) * (r + 1) <= (long long)T;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        long long cc[3];
+        float dw[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            cc[j] = base[j] + ((k >> j) & 1);
+            dw[j] = 1.0f - fabsf(xh[j] - (float)cc[j]);
+        }
+        c.w[k] = (dw[0] * dw[1]) * dw[2];
+        if (bij) {
+            const long long r1 = r + 1;
+            long long q[3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) q[j] = cc[j] < 0 ? 0 : (cc[j] > r ? r : cc[j]);
+            c.idx[k] = q[0] + r1 * q[1] + r1 * r1 * q[2];
+        } else {
+            const long long h = (cc[0] * 1LL) ^ (cc[1] * 2654435761LL) ^ (cc[2] * 805459861LL);
+            long long m = h % (long long)T;
+            c.idx[k] = m < 0 ? m + T : m;
+        }
+    }
+    return c;
+}
+
+__global__ __launch_bounds__(256) void hashgrid_fwd_kernel(HashArgs a, const float* __restrict__ table,
+                                                           float* __restrict__ out, int64_t ld) {
+#pragma clang fp contract(off)
+    const int L = a.p.levels, F = a.p.features, T = a.p.table_size;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n = t / L;
+    const int l = (int)(t - n * L);
+    if (n >= a.n) return;
+    float p[3];
+    sample_position(a, n, p);
+    const Corners c = level_corners(p, a.p.res[l], T);
+    const float* tab = table + (int64_t)l * T * F;
+    float acc[NERF_HASHGRID_MAX_FEATURES];
+#pragma unroll
+    for (int f = 0; f < NERF_HASHGRID_MAX_FEATURES; ++f) acc[f] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+#pragma unroll
+        for (int f = 0; f < NERF_HASHGRID_MAX_FEATURES; ++f)
+            if (f < F) acc[f] = acc[f] + c.w[k] * tab[c.idx[k] * F + f];
+    }
+    float* o = out + n * ld + (int64_t)l * F;
+#pragma unroll
+    for (int f = 0; f < NERF_HASHGRID_MAX_FEATURES; ++f)
+        if (f < F) o[f] = acc[f];
+}
+
+// max |grad_out| over the batch as the bits of a non-negative float (order-preserving as uint32);
+// non-finite values land above every finite one
+__global__ __launch_bounds__(256) void hashgrid_gmax_kernel(const float* __restrict__ g, int64_t ld, int64_t n,
+                                                            int cols, unsigned* __restrict__ gmax) {
+    unsigned m = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n * cols; i += (int64_t)gridDim.x * 256) {
+        const int64_t r = i / cols;
+        const float v = fabsf(g[r * ld + (i - r * cols)]);
+        const unsigned b = __float_as_uint(v);
+        m = b > m ? b : m;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned o = __shfl_xor(m, off, 64);
+        m = o > m ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0 && m != 0) atomicMax(gmax, m);
+}
+
+// fixed-point exponent s with 8 * n * gmax * 2^s < 2^62 (no entry can overflow); -1000 flags a
+// non-finite gradient
+__device__ __forceinline__ int fixed_shift(unsigned gmax_bits, int64_t n) {
+    const float gm = __uint_as_float(gmax_bits);
+    if (!(gm < INFINITY)) return -1000;
+    if (gm == 0.0f) return 60;
+    const double bound = 8.0 * (double)n * (double)gm;
+    int e;
+    frexp(bound, &e);                       // bound < 2^e
+    int s = 62 - e;
+    return s > 120 ? 120 : s;
+}
+
+__global__ __launch_bounds__(256) void hashgrid_bwd_kernel(HashArgs a, const float* __restrict__ g, int64_t ld,
+                                                           const unsigned* __restrict__ gmax,
+                                                           unsigned long long* __restrict__ acc) {
+    const int L = a.p.levels, F = a.p.features, T = a.p.table_size;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n = t / L;
+    const int l = (int)(t - n * L);
+    if (n >= a.n) return;
+    const int s = fixed_shift(*gmax, a.n);
+    if (s == -1000) return;
+    const double scale = ldexp(1.0, s);
+    float p[3];
+    sample_position(a, n, p);
+    const Corners c = level_corners(p, a.p.res[l], T);
+    unsigned long long* base = acc + (int64_t)l * T * F;
+    const float* gr = g + n * ld + (int64_t)l * F;
+    float gv[NERF_HASHGRID_MAX_FEATURES];
+#pragma unroll
+    for (int f = 0; f < NERF_HASHGRID_MAX_FEATURES; ++f) gv[f] = f < F ? gr[f] : 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+#pragma unroll
+        for (int f = 0; f < NERF_HASHGRID_MAX_FEATURES; ++f) {
+            if (f >= F) continue;
+            // w * g is exact in fp64 (two 24-bit mantissas); one rounding to the fixed-point grid
+            const long long q = llrint((double)c.w[k] * (double)gv[f] * scale);
+            if (q != 0) atomicAdd(base + c.idx[k] * F + f, (unsigned long long)q);
+        }
+    }
+}
+
+// table gradient = accumulator * 2^-s (or NaN after a non-finite gradient); the accumulators are
+// zeroed for the next call
+__global__ __launch_bounds__(256) void hashgrid_finish_kernel(unsigned long long* __restrict__ acc, int64_t count,
+                                                              const unsigned* __restrict__ gmax, int64_t n,
+                                                              float* __restrict__ grad, int accumulate) {
+    const int s = fixed_shift(*gmax, n);
+    const double inv = s == -1000 ? 0.0 : ldexp(1.0, -s);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (int64_t)gridDim.x * 256) {
+        const long long q = (long long)acc[i];
+        const float v = s == -1000 ? NAN : (float)((double)q * inv);
+        grad[i] = accumulate ? grad[i] + v : v;
+        acc[i] = 0ull;
+    }
+}
+
+bool valid_params(const nerf_hashgrid_params* p) {
+    if (p == nullptr || p->levels < 1 || p->levels > NERF_HASHGRID_MAX_LEVELS) return false;
+    if (p->features < 1 || p->features > NERF_HASHGRID_MAX_FEATURES || p->table_size < 1) return false;
+    if ((int64_t)p->levels * p->table_size * p->features >= ((int64_t)1 << 31)) return false;
+    for (int l = 0; l < p->levels; ++l)
+        if (p->res[l] < 1 || p->res[l] > (1 << 20)) return false;
+    return p->query == 0 || p->query == 1;
+}
+
+}  // namespace
+
+extern "C" int nerf_hashgrid_fwd(const nerf_hashgrid_params* params, const float* x, const float* ray_o,
+                                 const float* ray_d, const float* t_start, const float* t_end, int64_t n_samples,
+                                 int32_t samples_per_ray, const float* table, float* out, int64_t out_ld,
+                                 void* stream) {
+    NERF_REQUIRE(valid_params(params) && table != nullptr && out != nullptr && n_samples >= 0);
+    NERF_REQUIRE(out_ld >= (int64_t)params->levels * params->features);
+    NERF_REQUIRE(x != nullptr || (ray_o && ray_d && t_start && samples_per_ray >= 1 &&
+                                  (params->query == 0 || t_end)));
+    if (n_samples == 0) return NERF_OK;
+    HashArgs a{*params, x, ray_o, ray_d, t_start, t_end, n_samples, samples_per_ray};
+    const int64_t threads = n_samples * params->levels;
+    hipLaunchKernelGGL(hashgrid_fwd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                       as_stream(stream), a, table, out, out_ld);
+    NERF_CHECK_LAUNCH();
+    return NERF_OK;
+}
+
+extern "C" size_t nerf_hashgrid_workspace(const nerf_hashgrid_params* params) {
+    if (!valid_params(params)) return 0;
+    return 256 + (size_t)params->levels * params->table_size * params->features * sizeof(unsigned long long);
+}
+
+extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float* x, const float* ray_o,
+                                 const float* ray_d, const float* t_start, const float* t_end, int64_t n_samples,
+                                 int32_t samples_per_ray, const float* grad_out, int64_t g_ld, float* grad_table,
+                                 int32_t accumulate, void* workspace, size_t workspace_bytes, void* stream) {
+    NERF_REQUIRE(valid_params(params) && grad_out != nullptr && grad_table != nullptr && workspace != nullptr);
+    NERF_REQUIRE(n_samples >= 0 && g_ld >= (int64_t)params->levels * params->features);
+    NERF_REQUIRE(x != nullptr || (ray_o && ray_d && t_start && samples_per_ray >= 1 &&
+                                  (params->query == 0 || t_end)));
+    if (workspace_bytes < nerf_hashgrid_workspace(params)) return NERF_ERR_WORKSPACE;
+    NERF_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 255) == 0);
+    unsigned* gmax = static_cast<unsigned*>(workspace);
+    unsigned long long* acc = reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) + 256);
+    const int64_t count = (int64_t)params->levels * params->table_size * params->features;
+    hipStream_t s = as_stream(stream);
+    if (hipMemsetAsync(gmax, 0, sizeof(unsigned), s) != hipSuccess) return NERF_ERR_LAUNCH;
+    HashArgs a{*params, x, ray_o, ray_d, t_start, t_end, n_samples, samples_per_ray};
+    if (n_samples > 0) {
+        const int cols = params->levels * params->features;
+        int64_t blocks = (n_samples * cols + 255) / 256;
+        blocks = blocks < 2048 ? blocks : 2048;
+        hipLaunchKernelGGL(hashgrid_gmax_kernel, dim3((unsigned)blocks), dim3(256), 0, s, grad_out, g_ld, n_samples,
+                           cols, gmax);
+        NERF_CHECK_LAUNCH();
+        const int64_t threads = n_samples * params->levels;
+        hipLaunchKernelGGL(hashgrid_bwd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, a,
+                           grad_out, g_ld, gmax, acc);
+        NERF_CHECK_LAUNCH();
+    }
+    int64_t fb = (count + 255) / 256;
+    fb = fb < 4096 ? fb : 4096;
+    hipLaunchKernelGGL(hashgrid_finish_kernel, dim3((unsigned)fb), dim3(256), 0, s, acc, count, gmax,
+                       n_samples > 0 ? n_samples : 1, grad_table, accumulate);
+    NERF_CHECK_LAUNCH();
+    return NERF_OK;
+}

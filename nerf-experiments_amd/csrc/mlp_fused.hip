@@ -2,26 +2,33 @@
 // (a7, barf/model_interpolation_architecture.py:96-141; contract in include/nerf_amd.h).
 //
 // Layer-by-layer GEMMs move each 256-wide fp32 activation through HBM twice (written by
-// one launch, read by the next: 536 MB per layer at 262 144 samples).  Here a wave owns 16
-// samples and keeps their activations in registers across the whole network:
+// one launch, read by the next: 536 MB per layer at 262 144 samples).  Here a wave owns 32
+// samples and keeps their layer input in registers across the whole network:
 //
 //   out^T[n][s] = W[n][:] . x^T[:][s]    A operand = weights (rows n), B = activations (cols s)
 //
 // on v_mfma_f32_16x16x32_bf16.  Its 16x16 accumulator holds, in lane (s, g) (s = lane & 15,
-// g = lane >> 4), output rows 4g .. 4g+3 of sample s.  Two such blocks (rows 32q .. 32q+15 and
-// 32q+16 .. 32q+31) give lane (s, g) exactly the eight k-values it must supply as the B operand
-// of one 32-deep k-block of the next layer, once the reduction index is permuted the same way
-// in the packed weights (element j of lane group g <-> feature 32q + 16(j >> 2) + 4g + (j & 3)).
-// A layer's output so becomes the next layer's input with no data movement: bias + ReLU + the
-// bf16 hi/lo split (3 x bf16 products, as linear_x3.hip) are applied in registers.
+// g = lane >> 4), output rows 4g .. 4g+3 of sample s.  Output rows 32q .. 32q+15 and 32q+16 ..
+// 32q+31 give lane (s, g) exactly the eight k-values it must supply as the B operand of k-block q
+// of the next layer, once the reduction index is permuted the same way in the packed weights
+// (element j of lane group g <-> feature 32q + 16(j >> 2) + 4g + (j & 3)).  bias + ReLU + the bf16
+// hi/lo split (3 x bf16 products, as linear_x3.hip) are applied in registers.
 //
-// Weights (2.6 MB for NerfModel) stream through LDS.  Chunk = 32 output rows of one layer: for
-// every k-block the two 16-row A fragments ([hi 64 lanes x 16 B][lo 64 lanes x 16 B] each, one
-// conflict-free ds_read_b128 per half) + 1 KB holding the 32 biases.  Chunks are LDS-DMA'd
-// (global_load_lds_dwordx4) into a 3-slot ring two chunks ahead and shared by the 8 waves of a
-// workgroup (two per SIMD, <= 256 registers each), so the weights cross L2 -> LDS once per
-// 128 samples.  Only HBM-fed inputs (encodings) are loaded and only what the backward needs
-// (each layer's output, its ReLU mask bits, the density column) is stored.
+// One wave per SIMD (4 per workgroup) holds two 16-sample column blocks: every weight fragment
+// read from LDS feeds both (6 MFMAs per 2 ds_read_b128 and k-block).  A chunk is 16 output rows:
+// its MFMA stages interleave the previous chunk's epilogue (bias, ReLU, fp32 stores, mask bits,
+// hi/lo split), whose split halves go to the wave's 32 KB LDS image of the next layer's operand;
+// at the end of the layer that image is read back into the operand registers (compile-time
+// indices: no register array is ever indexed at run time).
+//
+// Weights (2.6 MB for NerfModel) stream through LDS: the register-fed k-blocks of a chunk
+// ([kb][hi 1 KB | lo 1 KB], lane-linear 16 B per lane: one conflict-free ds_read_b128 each) are
+// LDS-DMA'd (global_load_lds_dwordx4) into a 2 x 16 KB ring one chunk ahead and shared by the 4
+// waves, so the weights cross L2 -> LDS once per 128 samples.  The k-blocks fed by HBM inputs
+// (encodings, or the head / density gradients of the backward chain) and the biases are read by
+// each wave from L2 (2 KB + 64 B per chunk).  LDS: 32 KB ring + 4 x 32 KB operand images = 160 KB.
+// Only HBM-fed inputs are loaded and only what the backward needs (each layer's output, its ReLU
+// mask bits, the density column) is stored.
 #include <stddef.h>
 
 #include "common.h"
@@ -31,30 +38,36 @@ using namespace nerf;
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 
-constexpr int SLOT_BYTES = 40 * 1024;      // largest chunk: 10 k-blocks x 4 KB
+constexpr int SLOT_BYTES = 16 * 1024;      // register-fed part of a 16-row chunk: <= 8 k-blocks x 2 KB
 constexpr int NSLOT = 2;
-constexpr int XO_BYTES = 8 * 2048;         // per wave pair: the next layer's B operand, [kb][hi|lo][lane] 16 B
-constexpr int MX_BYTES = 64 * 8;           // per wave pair: mask-word exchange (the high nibbles)
-constexpr int BIAS_LDS = 12 * 1024;        // all biases of the network ([layer][nb][32] fp32), copied once
-constexpr int WG = 512;                    // 8 waves, two per SIMD (<= 256 registers each)
+#ifndef NERF_FUSED_SB
+#define NERF_FUSED_SB 1
+#endif
+constexpr int SB = NERF_FUSED_SB;          // 16-sample column blocks per wave
+constexpr int XIMG_BYTES = SB * 16 * 1024; // per wave: the next layer's operand, [kb][sb][hi|lo][lane] 16 B
+constexpr int WG = 512 / SB;               // 8 waves (two per SIMD) of 16 samples, or 4 of 32
 constexpr int NWAVE = WG / 64;
-constexpr int SPW = 16;                    // samples per wave pair
-constexpr int TILE = NWAVE / 2 * SPW;      // samples per workgroup tile
+constexpr int SPW = 16 * SB;               // samples per wave
+constexpr int TILE = NWAVE * SPW;          // samples per workgroup tile
 constexpr int KBMAX = 8;                   // register-fed 32-deep k-blocks (256 features)
 constexpr unsigned OOB = 0x80000000u;      // buffer offset past every num_records: load 0 / drop store
 constexpr int RSRC_W3 = 0x00020000;
-constexpr int EPI_MIN_VM = 2;
+// vector-memory ops issued after a chunk's DMA (at the start of its predecessor) before the chunk
+// starts: the predecessor's 4 epilogue stores (absent outputs included, as dropped stores) and the
+// bias load at the start of the chunk itself
+constexpr int AFTER_DMA_VM = 1 + 2 * SB;
 
 struct FusedArgs {
     nerf_fused_layer L[NERF_FUSED_MAX_LAYERS];
     const char* img;
-    int bias_base, bias_bytes;   // the biases' byte range in the image (contiguous, layer order)
+    int img_bytes;
     int n_layers;
     int M;
     int ntiles;
@@ -79,12 +92,6 @@ typedef const uint8_t* cu8ptr_t;
 __device__ __forceinline__ f4 mfma16(bf16x8 a, bf16x8 b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
-// acc += a*b, both operands split hi/lo; small terms first (as linear_x3.hip)
-__device__ __forceinline__ f4 mfma_x3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f4 c) {
-    c = mfma16(al, bh, c);
-    c = mfma16(ah, bl, c);
-    return mfma16(ah, bh, c);
-}
 __device__ __forceinline__ void split8(f8 v, bf16x8& hi, bf16x8& lo) {
     hi = __builtin_convertvector(v, bf16x8);
     lo = __builtin_convertvector(v - __builtin_convertvector(hi, f8), bf16x8);
@@ -96,186 +103,300 @@ __device__ __forceinline__ void barrier() {
     __builtin_amdgcn_sched_barrier(0);
 }
 
+__device__ __forceinline__ int n16_of(int N) { return (N + 15) >> 4; }
+
+// Weight-fragment reads from the LDS ring by inline asm with explicitly counted waits.  hipcc
+// cannot tell the ring slot being read from the one the LDS-DMA is filling, so for its own reads it
+// waits for every outstanding DMA (vmcnt) and for every LDS read (lgkmcnt(0)), which empties the
+// one-chunk-ahead prefetch.  The fragments pass through the wait statement, so no instruction can
+// use them before it.
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+template <int OFF>
+__device__ __forceinline__ void lds_frag(bf16x8& f, unsigned addr) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f) : "v"(addr), "n"(OFF));
+}
+template <int N>
+__device__ __forceinline__ void lds_wait(bf16x8& f0, bf16x8& f1) {
+    asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(f0), "+v"(f1) : "n"(N));
+}
+// The HBM-fed weight fragments and the biases are inline-asm buffer loads waited for by explicit
+// counts (hipcc's own wait for a buffer load in the chunk loop is vmcnt(0), which also waits for the
+// DMA issued before it); the loaded values pass through the wait statements.
+template <int N>
+__device__ __forceinline__ void frag_vwait(bf16x8& f0, bf16x8& f1) {
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(f0), "+v"(f1) : "n"(N));
+}
+template <int N>
+__device__ __forceinline__ void bias_wait(f4& b) {
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(b) : "n"(N));
+}
+__device__ __forceinline__ void buf_load16(f4& v, unsigned off, __amdgpu_buffer_rsrc_t r) {
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r));
+}
+__device__ __forceinline__ void buf_load16(bf16x8& v, unsigned off, __amdgpu_buffer_rsrc_t r) {
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r));
+}
+
+// kernel modes: the forward (bias, ReLU, mask bits and column outputs) and the backward's
+// input-gradient chain (ReLU-bit multiply, second output for encoding rows; no bias)
+constexpr int MODE_FWD = 0;
+constexpr int MODE_DGRAD = 1;
+
 struct Ctx {
     kchar_t* kargs;
     char* smem;
-    const char* img;
-    int wave, lane, M, n_layers, bias_base;
-    int half;             // which 16-row block of every 32-row chunk this wave computes
-    int cur;              // ring slot of the chunk being computed
-    // vector-memory ops issued after the newest chunk DMA (= the chunk about to be computed), so
-    // s_waitcnt vmcnt(after_last) is exactly its wait
-    int after_prev, after_last;
-    // DMA cursor: chunks of consecutive layers are contiguous in the image and the stream
-    // repeats per tile, so the next chunk is d_off; layer fields are only read when it changes
+    char* ximg;           // this wave's LDS image of the next layer's operand
+    __amdgpu_buffer_rsrc_t rimg;
+    int wave, lane, M, n_layers;
+    int cur;              // ring slot of the next register-fed chunk
+    // DMA cursor over the register-fed chunks of the network (layers with kbr = 0 have none); the
+    // stream repeats per tile
     int d_off, d_units, d_left, d_layer;
     int d_remaining;      // chunks still to issue
-    char* xo;             // the wave pair's LDS image of the next layer's B operand
-    char* mx;             // the wave pair's mask-word exchange
-    const char* bias;     // LDS copy of the biases
-    // the current layer's register-fed input (B operand)
-    bf16x8 xh[KBMAX], xl[KBMAX];
+    // per-layer DMA table, lane l = layer l (read by v_readlane: no scalar memory loads in the chunk
+    // loop, whose out-of-order returns would force lgkmcnt(0) waits on the LDS reads)
+    int t_off, t_units, t_n16, t_next;
+    // the current layer's register-fed input (B operand): [32-deep k-block][16-sample column block]
+    bf16x8 xh[KBMAX][SB], xl[KBMAX][SB];
 };
 
-__device__ __forceinline__ void count_vm(Ctx& c, int n) {
-    c.after_prev += n;
-    c.after_last += n;
+__device__ __forceinline__ int dma_units(Ctx& c, int l) { return LF(int, chunk_units, l); }
+
+// first layer at or after l (cyclically) with a register-fed part (kernel prologue only)
+__device__ __forceinline__ int next_ring_layer(Ctx& c, int l) {
+    for (int i = 0; i < c.n_layers; ++i, l = (l + 1 == c.n_layers ? 0 : l + 1))
+        if (dma_units(c, l) > 0) return l;
+    return -1;
 }
 
-// LDS-DMA of the next chunk of the stream into ring slot `slot` (the 8 waves share its 1 KB units)
+__device__ __forceinline__ void dma_seek(Ctx& c, int l) {
+    c.d_layer = l;
+    c.d_off = __builtin_amdgcn_readlane(c.t_off, l);
+    c.d_units = __builtin_amdgcn_readlane(c.t_units, l);
+    c.d_left = __builtin_amdgcn_readlane(c.t_n16, l);
+}
+
+// LDS-DMA (buffer_load_dwordx4 ... lds: image offset in an SGPR, the lane's 16 bytes in a constant
+// VGPR) of the next register-fed chunk of the stream into ring slot `slot`: exactly DMA_PER_WAVE
+// 1 KB pieces per wave, unconditionally (a chunk of 8 register-fed k-blocks is 16 pieces; smaller
+// ones repeat pieces, and past the end of the stream the last chunk is fetched again), so that the
+// count of vector-memory ops in a chunk is the same on every path
+constexpr int DMA_PER_WAVE = 2 * KBMAX / NWAVE;
 __device__ __forceinline__ void issue_dma(Ctx& c, int slot) {
-    int cnt = 0;
-    if (c.d_remaining > 0) {
-        const char* src = c.img + c.d_off + c.lane * 16;
-        char* dst = c.smem + slot * SLOT_BYTES;
-        for (int u = c.wave; u < c.d_units; u += NWAVE) {
-            __builtin_amdgcn_global_load_lds((glb_void_t*)(src + u * 1024), (lds_void_t*)(dst + u * 1024), 16, 0, 0);
-            ++cnt;
-        }
+    char* dst = c.smem + slot * SLOT_BYTES;
+#pragma unroll
+    for (int i = 0; i < DMA_PER_WAVE; ++i) {
+        const int u = (c.wave + NWAVE * i) & (c.d_units - 1);   // d_units: 8 or 16
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rimg, (lds_void_t*)(dst + u * 1024), 16, c.lane * 16,
+                                                 c.d_off + u * 1024, 0, 0);
+    }
+    if (c.d_remaining > 1) {
         c.d_off += c.d_units * 1024;
-        if (--c.d_left == 0) {
-            if (++c.d_layer == c.n_layers) {
-                c.d_layer = 0;
-                c.d_off = 0;
-            }
-            c.d_units = LF(int, chunk_units, c.d_layer);
-            c.d_left = LF(int, nb, c.d_layer);
-        }
+        if (--c.d_left == 0) dma_seek(c, __builtin_amdgcn_readlane(c.t_next, c.d_layer));
         --c.d_remaining;
     }
-    c.after_prev = c.after_last + cnt;
-    c.after_last = 0;
 }
 
 struct LayerState {
-    int NB;
-    bool row_ok;
     int floor_i;          // ReLU as an integer max on the fp32 bits: 0, or INT_MIN for no ReLU
-    int sample, col_idx;
-    unsigned sample_off;  // sample * 4 (OOB past M)
-    unsigned row_off;     // byte offset of this lane's sample row (OOB past M)
-    int64_t ldo;
-    __amdgpu_buffer_rsrc_t ro, rm, rc;
-    int bias_lds;         // LDS byte offset of the layer's biases (+128 per chunk; >= 128)
-    unsigned mw[2];       // ReLU mask words 2g, 2g + 1 of this lane's sample row (this wave's nibbles)
-    int n1;               // chunks routed to out (fed forward, masked); the rest go to out2
-    unsigned row_off2;    // byte offset of this lane's sample row in out2 (OOB past M)
-    int64_t ldo2;
-    __amdgpu_buffer_rsrc_t ro2;
-    bool mask_in;         // multiply the output by the ReLU bits min (input-gradient chain)
-    unsigned mi[8];       // this lane's sample row of those bits
+    int col_chunk;        // 16-row chunk holding the column output (-1: none)
+    int n1;               // 16-row chunks routed to out (fed forward, masked); the rest go to out2
+    unsigned bias_off;
+    unsigned row_off[SB];     // byte offset of this lane's 4 columns of chunk 0 in out (OOB past M)
+    unsigned row_off2[SB];    // ... in out2 (chunk n1)
+    int colok, colok2;        // ldo - 4 g: chunk ch is in range while 16 ch < colok
+    unsigned sample_off[SB];  // sample * 4 for lane group 0 (OOB otherwise / past M)
+    unsigned mrow_off[SB];    // this lane's 8 bytes of the sample's mask row (OOB past M)
+    __amdgpu_buffer_rsrc_t ro, rm, rc, ro2;
+    unsigned mw[SB][2];   // ReLU mask words 2g, 2g + 1 of this lane's sample rows
+    unsigned mi[SB][8];   // mask_in: the sample rows of those bits
 };
 
-// Epilogue of this wave's block of chunk nbc (output rows 32 nbc + 16 half .. +15, accumulator v):
-// bias + ReLU, stores, mask bits and the wave pair's B-operand image.  Straight-line code in
-// four parts (absent outputs are buffer stores with out-of-range offsets, which the hardware
-// drops), placed in the stages of the next chunk so that its VALU work issues in MFMA shadows.
-// nbc = -1 (the call in a layer's first chunk) writes nothing visible.
-template <int PART>
-__device__ __forceinline__ void chunk_epilogue(Ctx& c, LayerState& st, int nbc, f4& v, unsigned& w) {
+// hi = bf16(v), lo = bf16(v - hi) of two values, packed (the rounded pair's halves read back as fp32
+// by a shift / a mask instead of a second conversion)
+__device__ __forceinline__ void split2(float x, float y, unsigned& hi, unsigned& lo) {
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    const bf16x2 h = __builtin_convertvector((f4{x, y, 0.f, 0.f}).xy, bf16x2);
+    hi = __builtin_bit_cast(unsigned, h);
+    const float hx = __builtin_bit_cast(float, hi << 16), hy = __builtin_bit_cast(float, hi & 0xffff0000u);
+    lo = __builtin_bit_cast(unsigned, __builtin_convertvector((f4{x - hx, y - hy, 0.f, 0.f}).xy, bf16x2));
+}
+
+// Epilogue of 16-row chunk ch (output rows 16 ch .. 16 ch + 15; ch = -1: none, the stores are
+// dropped), in four parts placed between the next chunk's MFMA stages: 0 / 1 = the values of column
+// block 0 / 1 (FWD: bias + ReLU; DGRAD: times the ReLU bits) and their fp32 stores; 2 = ReLU mask
+// bits (FWD); 3 = the hi/lo split into the LDS image of the next layer's operand.
+template <int MODE>
+__device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, f4 (&a)[SB], f4 b) {
     const int g = c.lane >> 4;
-    if constexpr (PART == 0) {
-        const f4 b = *reinterpret_cast<const f4*>(c.bias + st.bias_lds + 128 * nbc + 64 * c.half + 16 * g);
+    const int q = ch >> 1, bb = ch & 1;
+    if (p < 2) {
+        if (p >= SB) return;
+        const int sb = p;
+        f4& v = a[sb];
+        if constexpr (MODE == MODE_FWD) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-            v[r] = __builtin_bit_cast(float, max(__builtin_bit_cast(int, v[r] + b[r]), st.floor_i));
-        const bool sec = nbc >= st.n1;               // an encoding input's rows (chain: out2)
-        if (st.mask_in && !sec) {
-            // column 32 nbc + 16 half + 4 g + r: bit 4 half + g of byte (nbc & 3) of word 2 r + (nbc >> 2)
-            const int sh = 8 * (nbc & 3) + 4 * c.half + g;
-            const bool hi = nbc >= 4;
+            for (int r = 0; r < 4; ++r)
+                v[r] = __builtin_bit_cast(float, max(__builtin_bit_cast(int, v[r] + b[r]), st.floor_i));
+            const unsigned off = ch >= 0 && 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
+            __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, off, 0, 0);
+            const unsigned coff = ch == st.col_chunk ? st.sample_off[sb] : OOB;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), st.rc, coff, 0, 0);
+        } else {
+            const bool sec = ch >= st.n1;          // an encoding input's rows (out2): not masked
+            // column 16 ch + 4 g + r = 32 q + 16 bb + 4 g + r is bit 8 (q & 3) + 4 bb + g of word
+            // 2 r + (q >> 2) (all ones without mask_in)
+            const int sh = 8 * (q & 3) + 4 * bb + g;
+            // word 2 r or 2 r + 1 by a uniform bit mask (a select here becomes a runtime-indexed
+            // private array, i.e. scratch)
+            const unsigned hm = (unsigned)__builtin_amdgcn_readfirstlane(q >= 4 ? -1 : 0);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const unsigned word = hi ? st.mi[2 * r + 1] : st.mi[2 * r];
-                v[r] = ((word >> sh) & 1u) ? v[r] : 0.f;
+                const unsigned word = st.mi[sb][2 * r] ^ ((st.mi[sb][2 * r] ^ st.mi[sb][2 * r + 1]) & hm);
+                const int keep = sec ? -1 : -(int)((word >> sh) & 1u);
+                // (through a scalar: __builtin_bit_cast of the vector element lvalue v[r] reads element 0)
+                const float x = v[r];
+                v[r] = __builtin_bit_cast(float, __builtin_bit_cast(int, x) & keep);
+            }
+            // one store to each output, the one not addressed dropped (a select of the two resources
+            // or offsets here becomes a runtime-indexed private array, i.e. scratch)
+            const unsigned off1 = !sec && ch >= 0 && 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
+            const unsigned off2 = sec && 16 * (ch - st.n1) < st.colok2 ? st.row_off2[sb] + 64u * (unsigned)(ch - st.n1) : OOB;
+            __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, off1, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(v, st.ro2, off2, 0, 0);
+        }
+    } else if (p == 2) {
+        if constexpr (MODE == MODE_FWD) {
+            // NERF_EPI_MASKOUT layout; byte r of t collects row r's bits over the lane groups, lane
+            // group g keeps the byte of r = g
+            const unsigned keep = (ch >= 0 && ch < 2 * KBMAX) ? 0xffu : 0u;
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) {
+                unsigned t = 0;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) t |= (a[sb][r] > 0.f ? 1u : 0u) << (8 * r + 4 * bb + g);
+                const auto x16 = __builtin_amdgcn_permlane16_swap(t, t, false, false);   // OR with lane ^ 16
+                t = x16[0] | x16[1];
+                const auto x32 = __builtin_amdgcn_permlane32_swap(t, t, false, false);   // OR with lane ^ 32
+                t = x32[0] | x32[1];
+                const unsigned byte = ((t >> (8 * g)) & keep) << (8 * (q & 3));
+                st.mw[sb][0] |= q < 4 ? byte : 0u;
+                st.mw[sb][1] |= q < 4 ? 0u : byte;
             }
         }
-        const int colok = nbc >= 0 ? (int)(sec ? st.ldo2 : st.ldo) : 0;
-        const int col = 32 * (sec ? nbc - st.n1 : nbc) + 16 * c.half + 4 * g;
-        const unsigned off = (unsigned)col < (unsigned)colok ? (sec ? st.row_off2 : st.row_off) + (unsigned)col * 4u
-                                                             : OOB;   // nbc = -1: col < 0
-        const unsigned coff = (c.half == 0 && g == 0 && st.col_idx == 32 * nbc) ? st.sample_off : OOB;
-        __builtin_amdgcn_raw_buffer_store_b128(v, sec ? st.ro2 : st.ro, off, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), st.rc, coff, 0, 0);
-        count_vm(c, 2);
-    } else if constexpr (PART == 1) {
-        // NERF_EPI_MASKOUT layout: column 32 nb + 16 bb + 4 g + r is bit 4 bb + g of byte (nb & 3)
-        // of word 2 r + (nb >> 2) of the row; lane group g keeps the byte of r = g
-        w = 0;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) w |= (v[r] > 0.f ? 1u : 0u) << (8 * r + 4 * c.half + g);
-    } else if constexpr (PART == 2) {
-        const auto x16 = __builtin_amdgcn_permlane16_swap(w, w, false, false);   // OR with lane ^ 16
-        w = x16[0] | x16[1];
-        const auto x32 = __builtin_amdgcn_permlane32_swap(w, w, false, false);   // OR with lane ^ 32
-        w = x32[0] | x32[1];
-        const unsigned byte = ((w >> (8 * g)) & 0xffu) << (8 * (nbc & 3));
-        st.mw[0] |= (nbc >= 0 && nbc < 4) ? byte : 0u;
-        st.mw[1] |= (nbc >= 4 && nbc < 8) ? byte : 0u;
     } else {
-        // the next layer's B operand, k-block nbc: elements j < 4 are block 0 (this pair's
-        // half-0 wave), j >= 4 block 1 -> 8 bytes of each lane's 16-byte hi and lo slots
-        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-        const bf16x4 h = __builtin_convertvector(v, bf16x4);
-        const bf16x4 lo = __builtin_convertvector(v - __builtin_convertvector(h, f4), bf16x4);
-        if (nbc >= 0 && nbc < KBMAX && nbc < st.n1) {
-            *reinterpret_cast<bf16x4*>(c.xo + nbc * 2048 + c.lane * 16 + 8 * c.half) = h;
-            *reinterpret_cast<bf16x4*>(c.xo + nbc * 2048 + 1024 + c.lane * 16 + 8 * c.half) = lo;
+        // rows 16 bb + 4 g + r of k-block q of the next layer = elements 4 bb + r of lane (s, g):
+        // 8 bytes of the lane's 16-byte hi and lo slots (chunks past the fed outputs are not written)
+        if (ch >= 0 && ch < 2 * KBMAX && ch < st.n1) {
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) {
+                typedef unsigned u2 __attribute__((ext_vector_type(2)));
+                unsigned h0, l0, h1, l1;
+                split2(a[sb][0], a[sb][1], h0, l0);
+                split2(a[sb][2], a[sb][3], h1, l1);
+                const u2 h = {h0, h1}, lo = {l0, l1};
+                char* d = c.ximg + ((q * SB + sb) * 2) * 1024 + c.lane * 16 + 8 * bb;
+                *reinterpret_cast<u2*>(d) = h;
+                *reinterpret_cast<u2*>(d + 1024) = lo;
+            }
         }
     }
 }
 
-// one layer: runtime loop over its 32-row output chunks (this wave: one 16-row block of each);
-// k-blocks unrolled (KBR register-fed, KBH HBM-fed).  Reads c.xh/c.xl, leaves the next layer's
-// input there.
-template <int KBR, int KBH>
-__device__ __forceinline__ void fused_layer(Ctx& c, int l, int sample) {
-    constexpr int KB = KBR + KBH;
-    const int g = c.lane >> 4;
-    LayerState st;
-    st.NB = LF(int, nb, l);
-    st.floor_i = LF(int, relu, l) != 0 ? 0 : (int)0x80000000;
-    st.ldo = LF(int64_t, ldo, l);
-    st.sample = sample;
-    st.row_ok = sample < c.M;
-    st.row_off = st.row_ok ? (unsigned)((int64_t)sample * st.ldo * 4) : OOB;
-    st.sample_off = st.row_ok ? (unsigned)(sample * 4) : OOB;
-    st.mw[0] = st.mw[1] = 0;
-    st.ro = __builtin_amdgcn_make_buffer_rsrc(LF(fptr_t, out, l), 0, (int)((int64_t)c.M * st.ldo * 4), RSRC_W3);
-    uint8_t* mptr = LF(u8ptr_t, mask, l);
-    st.rm = __builtin_amdgcn_make_buffer_rsrc(mptr, 0, mptr != nullptr ? c.M * 32 : 0, RSRC_W3);
-    float* cptr = LF(fptr_t, col_out, l);
-    st.col_idx = cptr != nullptr ? LF(int, col_idx, l) : -1;
-    st.rc = __builtin_amdgcn_make_buffer_rsrc(cptr, 0, cptr ? c.M * 4 : 0, RSRC_W3);
-    st.bias_lds = (int)LF(int64_t, bias_off, l) - c.bias_base + 128;
-    {
-        float* o2 = LF(fptr_t, out2, l);
-        st.n1 = o2 != nullptr ? LF(int, n1, l) : st.NB;
-        st.ldo2 = o2 != nullptr ? LF(int64_t, ldo2, l) : 0;
-        st.ro2 = __builtin_amdgcn_make_buffer_rsrc(o2, 0, o2 ? (int)((int64_t)c.M * st.ldo2 * 4) : 0, RSRC_W3);
-        st.row_off2 = st.row_ok ? (unsigned)((int64_t)sample * st.ldo2 * 4) : OOB;
+// One 16-row chunk's register-fed k-blocks (compile-time KB_I: immediate LDS offsets), fragments
+// read two steps ahead; the previous chunk's epilogue parts 0-2 at stages EPI0 .. EPI0 + 2.
+template <int MODE, int KBR, int KBH, int KB_I>
+__device__ __forceinline__ void reg_steps(Ctx& c, LayerState& st, unsigned sa, bf16x8 (&fr)[2][2], f4 (&a)[SB],
+                                          f4 (&pv)[SB], f4& pb, int ch) {
+    constexpr int EPI0 = KBR >= 8 ? 4 : (KBR >= 4 ? 1 : 0);
+    if constexpr (KB_I < KBR) {
+        bf16x8(&f)[2] = fr[KB_I & 1];
+        // this step's fragments have landed (the next step's two reads may still be in flight)
+        lds_wait<(KB_I + 1 < KBR ? 2 : 0)>(f[0], f[1]);
+        // products lo*hi + hi*lo + hi*hi per accumulator (small terms first, as linear_x3.hip)
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(f[1], c.xh[KB_I][sb], a[sb]);
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(f[0], c.xl[KB_I][sb], a[sb]);
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(f[0], c.xh[KB_I][sb], a[sb]);
+        if constexpr (KB_I + 2 < KBR) {
+            lds_frag<(KB_I + 2) * 2048>(f[0], sa);
+            lds_frag<(KB_I + 2) * 2048 + 1024>(f[1], sa);
+        }
+        if constexpr (KB_I == EPI0) bias_wait<(KBR > 0 ? DMA_PER_WAVE : 0) + 2 * KBH>(pb);
+        if constexpr (KB_I >= EPI0 && KB_I < EPI0 + 3) epi_part<MODE>(c, st, KB_I - EPI0, ch - 1, pv, pb);
+        __builtin_amdgcn_sched_barrier(0);
+        reg_steps<MODE, KBR, KBH, KB_I + 1>(c, st, sa, fr, a, pv, pb, ch);
     }
-    {
+}
+
+// One layer of shape (KBR register-fed, KBH HBM-fed 32-deep k-blocks): runtime loop over its
+// 16-row output chunks.
+template <int MODE, int KBR, int KBH>
+__device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
+    constexpr int EPI0 = KBR >= 8 ? 4 : (KBR >= 4 ? 1 : 0);   // first stage carrying an epilogue part
+    const int g = c.lane >> 4;
+    const int N = LF(int, N, l);
+    const int NC = n16_of(N);
+    LayerState st;
+    const int ldo = (int)LF(int64_t, ldo, l);
+    st.floor_i = LF(int, relu, l) != 0 ? 0 : (int)0x80000000;
+    st.colok = ldo - 4 * g;
+    int sample[SB];
+    bool row_ok[SB];
+#pragma unroll
+    for (int sb = 0; sb < SB; ++sb) {
+        sample[sb] = base + 16 * sb + (c.lane & 15);
+        row_ok[sb] = sample[sb] < c.M;
+        st.row_off[sb] = row_ok[sb] ? (unsigned)sample[sb] * (unsigned)ldo * 4u + 16u * g : OOB;
+        st.sample_off[sb] = row_ok[sb] && g == 0 ? (unsigned)sample[sb] * 4u : OOB;
+        st.mrow_off[sb] = row_ok[sb] ? (unsigned)sample[sb] * 32u + 8u * g : OOB;
+        st.mw[sb][0] = st.mw[sb][1] = 0;
+    }
+    st.ro = __builtin_amdgcn_make_buffer_rsrc(LF(fptr_t, out, l), 0, c.M * ldo * 4, RSRC_W3);
+    st.bias_off = (unsigned)LF(int64_t, bias_off, l) + 16u * g;
+    if constexpr (MODE == MODE_FWD) {
+        uint8_t* mptr = LF(u8ptr_t, mask, l);
+        st.rm = __builtin_amdgcn_make_buffer_rsrc(mptr, 0, mptr != nullptr ? c.M * 32 : 0, RSRC_W3);
+        float* cptr = LF(fptr_t, col_out, l);
+        st.col_chunk = cptr != nullptr ? LF(int, col_idx, l) / 16 : -1;
+        st.rc = __builtin_amdgcn_make_buffer_rsrc(cptr, 0, cptr ? c.M * 4 : 0, RSRC_W3);
+        st.n1 = NC;
+    } else {
+        float* o2 = LF(fptr_t, out2, l);
+        st.n1 = o2 != nullptr ? 2 * LF(int, n1, l) : NC;
+        const int ldo2 = o2 != nullptr ? (int)LF(int64_t, ldo2, l) : 0;
+        st.colok2 = ldo2 - 4 * g;
+        st.ro2 = __builtin_amdgcn_make_buffer_rsrc(o2, 0, o2 ? c.M * ldo2 * 4 : 0, RSRC_W3);
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb)
+            st.row_off2[sb] = row_ok[sb] ? (unsigned)sample[sb] * (unsigned)ldo2 * 4u + 16u * g : OOB;
         const uint8_t* mi = LF(cu8ptr_t, mask_in, l);
-        st.mask_in = mi != nullptr;
-        if (st.mask_in) {
-            const __amdgpu_buffer_rsrc_t rmi =
-                __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(mi), 0, c.M * 32, RSRC_W3);
-            const unsigned off = st.row_ok ? (unsigned)(sample * 32) : OOB;
-            typedef unsigned u4 __attribute__((ext_vector_type(4)));
+        const __amdgpu_buffer_rsrc_t rmi =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(mi), 0, mi != nullptr ? c.M * 32 : 0, RSRC_W3);
+        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb) {
+            const unsigned off = row_ok[sb] ? (unsigned)sample[sb] * 32u : OOB;
             const u4 w0 = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rmi, off, 0, 0));
             const u4 w1 = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rmi, off + 16, 0, 0));
-            st.mi[0] = w0.x; st.mi[1] = w0.y; st.mi[2] = w0.z; st.mi[3] = w0.w;
-            st.mi[4] = w1.x; st.mi[5] = w1.y; st.mi[6] = w1.z; st.mi[7] = w1.w;
-            count_vm(c, 2);
+            st.mi[sb][0] = w0.x; st.mi[sb][1] = w0.y; st.mi[sb][2] = w0.z; st.mi[sb][3] = w0.w;
+            st.mi[sb][4] = w1.x; st.mi[sb][5] = w1.y; st.mi[sb][6] = w1.z; st.mi[sb][7] = w1.w;
+            if (mi == nullptr) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) st.mi[sb][i] = ~0u;
+            }
         }
     }
 
-    // ---- HBM-fed input blocks (encodings): lane (s, g) of block kh holds columns 32 kh + 8 g .. +7
-    bf16x8 hh[KBH > 0 ? KBH : 1], hl[KBH > 0 ? KBH : 1];
+    // ---- HBM-fed input blocks (encodings, gradients): lane (s, g) of block kh holds columns
+    // 32 kh + 8 g .. +7 of its sample
+    bf16x8 hh[KBH > 0 ? KBH : 1][SB], hl[KBH > 0 ? KBH : 1][SB];
     if constexpr (KBH > 0) {
         const int kb0 = LFI(int, seg_kb, 0, l);
-        f8 raw[KBH];
 #pragma unroll
         for (int kh = 0; kh < KBH; ++kh) {
             const int sg = kh < kb0 ? 0 : 1;            // segment of this block
@@ -287,135 +408,151 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int sample) {
             const int rows = sg ? LFI(int, seg_rows, 1, l) : LFI(int, seg_rows, 0, l);
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, (int)((int64_t)rows * ld * 4), RSRC_W3);
-            const unsigned m = (unsigned)(st.row_ok ? sample : 0);
-            const unsigned row = rd == 1 ? m : m / (unsigned)rd;
             const int col = 32 * khl + 8 * g;
-            const unsigned base = (unsigned)(((int64_t)row * ld + col) * 4);
-            const f4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, col < k ? base : OOB, 0, 0);
-            const f4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, col + 4 < k ? base + 16 : OOB, 0, 0);
-            raw[kh] = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) {
+                const unsigned m = (unsigned)(row_ok[sb] ? sample[sb] : 0);
+                const unsigned row = rd == 1 ? m : m / (unsigned)rd;
+                const unsigned rbase = (unsigned)(((int64_t)row * ld + col) * 4);
+                const f4 x0 = __builtin_amdgcn_raw_buffer_load_b128(rs, col < k ? rbase : OOB, 0, 0);
+                const f4 x1 = __builtin_amdgcn_raw_buffer_load_b128(rs, col + 4 < k ? rbase + 16 : OOB, 0, 0);
+                split8(__builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7), hh[kh][sb], hl[kh][sb]);
+            }
         }
-        count_vm(c, 2 * KBH);
-#pragma unroll
-        for (int kh = 0; kh < KBH; ++kh) split8(raw[kh], hh[kh], hl[kh]);
     }
+    const unsigned hbm_frag = (unsigned)LF(int, hbm_off, l) + (unsigned)c.lane * 16u;
 
-    f4 p = {};
-    for (int nbc = 0; nbc < st.NB; ++nbc) {
-        // this chunk's own DMA share has landed: every chunk issues its successor's DMA and then
-        // at least EPI_MIN_VM vector-memory ops (the epilogue stores; more at layer boundaries,
-        // which only makes this wait stricter), so a constant count is exact or safe
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EPI_MIN_VM) : "memory");
-        barrier();               // ... and everyone else's; the other slot is free
-        const int slot = c.cur;
-        // this wave's 16-row block of the chunk: [kb][block][hi 1 KB | lo 1 KB]
-        const char* S = c.smem + slot * SLOT_BYTES + c.half * 2048 + c.lane * 16;
-        // explicit software pipeline: the fragments of k-block kb + 2 are read while kb's three
-        // MFMAs run; sched_barriers pin the stages.  The previous chunk's epilogue covers the
-        // latency of the first reads and fills the MFMA shadows of the first stages.
-        bf16x8 fa[2], fb[2];
-        auto frag = [&](int kb, bf16x8 (&f)[2]) __attribute__((always_inline)) {
-            f[0] = *reinterpret_cast<const bf16x8*>(S + kb * 4096);
-            f[1] = *reinterpret_cast<const bf16x8*>(S + kb * 4096 + 1024);
-        };
-        frag(0, fa);
-        if (KB > 1) frag(1, fb);
-        issue_dma(c, slot ^ 1);                        // the next chunk, a whole chunk ahead
-        __builtin_amdgcn_sched_barrier(0);            // keep the DMA ahead of every other vmem op (vmcnt)
-        unsigned w = 0;
-        const int ep = nbc - 1;                        // the previous chunk (-1: none)
-        f4 a = {0.f, 0.f, 0.f, 0.f};
+    // the previous chunk's accumulators (its epilogue runs during the current chunk)
+    f4 pv[SB] = {};
+    for (int ch = 0; ch < NC; ++ch) {
+        // the previous chunk's biases (rows 4 g .. 4 g + 3), for its epilogue in this chunk, issued
+        // before this chunk's DMA so that waiting for it does not wait for the DMA
+        f4 pb;
+        if constexpr (MODE == MODE_FWD)
+            buf_load16(pb, st.bias_off + 64u * (unsigned)(ch > 0 ? ch - 1 : 0), c.rimg);
+        else
+            buf_load16(pb, st.bias_off, c.rimg);     // (zero biases: the load only keeps the count)
+        const unsigned sa = lds_addr(c.smem + c.cur * SLOT_BYTES + c.lane * 16);
+        bf16x8 fr[2][2];
+        if constexpr (KBR > 0) {
+            // this chunk's DMA share has landed (issued at the start of the previous register-fed
+            // chunk and followed by >= AFTER_DMA_VM vector-memory ops), then everyone else's; the
+            // other slot is free
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AFTER_DMA_VM) : "memory");
+            barrier();
+            lds_frag<0>(fr[0][0], sa);
+            lds_frag<1024>(fr[0][1], sa);
+            if (KBR > 1) {
+                lds_frag<2048>(fr[1][0], sa);
+                lds_frag<3072>(fr[1][1], sa);
+            }
+            issue_dma(c, c.cur ^ 1);                 // the next register-fed chunk, a whole chunk ahead
+            __builtin_amdgcn_sched_barrier(0);      // keep the DMA ahead of this chunk's vmem ops (vmcnt)
+        }
+        // this chunk's HBM-fed weight fragments, from L2
+        bf16x8 hf[KBH > 0 ? KBH : 1][2];
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-            bf16x8(&f)[2] = (kb & 1) ? fb : fa;
-            const bf16x8 bh = kb < KBR ? c.xh[kb < KBR ? kb : 0] : hh[kb < KBR ? 0 : kb - KBR];
-            const bf16x8 bl = kb < KBR ? c.xl[kb < KBR ? kb : 0] : hl[kb < KBR ? 0 : kb - KBR];
-            a = mfma_x3(f[0], f[1], bh, bl, a);
-            if (kb + 2 < KB) frag(kb + 2, f);
-            // the previous chunk's epilogue, one part per stage (all in the last stage if KB < 4)
-            if (kb == 0) chunk_epilogue<0>(c, st, ep, p, w);
-            if (kb == (KB > 1 ? 1 : 0)) chunk_epilogue<1>(c, st, ep, p, w);
-            if (kb == (KB > 2 ? 2 : KB - 1)) chunk_epilogue<2>(c, st, ep, p, w);
-            if (kb == (KB > 3 ? 3 : KB - 1)) chunk_epilogue<3>(c, st, ep, p, w);
+        for (int kh = 0; kh < KBH; ++kh)
+#pragma unroll
+            for (int hl_ = 0; hl_ < 2; ++hl_)
+                buf_load16(hf[kh][hl_], hbm_frag + (unsigned)(((ch * KBH + kh) * 2 + hl_) * 1024), c.rimg);
+        f4 a[SB];
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb) a[sb] = f4{0.f, 0.f, 0.f, 0.f};
+        reg_steps<MODE, KBR, KBH, 0>(c, st, sa, fr, a, pv, pb, ch);
+        // the HBM-fed fragments have landed: with a register-fed part the 4 epilogue stores of parts
+        // 0-1 were issued after them
+#pragma unroll
+        for (int kh = 0; kh < KBH; ++kh) frag_vwait<(KBR > 0 ? 2 * SB : 0)>(hf[kh][0], hf[kh][1]);
+#pragma unroll
+        for (int kh = 0; kh < KBH; ++kh) {
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(hf[kh][1], hh[kh][sb], a[sb]);
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(hf[kh][0], hl[kh][sb], a[sb]);
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(hf[kh][0], hh[kh][sb], a[sb]);
             __builtin_amdgcn_sched_barrier(0);
         }
-        c.cur = slot ^ 1;
-        p = a;
+        if constexpr (KBR == 0) bias_wait<0>(pb);
+#pragma unroll
+        for (int p = KBR >= EPI0 + 3 ? 3 : (KBR > EPI0 ? KBR - EPI0 : 0); p < 4; ++p) epi_part<MODE>(c, st, p, ch - 1, pv, pb);
+        if constexpr (KBR > 0) c.cur ^= 1;
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb) pv[sb] = a[sb];
     }
     {
-        unsigned w = 0;
-        const int nbc = st.NB - 1;
-        chunk_epilogue<0>(c, st, nbc, p, w);
-        chunk_epilogue<1>(c, st, nbc, p, w);
-        chunk_epilogue<2>(c, st, nbc, p, w);
-        chunk_epilogue<3>(c, st, nbc, p, w);
-    }
-    // the pair's halves meet: the half-1 wave hands its mask nibbles over, then both read the
-    // next layer's operand image
-    typedef unsigned u2 __attribute__((ext_vector_type(2)));
-    if (c.half == 1) *reinterpret_cast<u2*>(c.mx + c.lane * 8) = u2{st.mw[0], st.mw[1]};
-    barrier();
-    if (c.half == 0) {
-        const u2 o = *reinterpret_cast<const u2*>(c.mx + c.lane * 8);
-        const unsigned off = st.row_ok ? (unsigned)(sample * 32 + 8 * g) : OOB;
-        __builtin_amdgcn_raw_buffer_store_b64(u2{st.mw[0] | o.x, st.mw[1] | o.y}, st.rm, off, 0, 0);
-        count_vm(c, 1);
-    }
+        f4 lb;
+        buf_load16(lb, st.bias_off + (MODE == MODE_FWD ? 64u * (unsigned)(NC - 1) : 0u), c.rimg);
+        bias_wait<0>(lb);
 #pragma unroll
-    for (int kb = 0; kb < KBMAX; ++kb) {
-        c.xh[kb] = *reinterpret_cast<const bf16x8*>(c.xo + kb * 2048 + c.lane * 16);
-        c.xl[kb] = *reinterpret_cast<const bf16x8*>(c.xo + kb * 2048 + 1024 + c.lane * 16);
+        for (int p = 0; p < 4; ++p) epi_part<MODE>(c, st, p, NC - 1, pv, lb);
     }
+    if constexpr (MODE == MODE_FWD) {
+        // the sample rows' ReLU mask words 2g, 2g + 1
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb)
+            __builtin_amdgcn_raw_buffer_store_b64(u2{st.mw[sb][0], st.mw[sb][1]}, st.rm, st.mrow_off[sb], 0, 0);
+    }
+    // the next layer's operand: the wave's LDS image back into registers (same wave: LDS ops in order)
+#pragma unroll
+    for (int kb = 0; kb < KBMAX; ++kb)
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb) {
+            c.xh[kb][sb] = *reinterpret_cast<const bf16x8*>(c.ximg + ((kb * SB + sb) * 2) * 1024 + c.lane * 16);
+            c.xl[kb][sb] = *reinterpret_cast<const bf16x8*>(c.ximg + ((kb * SB + sb) * 2 + 1) * 1024 + c.lane * 16);
+        }
 }
 
-__global__ __launch_bounds__(WG, 1) void mlp_fused_fwd_kernel(FusedArgs a) {
-    __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT_BYTES + NWAVE / 2 * (XO_BYTES + MX_BYTES) + BIAS_LDS];
+template <int MODE>
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, NWAVE / 4))) void mlp_fused_kernel(FusedArgs a) {
+    __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT_BYTES + NWAVE * XIMG_BYTES];
     Ctx c;
     c.kargs = (kchar_t*)__builtin_amdgcn_kernarg_segment_ptr();
     c.smem = smem;
-    c.img = a.img;
+    c.rimg = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(a.img), 0, a.img_bytes, RSRC_W3);
     c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    c.half = c.wave & 1;
-    c.xo = smem + NSLOT * SLOT_BYTES + (c.wave >> 1) * XO_BYTES;
-    c.mx = smem + NSLOT * SLOT_BYTES + NWAVE / 2 * XO_BYTES + (c.wave >> 1) * MX_BYTES;
-    c.bias = smem + NSLOT * SLOT_BYTES + NWAVE / 2 * (XO_BYTES + MX_BYTES);
-    c.bias_base = a.bias_base;
+    c.ximg = smem + NSLOT * SLOT_BYTES + c.wave * XIMG_BYTES;
     c.lane = threadIdx.x & 63;
     c.M = a.M;
     c.n_layers = a.n_layers;
     if ((int)blockIdx.x >= a.ntiles) return;
     const int my_tiles = (a.ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
     int per_tile = 0;
-    for (int l = 0; l < a.n_layers; ++l) per_tile += LF(int, nb, l);
-    c.d_layer = 0;
-    c.d_off = 0;
-    c.d_units = LF(int, chunk_units, 0);
-    c.d_left = LF(int, nb, 0);
+    for (int l = 0; l < a.n_layers; ++l)
+        if (dma_units(c, l) > 0) per_tile += n16_of(LF(int, N, l));
     c.d_remaining = my_tiles * per_tile;
+    {
+        const int l = c.lane < c.n_layers ? c.lane : 0;
+        c.t_off = (int)LF(int64_t, img_off, l);
+        c.t_units = dma_units(c, l);
+        c.t_n16 = n16_of(LF(int, N, l));
+        c.t_next = next_ring_layer(c, l + 1 == c.n_layers ? 0 : l + 1);
+    }
+    const int l0 = next_ring_layer(c, 0);
+    if (l0 >= 0) dma_seek(c, l0);
     c.cur = 0;
-    c.after_prev = c.after_last = 0;
-    // every bias of the network into LDS (offset 128: a layer's chunk -1 reads in bounds)
-    for (int i = threadIdx.x * 16; i < a.bias_bytes; i += WG * 16)
-        *reinterpret_cast<f4*>(const_cast<char*>(c.bias) + 128 + i) =
-            *reinterpret_cast<const f4*>(a.img + a.bias_base + i);
-    issue_dma(c, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the first chunk (the steady-state wait assumes successors)
+    if (l0 >= 0) issue_dma(c, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the first chunk (the steady-state wait assumes predecessors)
     __syncthreads();
 #pragma unroll
-    for (int kb = 0; kb < KBMAX; ++kb) {
-        c.xh[kb] = bf16x8{};
-        c.xl[kb] = bf16x8{};
-    }
+    for (int kb = 0; kb < KBMAX; ++kb)
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb) {
+            c.xh[kb][sb] = bf16x8{};
+            c.xl[kb][sb] = bf16x8{};
+        }
     for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
-        const int sample = tile * TILE + (c.wave >> 1) * SPW + (c.lane & 15);
+        const int base = tile * TILE + c.wave * SPW;
         for (int l = 0; l < a.n_layers; ++l) {
             switch (LF(int, type, l)) {
-                case 1: fused_layer<0, 1>(c, l, sample); break;
-                case 2: fused_layer<0, 2>(c, l, sample); break;
-                case 3: fused_layer<4, 0>(c, l, sample); break;
-                case 6: fused_layer<8, 0>(c, l, sample); break;
-                case 7: fused_layer<8, 1>(c, l, sample); break;
-                case 8: fused_layer<8, 2>(c, l, sample); break;
+                case 1: fused_layer<MODE, 0, 1>(c, l, base); break;
+                case 2: fused_layer<MODE, 0, 2>(c, l, base); break;
+                case 3: fused_layer<MODE, 4, 0>(c, l, base); break;
+                case 6: fused_layer<MODE, 8, 0>(c, l, base); break;
+                case 7: fused_layer<MODE, 8, 1>(c, l, base); break;
+                case 8: fused_layer<MODE, 8, 2>(c, l, base); break;
                 default: break;                          // rejected on the host
             }
         }
@@ -472,23 +609,39 @@ extern "C" int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_laye
     NERF_REQUIRE(n_layers >= 1 && n_layers <= NERF_FUSED_MAX_LAYERS);
     NERF_REQUIRE(M >= 1 && M <= (int64_t)1 << 30);
     FusedArgs a;
+    int64_t img_end = 0;
+    // the input-gradient chain (a layer multiplies by ReLU bits or routes rows to a second output):
+    // no bias, no ReLU, no mask bits or column outputs; otherwise the forward, which has none of those
+    bool dgrad = false;
+    for (int l = 0; l < n_layers; ++l) dgrad = dgrad || layers[l].mask_in != nullptr || layers[l].out2 != nullptr;
+    for (int l = 0; l < n_layers; ++l) {
+        if (dgrad)
+            NERF_REQUIRE(layers[l].relu == 0 && layers[l].mask == nullptr && layers[l].col_out == nullptr);
+    }
     for (int l = 0; l < n_layers; ++l) {
         const nerf_fused_layer& L = layers[l];
         const int kbr = (L.type / 3) * 4, kbh = L.type % 3;
         NERF_REQUIRE(L.type == 1 || L.type == 2 || L.type == 3 || L.type == 6 || L.type == 7 || L.type == 8);
         NERF_REQUIRE((l == 0) == (kbr == 0));                  // only the first layer has no register input
         NERF_REQUIRE(L.N >= 1 && L.nb == (L.N + 31) / 32 && L.nb <= 16);
-        NERF_REQUIRE(L.chunk_units == 4 * (kbr + kbh));
+        const int n16 = (L.N + 15) / 16;
+        NERF_REQUIRE(L.chunk_units == 2 * kbr);
+        NERF_REQUIRE(L.img_off >= 0 && L.img_off % 1024 == 0);
+        NERF_REQUIRE(L.hbm_off >= 0 && L.hbm_off % 1024 == 0);
         NERF_REQUIRE(L.bias_off >= 0 && L.bias_off % 16 == 0);
-        // with a second output only the first n1 chunks land in out (columns past ldo are dropped);
-        // a null out (ldo 0) drops the layer's stores (inference keeps only the exposed outputs)
+        img_end = img_end > L.img_off + (int64_t)n16 * 2048 * kbr ? img_end : L.img_off + (int64_t)n16 * 2048 * kbr;
+        img_end = img_end > (int64_t)L.hbm_off + (int64_t)n16 * 2048 * kbh ? img_end
+                                                                          : (int64_t)L.hbm_off + (int64_t)n16 * 2048 * kbh;
+        img_end = img_end > L.bias_off + 64 * n16 ? img_end : L.bias_off + 64 * n16;
+        // with a second output only the first n1 32-column chunks land in out (columns past ldo are
+        // dropped); a null out (ldo 0) drops the layer's stores (inference keeps only the exposed outputs)
         NERF_REQUIRE((L.out == nullptr && L.ldo == 0) ||
                      (L.out != nullptr && aligned16(L.out) && L.ldo % 4 == 0 &&
                       L.ldo >= (L.out2 != nullptr ? (32 * L.n1 < L.N ? 32 * L.n1 : L.N) : L.N)));
         NERF_REQUIRE(M * L.ldo * 4 < ((int64_t)1 << 31));
         NERF_REQUIRE(L.mask == nullptr || (L.N <= 256 && M * 32 < ((int64_t)1 << 31)));
+        NERF_REQUIRE(L.mask_in == nullptr || M * 32 < ((int64_t)1 << 31));
         NERF_REQUIRE(L.col_out == nullptr || (L.col_idx >= 0 && L.col_idx % 32 == 0 && L.col_idx < L.N));
-        NERF_REQUIRE(L.img_off >= 0 && L.img_off % 1024 == 0);
         NERF_REQUIRE(L.out2 == nullptr || (aligned16(L.out2) && L.ldo2 % 4 == 0 && L.ldo2 > 0 && L.n1 >= 0 &&
                                            L.n1 <= L.nb && M * L.ldo2 * 4 < ((int64_t)1 << 31)));
         NERF_REQUIRE(L.nseg >= 0 && L.nseg <= 2);
@@ -502,9 +655,9 @@ extern "C" int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_laye
         }
         NERF_REQUIRE(kbs == kbh);
         if (l > 0) {
+            // the fed k-blocks are complete 32-row blocks of the previous layer's fed output
             const nerf_fused_layer& P = layers[l - 1];
-            const int pn = P.out2 != nullptr ? P.n1 : P.nb;
-            NERF_REQUIRE(kbr <= (pn < 8 ? pn : 8));      // fed blocks exist in the previous output
+            NERF_REQUIRE(32 * kbr <= (P.out2 != nullptr ? 32 * P.n1 : P.N));
         }
         a.L[l] = L;
         if (L.nseg < 2) {
@@ -512,23 +665,17 @@ extern "C" int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_laye
             a.L[l].seg_ptr[1] = L.nseg == 1 ? L.seg_ptr[0] : nullptr;
         }
     }
+    NERF_REQUIRE(img_end < ((int64_t)1 << 31));
     a.img = static_cast<const char*>(image);
-    // the biases: contiguous, in layer order, and small enough for their LDS copy
-    {
-        int64_t off = layers[0].bias_off;
-        for (int l = 0; l < n_layers; ++l) {
-            NERF_REQUIRE(layers[l].bias_off == off);
-            off += 128 * layers[l].nb;
-        }
-        NERF_REQUIRE(off - layers[0].bias_off + 128 <= BIAS_LDS && off < ((int64_t)1 << 31));
-        a.bias_base = (int)layers[0].bias_off;
-        a.bias_bytes = (int)(off - layers[0].bias_off);
-    }
+    a.img_bytes = (int)img_end;
     a.n_layers = n_layers;
     a.M = (int)M;
     a.ntiles = (int)((M + TILE - 1) / TILE);
     const int grid = a.ntiles < num_cus() ? a.ntiles : num_cus();
-    hipLaunchKernelGGL(mlp_fused_fwd_kernel, dim3(grid), dim3(WG), 0, as_stream(stream), a);
+    if (dgrad)
+        hipLaunchKernelGGL(mlp_fused_kernel<MODE_DGRAD>, dim3(grid), dim3(WG), 0, as_stream(stream), a);
+    else
+        hipLaunchKernelGGL(mlp_fused_kernel<MODE_FWD>, dim3(grid), dim3(WG), 0, as_stream(stream), a);
     NERF_CHECK_LAUNCH();
     return NERF_OK;
 }

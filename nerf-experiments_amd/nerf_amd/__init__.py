@@ -7,6 +7,7 @@ from .positional_encodings import (BarfPositionalEncoding, FourierFeatures, Iden
 from .model_interpolation_architecture import NerfBaseModel, NerfModel  # noqa: F401
 from .model_interpolation import MAGIC_NUMBER, NerfInterpolation, SchedulerLeNice  # noqa: F401
 from .model_garf import GaussAct, ProposalNetwork, RadianceNetwork  # noqa: F401
+from .model_ingp import INGPEncoding, INGPTable, NerfModelINGP  # noqa: F401
 from .optim import FusedAdam  # noqa: F401
 
 __version__ = "0.1.0"

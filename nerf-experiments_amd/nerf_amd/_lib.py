@@ -104,9 +104,22 @@ class NerfFusedLayer(ctypes.Structure):
         ("out2", c_vp),
         ("ldo2", c_i64),
         ("n1", c_i32),
-        ("pad1", c_i32),
+        ("hbm_off", c_i32),
     ]
 
+
+NERF_HASHGRID_MAX_LEVELS = 32
+NERF_HASHGRID_MAX_FEATURES = 8
+
+
+class NerfHashgridParams(ctypes.Structure):
+    _fields_ = [
+        ("levels", c_i32),
+        ("table_size", c_i32),
+        ("features", c_i32),
+        ("query", c_i32),
+        ("res", c_i32 * NERF_HASHGRID_MAX_LEVELS),
+    ]
 
 # name -> (restype, argtypes)
 _SIGNATURES = {
@@ -146,6 +159,11 @@ _SIGNATURES = {
     "nerf_pack_weight_x3": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
     "nerf_mlp_fused_fwd": (c_i32, [ctypes.POINTER(NerfFusedLayer), c_i32, c_vp, c_i64, c_vp]),
     "nerf_fused_pack": (c_i32, [ctypes.POINTER(c_vp), c_i32, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "nerf_hashgrid_fwd": (c_i32, [ctypes.POINTER(NerfHashgridParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
+                                  c_vp, c_vp, c_i64, c_vp]),
+    "nerf_hashgrid_workspace": (c_sz, [ctypes.POINTER(NerfHashgridParams)]),
+    "nerf_hashgrid_bwd": (c_i32, [ctypes.POINTER(NerfHashgridParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
+                                  c_vp, c_i64, c_vp, c_i32, c_vp, c_sz, c_vp]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES.keys())
@@ -168,7 +186,7 @@ def load(path: str | None = None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.nerf_abi_version() != 1:
+    if lib.nerf_abi_version() != 2:
         raise RuntimeError("nerf_amd: ABI version mismatch between Python binding and libnerf_amd.so")
     if path is None:
         _lib = lib

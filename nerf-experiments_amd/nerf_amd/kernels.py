@@ -447,3 +447,64 @@ def pack_weight(W: torch.Tensor, col_map: torch.Tensor, Kp: int, Wp: torch.Tenso
     st = _lib.load().nerf_pack_weight(_ptr(W), N, K_orig, _ptr(col_map), Kp, _ptr(Wp), _ptr(Wt), ldwt,
                                       _stream(W.device))
     _lib.check(st, "nerf_pack_weight")
+
+
+# ----------------------------------------------------------------------------- hash grid (a9)
+def make_hashgrid_params(levels: int, table_size: int, features: int, res, query: int = 1) -> _lib.NerfHashgridParams:
+    if not 1 <= levels <= _lib.NERF_HASHGRID_MAX_LEVELS:
+        raise ValueError(f"levels must be in [1, {_lib.NERF_HASHGRID_MAX_LEVELS}] (got {levels})")
+    if not 1 <= features <= _lib.NERF_HASHGRID_MAX_FEATURES:
+        raise ValueError(f"feature_dim must be in [1, {_lib.NERF_HASHGRID_MAX_FEATURES}] (got {features})")
+    p = _lib.NerfHashgridParams()
+    p.levels, p.table_size, p.features, p.query = levels, table_size, features, query
+    for i, r in enumerate(res):
+        p.res[i] = int(r)
+    return p
+
+
+def hashgrid_fwd(params, table: torch.Tensor, out: torch.Tensor, *, x=None, ray_o=None, ray_d=None, t_start=None,
+                 t_end=None, n_samples: int, samples_per_ray: int = 1) -> None:
+    _require_cuda_f32("table", table)
+    _require_cuda_f32("out", out)
+    if not table.is_contiguous() or table.shape != (params.levels, params.table_size, params.features):
+        raise ValueError(f"table must be a contiguous [{params.levels}, {params.table_size}, {params.features}] tensor")
+    if out.stride(1) != 1 or out.shape[0] < n_samples or out.shape[1] < params.levels * params.features:
+        raise ValueError("out must be a row-major [n, >= levels * features] tensor")
+    for name, t in (("x", x), ("ray_o", ray_o), ("ray_d", ray_d), ("t_start", t_start), ("t_end", t_end)):
+        if t is not None:
+            _require_cuda_f32(name, t)
+            if not t.is_contiguous():
+                raise ValueError(f"{name} must be contiguous")
+    end = TIMER.bracket("hashgrid_fwd", 0.0, 8.0 * n_samples * params.levels * params.features * 8
+                        + 4.0 * n_samples * params.levels * params.features, fn="hashgrid_fwd_kernel") \
+        if TIMER is not None else None
+    st = _lib.load().nerf_hashgrid_fwd(ctypes.byref(params), _ptr(x), _ptr(ray_o), _ptr(ray_d), _ptr(t_start),
+                                       _ptr(t_end), n_samples, samples_per_ray, table.data_ptr(), out.data_ptr(),
+                                       out.stride(0), _stream(table.device))
+    if end is not None:
+        end.record()
+    _lib.check(st, "nerf_hashgrid_fwd")
+
+
+def hashgrid_workspace_bytes(params) -> int:
+    return int(_lib.load().nerf_hashgrid_workspace(ctypes.byref(params)))
+
+
+def hashgrid_bwd(params, grad_out: torch.Tensor, grad_table: torch.Tensor, workspace: torch.Tensor, *, x=None,
+                 ray_o=None, ray_d=None, t_start=None, t_end=None, n_samples: int, samples_per_ray: int = 1,
+                 accumulate: bool = False) -> None:
+    _require_cuda_f32("grad_out", grad_out)
+    _require_cuda_f32("grad_table", grad_table)
+    if not grad_table.is_contiguous() or grad_out.stride(1) != 1:
+        raise ValueError("grad_table must be contiguous and grad_out row-major")
+    end = TIMER.bracket("hashgrid_bwd", 0.0, 8.0 * n_samples * params.levels * params.features * 8
+                        + 4.0 * n_samples * params.levels * params.features, fn="hashgrid_bwd_kernel") \
+        if TIMER is not None else None
+    st = _lib.load().nerf_hashgrid_bwd(ctypes.byref(params), _ptr(x), _ptr(ray_o), _ptr(ray_d), _ptr(t_start),
+                                       _ptr(t_end), n_samples, samples_per_ray, grad_out.data_ptr(),
+                                       grad_out.stride(0), grad_table.data_ptr(), int(accumulate),
+                                       workspace.data_ptr(), workspace.numel() * workspace.element_size(),
+                                       _stream(grad_out.device))
+    if end is not None:
+        end.record()
+    _lib.check(st, "nerf_hashgrid_bwd")

@@ -8,11 +8,13 @@ the per-layer descriptors, and launches it.  Outputs are exactly those of the la
 forward in mlp.py (every layer's output, the ReLU mask bits, the density column), so the
 backward is unchanged.
 
-Fragment order (mirrors the kernel header): chunk (layer, nb) holds output rows 32 nb .. +31;
-for every 32-deep k-block kb and 16-row half bb, lane l (s = l & 15, g = l >> 4) element j is
-W[32 nb + 16 bb + s][k(kb, g, j)] with
+Image layout (mirrors the kernel header): per layer, 16-row output chunks c (rows 16 c .. 16 c + 15);
+for every 32-deep k-block one A fragment of v_mfma_f32_16x16x32_bf16 as [hi 64 lanes x 16 B][lo 64
+lanes x 16 B]; lane l (s = l & 15, g = l >> 4) element j is W[16 c + s][k(kb, g, j)] with
   k = 32 kb + 16 (j >> 2) + 4 g + (j & 3)          register-fed input (previous layer output)
   k = seg_offset + 32 kh + 8 g + j                  HBM-fed segment block kh (encodings)
+The register-fed blocks of a chunk are contiguous ([c][kb], 2 KB each: one LDS-DMA stream), the
+HBM-fed ones live in a second region ([c][kh]) and the biases in a third ([c][16] fp32).
 """
 from __future__ import annotations
 
@@ -89,76 +91,113 @@ def eligible(plan, M: int) -> bool:
     return True
 
 
+def _fragment_maps(n16, kbr, kbh, row_of, red_reg, red_hbm, elem, img_off, hbm_off, bias_off, bias_code):
+    """Gather maps (source code: tensor << 24 | element, -1 = 0; destination: bf16 index of hi, or
+    ~fp32 word) of one layer's image: row_of(c) -> [16] weight rows of 16-row chunk c (-1 absent),
+    red_reg(kb) / red_hbm(kh) -> [64, 8] reduction indices of a register- / HBM-fed block (-1
+    absent), elem(rows[64,1], red[64,8]) -> codes (-1 where either is absent), bias_code(rows[16])."""
+    lane = np.arange(64)
+    srow = lane & 15
+    jj = np.arange(8)
+    srcs, dsts = [], []
+    for c in range(n16):
+        rows = row_of(c)                                   # [16]
+        r = rows[srow][:, None]                            # [64, 1]
+        for kb in range(kbr):
+            base = (img_off + (c * kbr + kb) * 2048) // 2
+            srcs.append(elem(r, red_reg(kb)).reshape(-1))
+            dsts.append((base + lane[:, None] * 8 + jj[None, :]).reshape(-1))
+        for kh in range(kbh):
+            base = (hbm_off + (c * kbh + kh) * 2048) // 2
+            srcs.append(elem(r, red_hbm(kh)).reshape(-1))
+            dsts.append((base + lane[:, None] * 8 + jj[None, :]).reshape(-1))
+        srcs.append(bias_code(rows))
+        dsts.append(~(bias_off // 4 + 16 * c + np.arange(16)))
+    return np.concatenate(srcs), np.concatenate(dsts)
+
+
+def _red_reg(kb):
+    """Reduction index of register-fed k-block kb, lane (s, g) element j: the previous layer's
+    accumulator order 32 kb + 16 (j >> 2) + 4 g + (j & 3)."""
+    lane = np.arange(64)
+    g = (lane >> 4)[:, None]
+    j = np.arange(8)[None, :]
+    return 32 * kb + 16 * (j >> 2) + 4 * g + (j & 3)
+
+
+def _layout_offsets(shapes):
+    """Byte offsets of each layer's register-fed, HBM-fed and bias regions: (n16, kbr, kbh) per
+    layer -> [(img_off, hbm_off, bias_off)], total bytes."""
+    offs = []
+    off = 0
+    for n16, kbr, kbh in shapes:
+        offs.append([off, 0, 0])
+        off += n16 * kbr * 2048
+    for i, (n16, kbr, kbh) in enumerate(shapes):
+        offs[i][1] = off
+        off += n16 * kbh * 2048
+    for i, (n16, kbr, kbh) in enumerate(shapes):
+        offs[i][2] = off
+        off += n16 * 64
+    return [tuple(o) for o in offs], off
+
+
 class FusedForward:
     """Packed image + static descriptors of one plan on one device."""
 
     def __init__(self, plan, device):
         self.plan = plan
         self.device = device
-        self.layers = []          # (kbr, kbh, hbm sources, nb, units, img_off, bias_off)
+        self.layers = []          # (kbr, kbh, hbm sources, nb, n16, img_off, hbm_off, bias_off)
         shapes = []
-        off = 0
         for idx, lp in enumerate(plan.layers):
             kbr, hbm = _layer_shape(plan, idx)
             kbh = sum(s.k_pad // 32 for s in hbm)
-            nb = (lp.module.out_features + 31) // 32
-            units = 4 * (kbr + kbh)
-            shapes.append((kbr, kbh, hbm, nb, units, off))
-            off += nb * units * 1024
+            shapes.append(((lp.module.out_features + 15) // 16, kbr, kbh))
+        offs, total = _layout_offsets(shapes)
         src_codes, dst_codes = [], []
         for idx, lp in enumerate(plan.layers):
-            kbr, kbh, hbm, nb, units, img_off = shapes[idx]
-            self.layers.append((kbr, kbh, hbm, nb, units, img_off, off))
-            s, d = self._maps(idx, lp, kbr, hbm, nb, units, img_off, off)
-            src_codes.append(s)
-            dst_codes.append(d)
-            off += nb * 128
-        self.image_bytes = off
-        self.image = torch.zeros(off // 2, dtype=torch.bfloat16, device=device)
+            kbr, hbm = _layer_shape(plan, idx)
+            n16, _, kbh = shapes[idx]
+            nb = (lp.module.out_features + 31) // 32
+            img_off, hbm_off, bias_off = offs[idx]
+            self.layers.append((kbr, kbh, hbm, nb, n16, img_off, hbm_off, bias_off))
+            s_, d_ = self._maps(idx, lp, kbr, hbm, n16, img_off, hbm_off, bias_off)
+            src_codes.append(s_)
+            dst_codes.append(d_)
+        self.image_bytes = total
+        self.image = torch.zeros(total // 2, dtype=torch.bfloat16, device=device)
         self.map_src = torch.from_numpy(np.concatenate(src_codes).astype(np.int32)).to(device)
         self.map_dst = torch.from_numpy(np.concatenate(dst_codes).astype(np.int32)).to(device)
 
     @staticmethod
-    def _maps(idx, lp, kbr, hbm, nb, units, off, bias_off):
-        """Gather map of one layer: source codes (tensor << 24 | element, -1 = 0) and
-        destinations (bf16 index of hi, or ~fp32 word for raw bias words)."""
+    def _maps(idx, lp, kbr, hbm, n16, img_off, hbm_off, bias_off):
         N, K_orig = lp.module.out_features, lp.module.in_features
         tw, tb = 2 * idx, 2 * idx + 1
-        # original weight column offsets of the sources (plan order, k_valid wide)
         orig = {}
         o = 0
         for s in lp.sources:
             orig[id(s)] = o
             o += s.k_valid
         lane = np.arange(64)
-        srow, grp = lane & 15, lane >> 4
-        j = np.arange(8)
-        kb_total = kbr + sum(s.k_pad // 32 for s in hbm)
-        col = np.full((kb_total, 64, 8), -1, dtype=np.int64)       # weight column per (kb, lane, j)
-        for kb in range(kbr):
-            col[kb] = 32 * kb + 16 * (j[None, :] >> 2) + 4 * grp[:, None] + (j[None, :] & 3)
-        kb = kbr
+        g = (lane >> 4)[:, None]
+        j = np.arange(8)[None, :]
+        hbm_cols = []
         for s in hbm:
             for kh in range(s.k_pad // 32):
-                local = 32 * kh + 8 * grp[:, None] + j[None, :]
-                col[kb] = np.where(local < s.k_valid, orig[id(s)] + local, -1)
-                kb += 1
-        srcs, dsts = [], []
-        for c in range(nb):
-            base = off + c * units * 1024
-            for bb in range(2):
-                n = 32 * c + 16 * bb + srow                          # [64]
-                nn = np.broadcast_to(n[None, :, None], col.shape)
-                valid = (col >= 0) & (nn < N)
-                code = np.where(valid, (tw << 24) + nn * K_orig + col, -1)
-                dst = (base + np.arange(kb_total)[:, None, None] * 4096 + bb * 2048) // 2 + \
-                    lane[None, :, None] * 8 + j[None, None, :]
-                srcs.append(code.reshape(-1))
-                dsts.append(np.broadcast_to(dst, col.shape).reshape(-1))
-            nbias = 32 * c + np.arange(32)
-            srcs.append(np.where(nbias < N, (tb << 24) + nbias, -1))
-            dsts.append(~(bias_off // 4 + nbias))
-        return np.concatenate(srcs), np.concatenate(dsts)
+                local = 32 * kh + 8 * g + j
+                hbm_cols.append(np.where(local < s.k_valid, orig[id(s)] + local, -1))
+
+        def row_of(c):
+            n = 16 * c + np.arange(16)
+            return np.where(n < N, n, -1)
+
+        def elem(r, red):
+            ok = (r >= 0) & (red >= 0)
+            return np.where(ok, (tw << 24) + r * K_orig + red, -1)
+
+        return _fragment_maps(n16, kbr, len(hbm_cols), row_of, _red_reg, lambda kh: hbm_cols[kh], elem,
+                              img_off, hbm_off, bias_off, lambda rows: np.where(rows >= 0, (tb << 24) + rows, -1))
 
     def pack(self):
         _pack_image(self)
@@ -172,7 +211,7 @@ class FusedForward:
         flops = 0.0
         nbytes = 0.0
         for idx, lp in enumerate(self.plan.layers):
-            kbr, kbh, hbm, nb, units, off, bias_off = self.layers[idx]
+            kbr, kbh, hbm, nb, n16, off, hbm_off, bias_off = self.layers[idx]
             d = descs[idx]
             d.type = FUSED_TYPES[(kbr, kbh)]
             d.N = lp.module.out_features
@@ -187,7 +226,7 @@ class FusedForward:
                 d.seg_rows[si] = t.shape[0]
                 d.seg_ld[si] = t.stride(0)
                 d.seg_ptr[si] = t.data_ptr()
-            d.chunk_units = units
+            d.chunk_units = 2 * kbr
             d.col_idx = -1
             # a layer without a tensor (inference: not an exposed output) has its stores dropped
             d.out = acts[idx].data_ptr() if acts[idx] is not None else None
@@ -197,6 +236,7 @@ class FusedForward:
                 d.col_out = col_outs[idx].data_ptr()
                 d.col_idx = dict(self.plan.column_outputs)[idx]
             d.img_off = off
+            d.hbm_off = hbm_off
             d.bias_off = bias_off
             flops += 2.0 * M * lp.module.out_features * lp.module.in_features
             # algorithmic bytes: HBM-fed encodings read, stored outputs / mask bits / columns written
@@ -279,70 +319,64 @@ class FusedInputGrad:
     def __init__(self, plan, device, need_pos: bool = False, need_dir: bool = False):
         self.plan = plan
         self.device = device
-        self.steps = []           # (l, kbr, kbh, n1, extra, n_out, nb, units, img_off, bias_off)
+        self.steps = []           # (l, kbr, kbh, n1, extra, n_out, nb, img_off, hbm_off, bias_off)
+        lay = self.layout(plan, need_pos, need_dir)
         shapes = []
-        off = 0
-        for (l, kbr, kbh, n1, x) in self.layout(plan, need_pos, need_dir):
+        for (l, kbr, kbh, n1, x) in lay:
             nb = n1 + (x.k_pad // 32 if x is not None else 0)
-            units = 4 * (kbr + kbh)
-            shapes.append((l, kbr, kbh, n1, x, nb, units, off))
-            off += nb * units * 1024
+            shapes.append((2 * nb, kbr, kbh))
+        offs, total = _layout_offsets(shapes)
         src_codes, dst_codes = [], []
-        for (l, kbr, kbh, n1, x, nb, units, img_off) in shapes:
-            self.steps.append((l, kbr, kbh, n1, x, 32 * nb, nb, units, img_off, off))
-            s, d = self._maps(plan.layers[l], l, kbr, kbh, n1, x, nb, units, img_off, off)
-            src_codes.append(s)
-            dst_codes.append(d)
-            off += nb * 128
-        self.image_bytes = off
-        self.image = torch.zeros(off // 2, dtype=torch.bfloat16, device=device)
+        for (l, kbr, kbh, n1, x), (n16, _, _), (img_off, hbm_off, bias_off) in zip(lay, shapes, offs):
+            nb = n16 // 2
+            self.steps.append((l, kbr, kbh, n1, x, 32 * nb, nb, img_off, hbm_off, bias_off))
+            s_, d_ = self._maps(plan.layers[l], l, kbr, kbh, n1, x, n16, img_off, hbm_off, bias_off)
+            src_codes.append(s_)
+            dst_codes.append(d_)
+        self.image_bytes = total
+        self.image = torch.zeros(total // 2, dtype=torch.bfloat16, device=device)
         self.map_src = torch.from_numpy(np.concatenate(src_codes).astype(np.int32)).to(device)
         self.map_dst = torch.from_numpy(np.concatenate(dst_codes).astype(np.int32)).to(device)
 
     @staticmethod
-    def _maps(lp, l, kbr, kbh, n1, x, nb, units, off, bias_off):
-        """A fragment (row i = input feature k of layer l, column = its output n) = W_l[n][k];
-        n permuted like the previous step's accumulator layout when register-fed, natural when
-        it is an HBM-fed gradient (head output, density column); rows of chunks >= n1 are the
-        columns of the encoding input x; biases zero."""
+    def _maps(lp, l, kbr, kbh, n1, x, n16, img_off, hbm_off, bias_off):
+        """A fragment (row = input feature k of layer l, reduction = its output n) = W_l[n][k]; n
+        permuted like the previous step's accumulator layout when register-fed, natural when it is
+        an HBM-fed gradient (head output, density column); rows of chunks >= 2 n1 are the columns of
+        the encoding input x; biases zero."""
         N, K_orig = lp.module.out_features, lp.module.in_features
         lane = np.arange(64)
-        srow, grp = lane & 15, lane >> 4
-        j = np.arange(8)
-        kb_total = kbr + kbh
-        nidx = np.full((kb_total, 64, 8), -1, dtype=np.int64)
-        for kb in range(kbr):
-            nidx[kb] = 32 * kb + 16 * (j[None, :] >> 2) + 4 * grp[:, None] + (j[None, :] & 3)
-        for kh in range(kbh):
-            # HBM-fed gradient columns follow the register-fed ones (natural order)
-            local = 32 * kbr + 32 * kh + 8 * grp[:, None] + j[None, :]
-            nidx[kbr + kh] = np.where(local < N, local, -1)
+        g = (lane >> 4)[:, None]
+        j = np.arange(8)[None, :]
         orig = {}
         o = 0
         for s_ in lp.sources:
             orig[id(s_)] = o
             o += s_.k_valid
         act_valid = lp.sources[0].k_valid if lp.sources[0].kind == "act" else 0
-        srcs, dsts = [], []
-        for c in range(nb):
-            base = off + c * units * 1024
-            for bb in range(2):
-                if c < n1:
-                    k = 32 * c + 16 * bb + srow
-                    kcol = np.where(k < act_valid, k, -1)
-                else:
-                    local = 32 * (c - n1) + 16 * bb + srow
-                    kcol = np.where(local < x.k_valid, orig[id(x)] + local, -1)
-                kk = np.broadcast_to(kcol[None, :, None], nidx.shape)
-                valid = (nidx >= 0) & (nidx < N) & (kk >= 0)
-                code = np.where(valid, ((2 * l) << 24) + nidx * K_orig + kk, -1)
-                dst = (base + np.arange(kb_total)[:, None, None] * 4096 + bb * 2048) // 2 + \
-                    lane[None, :, None] * 8 + j[None, None, :]
-                srcs.append(code.reshape(-1))
-                dsts.append(np.broadcast_to(dst, nidx.shape).reshape(-1))
-            srcs.append(np.full(32, -1))
-            dsts.append(~(bias_off // 4 + 32 * c + np.arange(32)))
-        return np.concatenate(srcs), np.concatenate(dsts)
+
+        def row_of(c):
+            i = np.arange(16)
+            if c < 2 * n1:
+                k = 16 * c + i
+                return np.where(k < act_valid, k, -1)
+            local = 16 * (c - 2 * n1) + i
+            return np.where(local < x.k_valid, orig[id(x)] + local, -1)
+
+        def red_reg(kb):
+            n = _red_reg(kb)
+            return np.where(n < N, n, -1)
+
+        def red_hbm(kh):
+            n = 32 * kbr + 32 * kh + 8 * g + j
+            return np.where(n < N, n, -1)
+
+        def elem(r, red):
+            ok = (r >= 0) & (red >= 0)
+            return np.where(ok, ((2 * l) << 24) + red * K_orig + r, -1)
+
+        return _fragment_maps(n16, kbr, kbh, row_of, red_reg, red_hbm, elem, img_off, hbm_off, bias_off,
+                              lambda rows: np.full(16, -1))
 
     def pack(self):
         _pack_image(self)
@@ -359,7 +393,7 @@ class FusedInputGrad:
         descs = (_lib.NerfFusedLayer * S)()
         flops = 0.0
         nbytes = 0.0
-        for i, (l, kbr, kbh, n1, x, n_out, nb, units, img_off, bias_off) in enumerate(self.steps):
+        for i, (l, kbr, kbh, n1, x, n_out, nb, img_off, hbm_off, bias_off) in enumerate(self.steps):
             lp = self.plan.layers[l]
             d = descs[i]
             d.type = FUSED_TYPES[(kbr, kbh)]
@@ -375,7 +409,7 @@ class FusedInputGrad:
                 d.seg_rows[0] = src.shape[0]
                 d.seg_ld[0] = src.stride(0)
                 d.seg_ptr[0] = src.data_ptr()
-            d.chunk_units = units
+            d.chunk_units = 2 * kbr
             d.col_idx = -1
             if l >= 1:
                 d.out = dY[l - 1].data_ptr()
@@ -393,6 +427,7 @@ class FusedInputGrad:
                 d.ldo2 = x_out[l].stride(0)
                 d.n1 = n1
             d.img_off = img_off
+            d.hbm_off = hbm_off
             d.bias_off = bias_off
             flops += 2.0 * M * lp.module.out_features * n_out
             # algorithmic bytes: HBM-fed gradients and ReLU bits read, dY / encoding gradients written

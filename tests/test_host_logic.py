@@ -243,16 +243,16 @@ def test_camera_extrinsics_matches_reference(golden):
 
 
 def _emulate_fused(plan, fused, image_f64, x_pos, x_dir, dir_rd, relu_floor=True):
-    """Lane-level numpy emulation of csrc/mlp_fused.hip over the packed image for ONE wave of
-    16 samples: B operands built exactly as the kernel's registers (epilogue order), MFMA
-    16x16x32 as D[i][s] += sum_{g,j} A[lane i+16g][j] * B[lane s+16g][j]."""
+    """Lane-level numpy emulation of csrc/mlp_fused.hip over the packed image for ONE 16-sample
+    column block: B operands built exactly as the kernel's registers (epilogue order), MFMA
+    16x16x32 as D[i][s] += sum_{g,j} A[lane i+16g][j] * B[lane s+16g][j], 16-row output chunks."""
     lane = np.arange(64)
     s_of, g_of = lane & 15, lane >> 4
     j = np.arange(8)
     xreg = None                      # [KBMAX, 64 lanes, 8] register-fed B operand
     outs = []
     for idx, lp in enumerate(plan.layers):
-        kbr, kbh, hbm, nb, units, off, bias_off = fused.layers[idx]
+        kbr, kbh, hbm, nb, n16, img_off, hbm_off, bias_off = fused.layers[idx]
         B = []
         for kb in range(kbr):
             B.append(xreg[kb])
@@ -263,24 +263,24 @@ def _emulate_fused(plan, fused, image_f64, x_pos, x_dir, dir_rd, relu_floor=True
                 c = 32 * kh + 8 * g_of[:, None] + j[None, :]
                 rows = (s_of // rd)[:, None]
                 B.append(np.where(c < s.k_seg, t[rows, np.minimum(c, t.shape[1] - 1)], 0.0))
-        KB = len(B)
         N = lp.module.out_features
-        out = np.zeros((16, 32 * nb))
-        for c in range(nb):
-            base = off + c * units * 1024
-            bias = image_f64["raw"][bias_off // 4 + 32 * c + np.arange(32)]
-            for bb in range(2):
-                acc = np.tile(bias[16 * bb:16 * bb + 16][:, None], (1, 16))     # [i rows][s]
-                for kb in range(KB):
-                    h0 = (base + kb * 4096 + bb * 2048) // 2
-                    frag = image_f64["w"][h0 + lane[:, None] * 8 + j[None, :]]   # hi + lo
-                    A = np.zeros((16, 32))
-                    Bm = np.zeros((32, 16))
-                    for g in range(4):
-                        A[:, 8 * g:8 * g + 8] = frag[np.arange(16) + 16 * g]
-                        Bm[8 * g:8 * g + 8, :] = B[kb][np.arange(16) + 16 * g].T
-                    acc += A @ Bm
-                out[:, 32 * c + 16 * bb:32 * c + 16 * bb + 16] = acc.T
+        out = np.zeros((16, 16 * n16))
+        for c in range(n16):
+            bias = image_f64["raw"][bias_off // 4 + 16 * c + np.arange(16)]
+            acc = np.tile(bias[:, None], (1, 16))               # [i rows][s]
+            for kb in range(kbr + kbh):
+                if kb < kbr:
+                    h0 = (img_off + (c * kbr + kb) * 2048) // 2
+                else:
+                    h0 = (hbm_off + (c * kbh + kb - kbr) * 2048) // 2
+                frag = image_f64["w"][h0 + lane[:, None] * 8 + j[None, :]]   # hi + lo
+                A = np.zeros((16, 32))
+                Bm = np.zeros((32, 16))
+                for g in range(4):
+                    A[:, 8 * g:8 * g + 8] = frag[np.arange(16) + 16 * g]
+                    Bm[8 * g:8 * g + 8, :] = B[kb][np.arange(16) + 16 * g].T
+                acc += A @ Bm
+            out[:, 16 * c:16 * c + 16] = acc.T
         if lp.relu:
             out = np.maximum(out, 0.0)
         outs.append(out[:, :N])
@@ -288,7 +288,7 @@ def _emulate_fused(plan, fused, image_f64, x_pos, x_dir, dir_rd, relu_floor=True
         xreg = np.zeros((8, 64, 8))
         for c in range(min(nb, 8)):
             rows = 32 * c + 16 * (j[None, :] >> 2) + 4 * g_of[:, None] + (j[None, :] & 3)
-            xreg[c] = out[s_of[:, None], rows]
+            xreg[c] = np.pad(out, ((0, 0), (0, 32 * nb - out.shape[1])))[s_of[:, None], rows]
     return outs
 
 

@@ -15,6 +15,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--M", type=int, default=4096 * 64)
 ap.add_argument("--layerwise", action="store_true")
+ap.add_argument("--train", action="store_true", help="record autograd: every layer output and mask is stored")
 args = ap.parse_args()
 
 import nerf_amd  # noqa: E402
@@ -32,7 +33,7 @@ pos[:, :60] = torch.rand(M, 60, device=dev) * 2 - 1
 dirs = torch.zeros(M // 64, 32, device=dev)
 dirs[:, :24] = torch.rand(M // 64, 24, device=dev) * 2 - 1
 plan = model._get_plan()
-with torch.no_grad():
+with torch.set_grad_enabled(args.train):
     for _ in range(3):
         MLPFunction.apply(plan, M, pos, dirs, 64, *plan.params())
     torch.cuda.synchronize()
@@ -44,5 +45,5 @@ with torch.no_grad():
     torch.cuda.synchronize()
 ms = s.elapsed_time(e) / args.iters
 flops = sum(2.0 * M * lp.module.in_features * lp.module.out_features for lp in plan.layers)
-print(f"{'layerwise' if args.layerwise else 'fused'} forward: {ms * 1e3:.1f} us/iter, "
+print(f"{'layerwise' if args.layerwise else 'fused'} {'training' if args.train else 'inference'} forward: {ms * 1e3:.1f} us/iter, "
       f"{flops / ms / 1e9:.1f} TFLOP/s (fp32-equivalent)")
