@@ -17,7 +17,10 @@ Other BASELINE.json configs as extra workloads (same JSON line, their own `confi
                    CameraExtrinsics (100 views) whose gradients come back through the fused
                    ray-mode encoding backward, 4096 rays per GPU
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload mip|n2v|barf]
+  --workload ingp  configs[4]: 3d-ingp hash-grid NeRF (16-level hash encoding + NerfModelINGP on the fused
+                   MLP), coarse 64 + fine 192 (round/argmax resample), 5120 rays per GPU
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload mip|n2v|barf|ingp]
     (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
 
 Prints ONE JSON line on rank 0 (schema: see DESIGN.md §Measurement).
@@ -52,6 +55,9 @@ WORKLOADS = {
     "mip": {"config": "mip-NeRF masked integrated PE, coarse 64 + fine 128 samples (pdf resample), shared "
                       "NerfModel, Lego 800x800, 4096 rays per GPU (BASELINE.json configs[2])",
             "rays": 4096, "coarse": 64, "fine": 128},
+    "ingp": {"config": "3d-ingp hash-grid NeRF: 16-level hash encoding (16 x 2^16 x 2 fp32 table), NerfModelINGP "
+                       "(8 x 256 MLP, softplus(z - 1)), coarse 64 + fine 192 samples (round/argmax resample), "
+                       "5120 rays per GPU (BASELINE.json configs[4])", "rays": 5120, "coarse": 64, "fine": 192},
     "barf": {"config": "BARF camera-pose refinement: masked Fourier PE L10/L4 + identity, 128 equidistant "
                        "samples, per-image so3 CameraExtrinsics (100 views), 4096 rays per GPU "
                        "(BASELINE.json configs[3])", "rays": 4096, "coarse": 0, "fine": 128},
@@ -237,6 +243,30 @@ def build_workload(name: str, device, rank: int, feed: bool = False):
             o2, d2, _, _ = extr(img, o, d)
             return ren(o2, d2, pw)
         return ren, [ren, extr], opt, loss_fn, render_fn
+    if name == "ingp":
+        from nerf_amd import NerfModelINGP
+        torch.manual_seed(0)
+        model = NerfModelINGP()
+        # 3d-ingp: near/far 2/7, no MAGIC factor in the compositor, round/argmax fine sampling
+        ren = NerfInterpolation(2.0, 7.0, model, w["fine"], "stratified_uniform", 0.0, "middle", model, w["coarse"],
+                                density_factor=(1.0, 1.0), resample_mode=1).to(device)
+        o, d, pw, target, _ = synthetic_batch_lego(w["rays"], 1000 + rank, device, 400)
+        opt = ren.configure_optimizers()["optimizer"]
+        if feed:
+            nxt = _feed_stream(device_feed(name, device, rank, w["rays"]))
+
+            def loss_fn():
+                o_, _, d_, _, c_, _, pw_ = next(nxt)
+                return ren.training_loss(o_, d_, pw_, c_[:, -1])[0]
+
+            def render_fn():
+                o_, _, d_, _, _, _, pw_ = next(nxt)
+                return ren(o_, d_, pw_)
+            return ren, [ren], opt, loss_fn, render_fn
+
+        def loss_fn():
+            return ren.training_loss(o, d, pw, target)[0]
+        return ren, [ren], opt, loss_fn, lambda: ren(o, d, pw)
     raise ValueError(name)
 
 

@@ -77,8 +77,12 @@ __device__ __forceinline__ Corners level_corners(const float* p, int r, int T) {
             c.idx[k] = q[0] + r1 * q[1] + r1 * r1 * q[2];
         } else {
             const long long h = (cc[0] * 1LL) ^ (cc[1] * 2654435761LL) ^ (cc[2] * 805459861LL);
-            long long m = h % (long long)T;
-            c.idx[k] = m < 0 ? m + T : m;
+            if ((T & (T - 1)) == 0) {
+                c.idx[k] = h & (long long)(T - 1);  // two's complement: the non-negative remainder
+            } else {
+                const long long m = h % (long long)T;
+                c.idx[k] = m < 0 ? m + T : m;
+            }
         }
     }
     return c;
@@ -142,34 +146,71 @@ __device__ __forceinline__ int fixed_shift(unsigned gmax_bits, int64_t n) {
     return s > 120 ? 120 : s;
 }
 
-__global__ __launch_bounds__(256) void hashgrid_bwd_kernel(HashArgs a, const float* __restrict__ g, int64_t ld,
-                                                           const unsigned* __restrict__ gmax,
-                                                           unsigned long long* __restrict__ acc) {
-    const int L = a.p.levels, F = a.p.features, T = a.p.table_size;
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t n = t / L;
-    const int l = (int)(t - n * L);
-    if (n >= a.n) return;
+// Backward as (level, part, slab) workgroups: a part is a run of PART_ENTRIES accumulators of one
+// level's table (bijective levels need only (r+1)^3 rows) held in LDS as 64-bit fixed-point sums; the
+// workgroup walks its slab of samples, adds every corner contribution whose row falls in its part
+// with LDS integer atomics, then adds the part to the global accumulators with one contiguous pass of
+// atomics.  Global atomics scattered one lane per row run ~17x below their contiguous rate (they
+// execute at the memory side, one request per lane), so the scattered adds stay on chip and only
+// coalesced ones leave it; positions and corners are recomputed per part (cheap VALU).
+constexpr int PART_ENTRIES = 16384;                 // 128 KiB of int64 per workgroup
+constexpr int BWD_THREADS = 1024;
+
+struct BwdPlan {
+    int start[NERF_HASHGRID_MAX_LEVELS + 1];        // prefix of parts per level
+    int rows_per_part;
+    int parts;                                      // parts of all levels (workgroups per slab)
+    int64_t slab;                                   // samples per slab
+};
+
+__host__ __device__ inline int64_t level_rows(int r, int T) {
+    const int64_t r1 = r + 1;
+    return r1 * r1 * r1 <= T ? r1 * r1 * r1 : T;
+}
+
+__global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_kernel(HashArgs a, BwdPlan pl, const float* __restrict__ g,
+                                                                   int64_t ld, const unsigned* __restrict__ gmax,
+                                                                   unsigned long long* __restrict__ acc) {
+    __shared__ unsigned long long part[PART_ENTRIES];
+    const int F = a.p.features, T = a.p.table_size;
+    const int w = (int)(blockIdx.x % (unsigned)pl.parts);
+    const int64_t slab = blockIdx.x / (unsigned)pl.parts;
+    int l = 0;
+    while (w >= pl.start[l + 1]) ++l;
+    const int64_t row0 = (int64_t)(w - pl.start[l]) * pl.rows_per_part;
+    const int64_t rows = level_rows(a.p.res[l], T) - row0;
+    const int prow = (int)(rows < pl.rows_per_part ? rows : pl.rows_per_part);
     const int s = fixed_shift(*gmax, a.n);
-    if (s == -1000) return;
+    if (s == -1000) return;                         // uniform: the finish pass writes NaN
     const double scale = ldexp(1.0, s);
-    float p[3];
-    sample_position(a, n, p);
-    const Corners c = level_corners(p, a.p.res[l], T);
-    unsigned long long* base = acc + (int64_t)l * T * F;
-    const float* gr = g + n * ld + (int64_t)l * F;
-    float gv[NERF_HASHGRID_MAX_FEATURES];
+    for (int e = threadIdx.x; e < prow * F; e += BWD_THREADS) part[e] = 0ull;
+    __syncthreads();
+    const int64_t n1 = (slab + 1) * pl.slab < a.n ? (slab + 1) * pl.slab : a.n;
+    for (int64_t n = slab * pl.slab + threadIdx.x; n < n1; n += BWD_THREADS) {
+        float p[3];
+        sample_position(a, n, p);
+        const Corners c = level_corners(p, a.p.res[l], T);
+        float gv[NERF_HASHGRID_MAX_FEATURES];
 #pragma unroll
-    for (int f = 0; f < NERF_HASHGRID_MAX_FEATURES; ++f) gv[f] = f < F ? gr[f] : 0.0f;
+        for (int f = 0; f < NERF_HASHGRID_MAX_FEATURES; ++f) gv[f] = f < F ? g[n * ld + (int64_t)l * F + f] : 0.0f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < 8; ++k) {
+            const int64_t rel = c.idx[k] - row0;
+            if ((uint64_t)rel >= (uint64_t)prow) continue;
 #pragma unroll
-        for (int f = 0; f < NERF_HASHGRID_MAX_FEATURES; ++f) {
-            if (f >= F) continue;
-            // w * g is exact in fp64 (two 24-bit mantissas); one rounding to the fixed-point grid
-            const long long q = llrint((double)c.w[k] * (double)gv[f] * scale);
-            if (q != 0) atomicAdd(base + c.idx[k] * F + f, (unsigned long long)q);
+            for (int f = 0; f < NERF_HASHGRID_MAX_FEATURES; ++f) {
+                if (f >= F) continue;
+                // w * g is exact in fp64 (two 24-bit mantissas); one rounding to the fixed-point grid
+                const long long q = llrint((double)c.w[k] * (double)gv[f] * scale);
+                if (q != 0) atomicAdd(&part[rel * F + f], (unsigned long long)q);
+            }
         }
+    }
+    __syncthreads();
+    unsigned long long* dst = acc + ((int64_t)l * T + row0) * F;
+    for (int e = threadIdx.x; e < prow * F; e += BWD_THREADS) {
+        const unsigned long long v = part[e];
+        if (v != 0ull) atomicAdd(dst + e, v);
     }
 }
 
@@ -244,8 +285,19 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
         hipLaunchKernelGGL(hashgrid_gmax_kernel, dim3((unsigned)blocks), dim3(256), 0, s, grad_out, g_ld, n_samples,
                            cols, gmax);
         NERF_CHECK_LAUNCH();
-        const int64_t threads = n_samples * params->levels;
-        hipLaunchKernelGGL(hashgrid_bwd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, a,
+        BwdPlan pl{};
+        pl.rows_per_part = PART_ENTRIES / params->features;
+        for (int l = 0; l < params->levels; ++l) {
+            const int64_t rows = level_rows(params->res[l], params->table_size);
+            pl.start[l + 1] = pl.start[l] + (int)((rows + pl.rows_per_part - 1) / pl.rows_per_part);
+        }
+        pl.parts = pl.start[params->levels];
+        // about four workgroups per CU in all, slabs of at least 4096 samples
+        int64_t slabs = (1024 + pl.parts - 1) / pl.parts;
+        const int64_t most = (n_samples + 4095) / 4096;
+        slabs = slabs < most ? slabs : most;
+        pl.slab = (n_samples + slabs - 1) / slabs;
+        hipLaunchKernelGGL(hashgrid_bwd_kernel, dim3((unsigned)(slabs * pl.parts)), dim3(BWD_THREADS), 0, s, a, pl,
                            grad_out, g_ld, gmax, acc);
         NERF_CHECK_LAUNCH();
     }
