@@ -117,14 +117,29 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(HashArgs a, const flo
 
 // max |grad_out| over the batch as the bits of a non-negative float (order-preserving as uint32);
 // non-finite values land above every finite one
+template <int V>
 __global__ __launch_bounds__(256) void hashgrid_gmax_kernel(const float* __restrict__ g, int64_t ld, int64_t n,
                                                             int cols, unsigned* __restrict__ gmax) {
+    // V-float vectors of the [n, cols] block of rows of stride ld; 32-bit index math when it fits
+    const int cv = cols / V;
+    const int64_t total = n * cv;
+    const bool small = total < ((int64_t)1 << 31);
     unsigned m = 0;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n * cols; i += (int64_t)gridDim.x * 256) {
-        const int64_t r = i / cols;
-        const float v = fabsf(g[r * ld + (i - r * cols)]);
-        const unsigned b = __float_as_uint(v);
-        m = b > m ? b : m;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int64_t r = small ? (int64_t)((unsigned)i / (unsigned)cv) : i / cv;
+        const float* p = g + r * ld + (i - r * cv) * V;
+        float v[V];
+        if constexpr (V == 4) {
+            const float4 q = *reinterpret_cast<const float4*>(p);
+            v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+        } else {
+            v[0] = p[0];
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const unsigned b = __float_as_uint(fabsf(v[j]));
+            m = b > m ? b : m;
+        }
     }
     for (int off = 32; off > 0; off >>= 1) {
         const unsigned o = __shfl_xor(m, off, 64);
@@ -168,41 +183,102 @@ __host__ __device__ inline int64_t level_rows(int r, int T) {
     return r1 * r1 * r1 <= T ? r1 * r1 * r1 : T;
 }
 
+// Each thread takes BWD_UNROLL samples per trip and issues all their loads (positions or ray
+// origin / direction / interval, and the F gradient values) before any is used, so a trip costs one
+// memory round trip instead of one per load.
+constexpr int BWD_UNROLL = 4;
+
+template <int F>
 __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_kernel(HashArgs a, BwdPlan pl, const float* __restrict__ g,
                                                                    int64_t ld, const unsigned* __restrict__ gmax,
                                                                    unsigned long long* __restrict__ acc) {
+#pragma clang fp contract(off)
     __shared__ unsigned long long part[PART_ENTRIES];
-    const int F = a.p.features, T = a.p.table_size;
+    const int T = a.p.table_size;
     const int w = (int)(blockIdx.x % (unsigned)pl.parts);
     const int64_t slab = blockIdx.x / (unsigned)pl.parts;
     int l = 0;
     while (w >= pl.start[l + 1]) ++l;
+    const int res = a.p.res[l];
     const int64_t row0 = (int64_t)(w - pl.start[l]) * pl.rows_per_part;
-    const int64_t rows = level_rows(a.p.res[l], T) - row0;
+    const int64_t rows = level_rows(res, T) - row0;
     const int prow = (int)(rows < pl.rows_per_part ? rows : pl.rows_per_part);
     const int s = fixed_shift(*gmax, a.n);
     if (s == -1000) return;                         // uniform: the finish pass writes NaN
     const double scale = ldexp(1.0, s);
     for (int e = threadIdx.x; e < prow * F; e += BWD_THREADS) part[e] = 0ull;
     __syncthreads();
+    const bool rays = a.x == nullptr, mid = a.p.query != 0, small = a.n < ((int64_t)1 << 31);
     const int64_t n1 = (slab + 1) * pl.slab < a.n ? (slab + 1) * pl.slab : a.n;
-    for (int64_t n = slab * pl.slab + threadIdx.x; n < n1; n += BWD_THREADS) {
-        float p[3];
-        sample_position(a, n, p);
-        const Corners c = level_corners(p, a.p.res[l], T);
-        float gv[NERF_HASHGRID_MAX_FEATURES];
+    for (int64_t nb = slab * pl.slab + threadIdx.x; nb < n1; nb += BWD_UNROLL * BWD_THREADS) {
+        float p[BWD_UNROLL][3], gv[BWD_UNROLL][F];
+        // loads first (indices clamped into the slab, so every load is in bounds) ...
+        if (rays) {
+            float t0[BWD_UNROLL], t1[BWD_UNROLL], o[BWD_UNROLL][3], d[BWD_UNROLL][3];
 #pragma unroll
-        for (int f = 0; f < NERF_HASHGRID_MAX_FEATURES; ++f) gv[f] = f < F ? g[n * ld + (int64_t)l * F + f] : 0.0f;
+            for (int u = 0; u < BWD_UNROLL; ++u) {
+                const int64_t n = nb + u * BWD_THREADS < n1 ? nb + u * BWD_THREADS : n1 - 1;
+                const int64_t ray = small ? (int64_t)((unsigned)n / (unsigned)a.spr) : n / a.spr;
+                t0[u] = a.t0[n];
+                t1[u] = mid ? a.t1[n] : 0.0f;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int64_t rel = c.idx[k] - row0;
-            if ((uint64_t)rel >= (uint64_t)prow) continue;
+                for (int j = 0; j < 3; ++j) {
+                    o[u][j] = a.o[ray * 3 + j];
+                    d[u][j] = a.d[ray * 3 + j];
+                }
 #pragma unroll
-            for (int f = 0; f < NERF_HASHGRID_MAX_FEATURES; ++f) {
-                if (f >= F) continue;
-                // w * g is exact in fp64 (two 24-bit mantissas); one rounding to the fixed-point grid
-                const long long q = llrint((double)c.w[k] * (double)gv[f] * scale);
-                if (q != 0) atomicAdd(&part[rel * F + f], (unsigned long long)q);
+                for (int f = 0; f < F; ++f) gv[u][f] = g[n * ld + (int64_t)l * F + f];
+            }
+            // ... then the positions, as sample_position computes them
+#pragma unroll
+            for (int u = 0; u < BWD_UNROLL; ++u) {
+                const float tq = mid ? (t0[u] + t1[u]) / 2.0f : t0[u];
+#pragma unroll
+                for (int j = 0; j < 3; ++j) p[u][j] = o[u][j] + tq * d[u][j];
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < BWD_UNROLL; ++u) {
+                const int64_t n = nb + u * BWD_THREADS < n1 ? nb + u * BWD_THREADS : n1 - 1;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) p[u][j] = a.x[n * 3 + j];
+#pragma unroll
+                for (int f = 0; f < F; ++f) gv[u][f] = g[n * ld + (int64_t)l * F + f];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < BWD_UNROLL; ++u) {
+            if (nb + u * BWD_THREADS >= n1) continue;
+            const Corners c = level_corners(p[u], res, T);
+            // An LDS atomic costs the same per wave-instruction however few lanes are active, and a
+            // part holds only ~1/parts of a sample's corners: so each lane queues its in-range
+            // corners and the wave issues one add per queued-corner round (its longest queue)
+            // instead of one per corner.
+            unsigned pend = 0;
+            int rel[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int64_t r = c.idx[k] - row0;
+                rel[k] = (int)r;
+                if ((uint64_t)r < (uint64_t)prow) pend |= 1u << k;
+            }
+            while (pend != 0u) {
+                const int k = __builtin_ctz(pend);
+                pend &= pend - 1u;
+                int rk = rel[0];
+                float wk = c.w[0];
+#pragma unroll
+                for (int j = 1; j < 8; ++j)
+                    if (k == j) {
+                        rk = rel[j];
+                        wk = c.w[j];
+                    }
+#pragma unroll
+                for (int f = 0; f < F; ++f) {
+                    // w * g is exact in fp64 (two 24-bit mantissas); one rounding to the fixed-point grid
+                    const long long q = llrint((double)wk * (double)gv[u][f] * scale);
+                    if (q != 0) atomicAdd(&part[rk * F + f], (unsigned long long)q);
+                }
             }
         }
     }
@@ -212,6 +288,12 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_kernel(HashArgs a, B
         const unsigned long long v = part[e];
         if (v != 0ull) atomicAdd(dst + e, v);
     }
+}
+
+template <int F>
+void launch_bwd(int64_t blocks, hipStream_t s, const HashArgs& a, const BwdPlan& pl, const float* g, int64_t ld,
+                const unsigned* gmax, unsigned long long* acc) {
+    hipLaunchKernelGGL(hashgrid_bwd_kernel<F>, dim3((unsigned)blocks), dim3(BWD_THREADS), 0, s, a, pl, g, ld, gmax, acc);
 }
 
 // table gradient = accumulator * 2^-s (or NaN after a non-finite gradient); the accumulators are
@@ -280,10 +362,15 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
     HashArgs a{*params, x, ray_o, ray_d, t_start, t_end, n_samples, samples_per_ray};
     if (n_samples > 0) {
         const int cols = params->levels * params->features;
-        int64_t blocks = (n_samples * cols + 255) / 256;
-        blocks = blocks < 2048 ? blocks : 2048;
-        hipLaunchKernelGGL(hashgrid_gmax_kernel, dim3((unsigned)blocks), dim3(256), 0, s, grad_out, g_ld, n_samples,
-                           cols, gmax);
+        const bool vec = cols % 4 == 0 && g_ld % 4 == 0 && (reinterpret_cast<uintptr_t>(grad_out) & 15) == 0;
+        int64_t blocks = (n_samples * (vec ? cols / 4 : cols) + 255) / 256;
+        blocks = blocks < 4096 ? blocks : 4096;
+        if (vec)
+            hipLaunchKernelGGL(hashgrid_gmax_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, s, grad_out, g_ld,
+                               n_samples, cols, gmax);
+        else
+            hipLaunchKernelGGL(hashgrid_gmax_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, s, grad_out, g_ld,
+                               n_samples, cols, gmax);
         NERF_CHECK_LAUNCH();
         BwdPlan pl{};
         pl.rows_per_part = PART_ENTRIES / params->features;
@@ -297,8 +384,19 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
         const int64_t most = (n_samples + 4095) / 4096;
         slabs = slabs < most ? slabs : most;
         pl.slab = (n_samples + slabs - 1) / slabs;
-        hipLaunchKernelGGL(hashgrid_bwd_kernel, dim3((unsigned)(slabs * pl.parts)), dim3(BWD_THREADS), 0, s, a, pl,
-                           grad_out, g_ld, gmax, acc);
+        void (*launch)(int64_t, hipStream_t, const HashArgs&, const BwdPlan&, const float*, int64_t,
+                       const unsigned*, unsigned long long*) = nullptr;
+        switch (params->features) {
+            case 1: launch = launch_bwd<1>; break;
+            case 2: launch = launch_bwd<2>; break;
+            case 3: launch = launch_bwd<3>; break;
+            case 4: launch = launch_bwd<4>; break;
+            case 5: launch = launch_bwd<5>; break;
+            case 6: launch = launch_bwd<6>; break;
+            case 7: launch = launch_bwd<7>; break;
+            default: launch = launch_bwd<8>; break;
+        }
+        launch(slabs * pl.parts, s, a, pl, grad_out, g_ld, gmax, acc);
         NERF_CHECK_LAUNCH();
     }
     int64_t fb = (count + 255) / 256;

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--spr", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--table", type=int, default=2 ** 16)
+    ap.add_argument("--only", type=int, default=None, help="time just this level (for PMC passes)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -56,6 +57,10 @@ def main():
         b = timed(lambda: kernels.hashgrid_bwd(p, gout, gt, ws, **kw))
         return f, b
 
+    if args.only is not None:
+        f, b = run([res_all[args.only]])
+        print(f"level {args.only}: fwd {f * 1e3:8.1f} us  bwd {b * 1e3:8.1f} us")
+        return
     f, b = run(res_all)
     print(f"all {len(res_all)} levels: fwd {f * 1e3:8.1f} us  bwd {b * 1e3:8.1f} us  ({n} samples)")
     for l, r in enumerate(res_all):
