@@ -425,6 +425,55 @@ def _roofline(ks_fn: dict, x3: bool, steps: int, workload: str):
             "pmc": pmc}
 
 
+def init_distributed(backend: str = "nccl"):
+    """(world, rank, local_rank, torch.distributed or None) from the torchrun environment; one
+    process per GPU ("nccl" = RCCL on ROCm), "gloo" for the CPU rehearsal in tests/."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world <= 1:
+        return world, rank, local_rank, None
+    import torch.distributed as dist
+    if backend == "nccl":
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        dist.init_process_group(backend)
+    return world, rank, local_rank, dist
+
+
+def run_timed(step, steps: int, warmup: int, dist, sync, device, on_timed_start=None):
+    """W untimed warmup steps, then EXACTLY K steps bracketed by barrier + device sync on both sides;
+    returns (max over ranks of the timed wall time, the last step's return value)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    if on_timed_start is not None:
+        on_timed_start()
+    out = None
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = step()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, out
+
+
+def teardown(dist) -> None:
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -446,25 +495,19 @@ def main():
     args = ap.parse_args()
     torch.set_float32_matmul_precision(args.matmul_precision)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    world, rank, local_rank, dist = init_distributed("nccl")
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
 
     import nerf_amd
     from nerf_amd import kernels as K
-    from nerf_amd.ddp import GradAllReduce
+    from nerf_amd.ddp import BucketedGradAllReduce
     nerf_amd._lib.load()
 
     wl = WORKLOADS[args.workload]
     ren, modules, opt, loss_fn, render_fn = build_workload(args.workload, device, rank, args.feed == "device")
-    allreduce = GradAllReduce([p for m in modules for p in m.parameters()])
+    # gradient buckets all-reduced asynchronously from post-accumulate-grad hooks (no-op at N=1)
+    allreduce = BucketedGradAllReduce([p for m in modules for p in m.parameters()])
     torch.manual_seed(1234 + rank)
     render = args.mode == "render"
 
@@ -476,32 +519,15 @@ def main():
         opt.zero_grad(set_to_none=True)
         loss = loss_fn()
         loss.backward()
-        if dist is not None:
-            allreduce()          # one RCCL all-reduce of the flat gradient bucket
+        allreduce.finish()       # waits for the bucket all-reduces launched during backward
         opt.step()
         return loss
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
+    def start_timer():
+        K.TIMER = K.KernelTimer()
 
-    K.TIMER = K.KernelTimer()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    elapsed, loss = run_timed(step, args.steps, args.warmup, dist, torch.cuda.synchronize, device, start_timer)
     timer, K.TIMER = K.TIMER, None
-    if dist is not None:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
     final_loss = float(loss.item())
 
     samples_per_gpu = wl["rays"] * (wl["coarse"] + wl["fine"])
@@ -543,7 +569,7 @@ def main():
             "config": {"workload": wl["config"], "workload_key": args.workload,
                        "rays_per_gpu": wl["rays"], "samples_per_ray": wl["coarse"] + wl["fine"],
                        "coarse_samples": wl["coarse"], "fine_samples": wl["fine"], "global_rays": wl["rays"] * world,
-                       "parallelism": f"ray-batch dp{world}" + (" (RCCL all-reduce)" if world > 1 else "")},
+                       "parallelism": f"ray-batch dp{world}" + (" (RCCL bucketed all-reduce from post-accumulate-grad hooks)" if world > 1 else "")},
             "roofline": roofline,
             "roofline_hbm": {"kernel": "encode_fwd + composite_fwd + composite_bwd (positional encoding and "
                                        "alpha compositing; algorithmic bytes per launch)",
@@ -567,8 +593,7 @@ def main():
             if cb is not None:
                 out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    teardown(dist)
 
 
 if __name__ == "__main__":

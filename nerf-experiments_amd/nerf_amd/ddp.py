@@ -1,10 +1,14 @@
-"""Ray-batch data parallelism: one process per GPU, one gradient all-reduce per step.
+"""Ray-batch data parallelism: one process per GPU, the gradient mean as the only exchange.
 
 Rays are independent through sampling, encoding, the field MLP, compositing and
 resampling, so every rank renders its own ray shard and the only
-exchange is the mean of the parameter gradients — one flat fp32 bucket (~2.6 MB
-for NerfModel) per step over RCCL ("nccl" backend = RCCL on ROCm; xGMI on one
-node).  The reference itself is single-device (run_barf.py:103-148).
+exchange is the mean of the parameter gradients (~2.6 MB fp32 for NerfModel) per
+step over RCCL ("nccl" backend = RCCL on ROCm; xGMI on one node).  The reference
+itself is single-device (run_barf.py:103-148).
+
+``BucketedGradAllReduce`` (what bench.py uses) launches one asynchronous all-reduce
+per gradient bucket from post-accumulate-grad hooks while the backward pass is still
+running; ``GradAllReduce`` is the one-collective-after-backward form.
 """
 from __future__ import annotations
 
@@ -49,6 +53,143 @@ class GradAllReduce:
             used = (parts[-1] > 0).tolist()       # host read of the reduced flags (only here)
         for i, (p, g) in enumerate(zip(self.params, parts[:-1])):
             p.grad = g.view_as(p) if used is None or used[i] else None
+
+
+class _Bucket:
+    __slots__ = ("params", "offsets", "flat", "flags_at", "ready", "pending", "handle", "launched")
+
+    def __init__(self, params, device, dtype):
+        self.params = params
+        self.offsets = []
+        off = 0
+        for p in params:
+            self.offsets.append(off)
+            off += p.numel()
+        self.flags_at = off
+        # gradients, then one "has a gradient" flag per parameter
+        self.flat = torch.zeros(off + len(params), device=device, dtype=dtype)
+        self.ready = [False] * len(params)
+        self.pending = len(params)
+        self.handle = None
+        self.launched = False
+
+    def view(self, j):
+        p = self.params[j]
+        return self.flat[self.offsets[j]:self.offsets[j] + p.numel()].view_as(p)
+
+
+class BucketedGradAllReduce:
+    """Gradient mean across the process group, overlapped with the backward pass.
+
+    Parameters are split into buckets of about ``bucket_bytes`` in REVERSE registration order (the
+    order backward produces their gradients).  A post-accumulate-grad hook moves each gradient into
+    its bucket (no copy when ``.grad`` already is the bucket view, as after
+    ``zero_grad(set_to_none=False)``) and, once a bucket is complete, launches its all-reduce
+    asynchronously (RCCL runs it on its own stream while backward continues).  Buckets launch
+    strictly in bucket order on every rank, so the collective sequence matches across ranks even when
+    gradients arrive in different orders.  ``finish()`` (after ``backward()``, before the optimizer)
+    launches the buckets still incomplete — a parameter without a local gradient contributes zeros
+    and a 0 flag — waits for all of them and leaves every ``.grad`` as a view of its reduced bucket;
+    a parameter that NO rank produced a gradient for ends with ``.grad = None`` on every rank, as
+    with one process (the reduced flags are read on the host only by a rank that itself lacked a
+    gradient).  Gradients are pre-scaled by 1/world and summed.  One backward per ``finish()``.
+    With world size 1 (or no process group) every method is a no-op and ``.grad`` is untouched."""
+
+    def __init__(self, params, bucket_bytes: int = 1 << 20, group=None):
+        seen, plist = set(), []
+        for p in params:
+            if p.requires_grad and id(p) not in seen:
+                seen.add(id(p))
+                plist.append(p)
+        self.params = plist
+        self.group = group
+        self.active = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        self.world = dist.get_world_size(group) if self.active else 1
+        self.buckets: list[_Bucket] = []
+        self._where = {}
+        self._next = 0
+        self._hooks = []
+        if not self.active:
+            return
+        cur, cur_bytes = [], 0
+        for p in reversed(plist):
+            if cur and (cur_bytes + p.numel() * p.element_size() > bucket_bytes
+                        or p.device != cur[0].device or p.dtype != cur[0].dtype):
+                self.buckets.append(_Bucket(cur, cur[0].device, cur[0].dtype))
+                cur, cur_bytes = [], 0
+            cur.append(p)
+            cur_bytes += p.numel() * p.element_size()
+        if cur:
+            self.buckets.append(_Bucket(cur, cur[0].device, cur[0].dtype))
+        for bi, b in enumerate(self.buckets):
+            for j, p in enumerate(b.params):
+                self._where[id(p)] = (bi, j)
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._hook))
+
+    def _hook(self, p) -> None:
+        bi, j = self._where[id(p)]
+        b = self.buckets[bi]
+        if b.launched or b.ready[j]:
+            raise RuntimeError("BucketedGradAllReduce: a gradient arrived twice in one step; call finish() "
+                               "after every backward()")
+        v = b.view(j)
+        if p.grad.data_ptr() != v.data_ptr():
+            v.copy_(p.grad)
+            p.grad = v
+        b.ready[j] = True
+        b.pending -= 1
+        self._launch_ready()
+
+    def _launch(self, b: _Bucket) -> None:
+        b.flat[b.flags_at:].fill_(1.0)
+        for j, r in enumerate(b.ready):
+            if not r:
+                b.flat[b.flags_at + j].fill_(0.0)
+        if self.world > 1:
+            b.flat.mul_(1.0 / self.world)
+        b.handle = dist.all_reduce(b.flat, group=self.group, async_op=True)
+        b.launched = True
+
+    def _launch_ready(self) -> None:
+        while self._next < len(self.buckets) and self.buckets[self._next].pending == 0:
+            self._launch(self.buckets[self._next])
+            self._next += 1
+
+    def finish(self) -> None:
+        if not self.active:
+            return
+        missing = []
+        for b in self.buckets[self._next:]:
+            for j, p in enumerate(b.params):
+                if not b.ready[j]:
+                    b.view(j).zero_()
+                    missing.append((b, j))
+            self._launch(b)
+        self._next = len(self.buckets)
+        for b in self.buckets:
+            b.handle.wait()
+        used = None
+        if missing:
+            used = {(id(b), j): f > 0 for b in {id(b): b for b, _ in missing}.values()
+                    for j, f in enumerate(b.flat[b.flags_at:].tolist())}
+        for b in self.buckets:
+            for j, p in enumerate(b.params):
+                if used is not None and not used.get((id(b), j), True):
+                    p.grad = None
+                else:
+                    p.grad = b.view(j)
+            b.ready = [False] * len(b.params)
+            b.pending = len(b.params)
+            b.handle = None
+            b.launched = False
+        self._next = 0
+
+    __call__ = finish
+
+    def remove(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
 
 
 def shard_rays(n_global: int, rank: int, world: int) -> slice:
