@@ -212,6 +212,8 @@ typedef struct nerf_seg {
                                 multiple of 16); bit b of word 2e+h <-> column 4(32h+b)+e */
 #define NERF_EPI_NO_PERSIST 256  /* tuning: one tile per workgroup instead of a persistent grid */
 #define NERF_EPI_NARROW_TILE 512 /* tuning: force the 128-column tile of the split-precision kernel for N > 128 */
+#define NERF_EPI_GAUSS     1024  /* internal (nerf_linear_gauss_x3): Gaussian activation forward */
+#define NERF_EPI_GAUSS_BWD 2048  /* internal (nerf_linear_gauss_x3): Gaussian activation backward */
 
 /* out[m, n] = epi( sum_k A[m, k] * W[n, k] ),  m < M, n < N.
  * W: packed row-major [ceil(N/128)*128][ldw], ldw = sum_j kp_j (zero padding
@@ -341,6 +343,28 @@ int nerf_fused_pack(const float* const* srcs, int32_t n_srcs, const int32_t* map
  * workspace: nerf_gauss_act_workspace(M, N) bytes.  accumulate: grad_inv_std += result.
  * ------------------------------------------------------------------------- */
 size_t nerf_gauss_act_workspace(int64_t M, int32_t N);
+
+/* Split-precision linear layer with the Gaussian activation in its epilogue (no separate
+ * activation pass over HBM).  inv_std [N]; v_n = inv_std_n^2 + 1e-6; every element formula and
+ * rounding as nerf_gauss_act_fwd / _bwd.
+ *   mode NERF_GAUSS_FWD: z = A W^T + bias -> out (the pre-activation the backward needs) and
+ *     y = exp((-(z*z)) * v) -> y (row stride ld_y).  grad_inv_std / workspace unused.
+ *   mode NERF_GAUSS_BWD: g = A W^T (the gradient w.r.t. this layer's activation, bias must be
+ *     NULL); z = this layer's pre-activation (row stride ld_z); out = grad_z = (((-ge)*2)*z)*v
+ *     with ge = g * exp((-(z*z)) * v); grad_inv_std_n (+)= (sum_m (-ge) z^2) * (2 inv_std_n),
+ *     the column sums formed per row tile in fp64 in a fixed order and the tiles summed in a
+ *     fixed order (deterministic).  workspace: nerf_linear_gauss_workspace(M, N) bytes.
+ * Requires N % 4 == 0, 16-byte aligned out / y / z / bias rows (row strides multiples of 4);
+ * returns NERF_ERR_UNSUPPORTED otherwise (callers then use nerf_linear_fwd_x3 +
+ * nerf_gauss_act_fwd / _bwd). */
+#define NERF_GAUSS_FWD 0
+#define NERF_GAUSS_BWD 1
+size_t nerf_linear_gauss_workspace(int64_t M, int32_t N);
+int nerf_linear_gauss_x3(const nerf_seg* segs, int32_t n_segs, int64_t M, const void* W_x, int32_t ldw,
+                         int32_t N, const float* bias, float* out, int64_t ldo, int32_t mode,
+                         const float* inv_std, float* y, int64_t ld_y, const float* z, int64_t ld_z,
+                         float* grad_inv_std, int32_t accumulate, void* workspace, size_t workspace_bytes,
+                         void* stream);
 int nerf_gauss_act_fwd(const float* z, int64_t ld_z, const float* inv_std, int64_t M, int32_t N,
                        float* y, int64_t ld_y, void* stream);
 int nerf_gauss_act_bwd(const float* grad_y, int64_t ld_g, const float* z, int64_t ld_z,

@@ -261,4 +261,12 @@ __device__ __forceinline__ void epi_quad(const EpiOut& E, bool ok, int m, int n,
         store_quad_bits<G>((unsigned char*)E.aux + (int64_t)m * E.ldaux, m < E.M, (n >> 2) & ~(G - 1), nib);
 }
 
+// Column sums of per-row-tile fp64 partials [slabs][N] for the Gaussian activation's
+// inverse-std gradient (gauss.hip): ds_n (+)= (float)(sum_i partial[i][n]) * (2 * s_n), summed in
+// a fixed order (chunks of slabs in parallel, then the chunks in order).  scratch holds
+// gauss_reduce_scratch(N) bytes.
+size_t gauss_reduce_scratch(int N);
+int gauss_reduce(const double* partial, int64_t slabs, int N, const float* s, float* ds, int accumulate,
+                 double* scratch, hipStream_t stream);
+
 }  // namespace nerf

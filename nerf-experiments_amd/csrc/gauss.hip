@@ -12,8 +12,9 @@
 // activation buffers).  Both kernels map 64 consecutive lanes to 64 consecutive columns of
 // one row, so every load/store is a coalesced 256-byte wave access; the backward keeps one
 // fp64 column partial per thread over a slab of rows, reduces the 4 row groups of a block
-// through LDS and writes one partial row per slab; nerf_gauss_act_bwd then sums the slabs in
-// a fixed order (deterministic, no atomics).
+// through LDS and writes one partial row per slab; nerf::gauss_reduce then sums the slabs in
+// a fixed order (deterministic, no atomics).  The same reduction serves the fused
+// linear + Gaussian-activation epilogue of linear_x3.hip (nerf_linear_gauss_x3).
 #include "common.h"
 
 using namespace nerf;
@@ -76,14 +77,35 @@ __global__ __launch_bounds__(256) void gauss_bwd_kernel(const float* g, int64_t 
     }
 }
 
-__global__ __launch_bounds__(256) void gauss_reduce_kernel(const double* __restrict__ partial, int slabs, int N,
-                                                           const float* __restrict__ s, float* __restrict__ ds,
-                                                           int accumulate) {
+// Column sums of the slab partials in two fixed-order levels: block (column group, chunk) sums
+// its chunk's slabs (4 row groups, each a strided run, combined in order), then one thread per
+// column sums the chunks in order.
+constexpr int kMaxChunks = 64;
+
+__global__ __launch_bounds__(256) void gauss_reduce_chunks_kernel(const double* __restrict__ partial, int64_t slabs,
+                                                                  int N, int64_t chunk, double* __restrict__ out2) {
+    __shared__ double red[kRowGroups][kCols];
+    const int c = threadIdx.x & (kCols - 1);
+    const int rg = threadIdx.x >> 6;
+    const int n = blockIdx.x * kCols + c;
+    const int64_t i0 = (int64_t)blockIdx.y * chunk;
+    const int64_t i1 = i0 + chunk < slabs ? i0 + chunk : slabs;
+    double acc = 0.0;
+    if (n < N)
+        for (int64_t i = i0 + rg; i < i1; i += kRowGroups) acc += partial[i * N + n];
+    red[rg][c] = acc;
+    __syncthreads();
+    if (rg == 0 && n < N) out2[(int64_t)blockIdx.y * N + n] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+}
+
+__global__ __launch_bounds__(256) void gauss_reduce_final_kernel(const double* __restrict__ out2, int chunks, int N,
+                                                                 const float* __restrict__ s, float* __restrict__ ds,
+                                                                 int accumulate) {
 #pragma clang fp contract(off)
     const int n = blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= N) return;
     double t = 0.0;
-    for (int i = 0; i < slabs; ++i) t += partial[(int64_t)i * N + n];
+    for (int i = 0; i < chunks; ++i) t += out2[(int64_t)i * N + n];
     const float sv = s[n];
     const float r = ((float)t) * (2.0f * sv);
     ds[n] = accumulate ? ds[n] + r : r;
@@ -99,9 +121,26 @@ int64_t slabs_for(int64_t M) {
 
 }  // namespace
 
+size_t nerf::gauss_reduce_scratch(int N) { return (size_t)kMaxChunks * (size_t)(N > 0 ? N : 0) * sizeof(double); }
+
+int nerf::gauss_reduce(const double* partial, int64_t slabs, int N, const float* s, float* ds, int accumulate,
+                       double* scratch, hipStream_t st) {
+    int64_t chunks = (slabs + 63) / 64;
+    chunks = chunks < 1 ? 1 : (chunks > kMaxChunks ? kMaxChunks : chunks);
+    const int64_t chunk = (slabs + chunks - 1) / chunks;
+    chunks = (slabs + chunk - 1) / chunk;
+    hipLaunchKernelGGL(gauss_reduce_chunks_kernel, dim3((unsigned)((N + kCols - 1) / kCols), (unsigned)chunks),
+                       dim3(256), 0, st, partial, slabs, N, chunk, scratch);
+    if (hipGetLastError() != hipSuccess) return NERF_ERR_LAUNCH;
+    hipLaunchKernelGGL(gauss_reduce_final_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, scratch,
+                       (int)chunks, N, s, ds, accumulate);
+    if (hipGetLastError() != hipSuccess) return NERF_ERR_LAUNCH;
+    return NERF_OK;
+}
+
 extern "C" size_t nerf_gauss_act_workspace(int64_t M, int32_t N) {
     if (M <= 0 || N <= 0) return 0;
-    return (size_t)slabs_for(M) * (size_t)N * sizeof(double);
+    return (size_t)slabs_for(M) * (size_t)N * sizeof(double) + nerf::gauss_reduce_scratch(N);
 }
 
 extern "C" int nerf_gauss_act_fwd(const float* z, int64_t ld_z, const float* inv_std, int64_t M, int32_t N, float* y,
@@ -141,8 +180,5 @@ extern "C" int nerf_gauss_act_bwd(const float* grad_y, int64_t ld_g, const float
     hipLaunchKernelGGL(gauss_bwd_kernel, grid, dim3(256), 0, st, grad_y, ld_g, z, ld_z, inv_std, M, N, grad_z, ld_dz,
                        rows, partial);
     NERF_CHECK_LAUNCH();
-    hipLaunchKernelGGL(gauss_reduce_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, partial,
-                       (int)slabs, N, inv_std, grad_inv_std, accumulate);
-    NERF_CHECK_LAUNCH();
-    return NERF_OK;
+    return nerf::gauss_reduce(partial, slabs, N, inv_std, grad_inv_std, accumulate, partial + slabs * N, st);
 }

@@ -99,7 +99,47 @@ struct NTArgs {
     int epi;
     const float* aux; int64_t ldaux;
     int vec_ok;
+    // Gaussian-activation epilogues (nerf_linear_gauss_x3): inverse std, activation output,
+    // per-row-tile fp64 column partials of the inverse-std gradient
+    const float* gs; float* y2; int64_t ldy2; double* part;
 };
+
+// Gaussian activation (garf/gaussian.py:8-31) on a column quad, with exactly the element
+// formulas of gauss.hip: v = s^2 + 1e-6, y = exp((-(z*z)) * v); backward ge = g * exp((-(z*z)) v),
+// dz = (((-ge) * 2) * z) * v, column partial += (double)((-ge) * z^2).
+__device__ __forceinline__ f4 gauss_v4(const float* s, int n) {
+#pragma clang fp contract(off)
+    const f4 sv = *reinterpret_cast<const f4*>(s + n);
+    return sv * sv + 1e-6f;
+}
+
+__device__ __forceinline__ void gauss_fwd_store(float* o, float* yo, f4 z, f4 v) {
+#pragma clang fp contract(off)
+    *reinterpret_cast<f4*>(o) = z;
+    f4 y;
+    y.x = expf((-(z.x * z.x)) * v.x);
+    y.y = expf((-(z.y * z.y)) * v.y);
+    y.z = expf((-(z.z * z.z)) * v.z);
+    y.w = expf((-(z.w * z.w)) * v.w);
+    *reinterpret_cast<f4*>(yo) = y;
+}
+
+__device__ __forceinline__ float gauss_bwd1(float g, float zz, float v, double& acc) {
+#pragma clang fp contract(off)
+    const float z2 = zz * zz;
+    const float ge = g * expf((-z2) * v);
+    acc += (double)((-ge) * z2);
+    return (((-ge) * 2.0f) * zz) * v;
+}
+
+__device__ __forceinline__ void gauss_bwd_store(float* o, f4 g, f4 z, f4 v, double (&acc)[4]) {
+    f4 dz;
+    dz.x = gauss_bwd1(g.x, z.x, v.x, acc[0]);
+    dz.y = gauss_bwd1(g.y, z.y, v.y, acc[1]);
+    dz.z = gauss_bwd1(g.z, z.z, v.z, acc[2]);
+    dz.w = gauss_bwd1(g.w, z.w, v.w, acc[3]);
+    *reinterpret_cast<f4*>(o) = dz;
+}
 
 // ------------------------------------------------------------------------- NT
 __global__ __launch_bounds__(256, 2) void linear_nt_x3_kernel(NTArgs a, int ntm, int ntiles) {
@@ -254,6 +294,8 @@ __global__ __launch_bounds__(256, 2) void linear_nt_x3_kernel(NTArgs a, int ntm,
         }
 
         float* Cs = reinterpret_cast<float*>(smem + (cur ^ 1) * BUFB);
+        const bool gmode = (a.epi & (NERF_EPI_GAUSS | NERF_EPI_GAUSS_BWD)) != 0;
+        double gp[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (wr == h) {
@@ -276,7 +318,40 @@ __global__ __launch_bounds__(256, 2) void linear_nt_x3_kernel(NTArgs a, int ntm,
                 const int row = q / Q, cq = q - (q / Q) * Q;
                 const int m = m0 + h * HR + row;
                 const int n = n0 + cq * 4;
-                epi_quad<BN / 4>(E, m < a.M && n < a.N, m, n, *reinterpret_cast<const f4*>(Cs + row * LDC + cq * 4));
+                const f4 c = *reinterpret_cast<const f4*>(Cs + row * LDC + cq * 4);
+                if (gmode) {
+                    // N % 4 == 0 and 16-byte rows (nerf_linear_gauss_x3 checks): whole quads
+                    if (m < a.M && n < a.N) {
+                        const f4 v = gauss_v4(a.gs, n);
+                        if (a.epi & NERF_EPI_GAUSS) {
+                            f4 z = c;
+                            if (a.epi & NERF_EPI_BIAS) z += *reinterpret_cast<const f4*>(a.bias + n);
+                            gauss_fwd_store(a.out + (int64_t)m * a.ldo + n, a.y2 + (int64_t)m * a.ldy2 + n, z, v);
+                        } else {
+                            gauss_bwd_store(a.out + (int64_t)m * a.ldo + n, c,
+                                            *reinterpret_cast<const f4*>(a.aux + (int64_t)m * a.ldaux + n), v, gp);
+                        }
+                    }
+                } else {
+                    epi_quad<BN / 4>(E, m < a.M && n < a.N, m, n, c);
+                }
+            }
+            __syncthreads();
+        }
+        if (a.epi & NERF_EPI_GAUSS_BWD) {
+            // the tile's column partials: thread t holds rows = t / 32 (mod 8) of column quad t % 32;
+            // the 8 row groups are added in order, one fp64 row per 128-row tile
+            static_assert(256 % (BN / 4) == 0, "fixed column quad per thread");
+            double* R = reinterpret_cast<double*>(Cs);
+            const int grp = t / (BN / 4), cq = t % (BN / 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) R[grp * BN + cq * 4 + e] = gp[e];
+            __syncthreads();
+            if (t < BN && n0 + t < a.N) {
+                double sum = 0.0;
+#pragma unroll
+                for (int g = 0; g < 256 / (BN / 4); ++g) sum += R[g * BN + t];
+                a.part[(int64_t)(m0 / BM) * a.N + n0 + t] = sum;
             }
             __syncthreads();
         }
@@ -465,6 +540,10 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
     const int en = ec4 * 4;
     f4 bias4 = f4{0.f, 0.f, 0.f, 0.f};
     if ((EPI & NERF_EPI_BIAS) && a.vec_ok && en + 4 <= a.N) bias4 = *reinterpret_cast<const f4*>(a.bias + en);
+    constexpr bool GF = (EPI & NERF_EPI_GAUSS) != 0, GB = (EPI & NERF_EPI_GAUSS_BWD) != 0;
+    f4 gv4 = f4{0.f, 0.f, 0.f, 0.f};
+    if ((GF || GB) && en + 4 <= a.N) gv4 = gauss_v4(a.gs, en);
+    double gp[4] = {0.0, 0.0, 0.0, 0.0};          // GB: this thread's column-quad partials of the tile
     const EpiOut E{a.out, a.ldo, a.bias, a.aux, a.ldaux, a.M, a.N,
                    EPI | (a.epi & (NERF_EPI_MASKBITS | NERF_EPI_MASKOUT)), a.vec_ok};
     const bool mbits = (a.epi & NERF_EPI_MASKBITS) != 0, mout = (a.epi & NERF_EPI_MASKOUT) != 0;
@@ -517,12 +596,12 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
             for (int qb = 0; qb < PR / RS; qb += UB) {
                 f4 xa[UB], xo[UB];
                 unsigned xb[UB];
-                if (vec && (EPI & (NERF_EPI_MASK | NERF_EPI_ACCUM))) {
+                if (vec && (EPI & (NERF_EPI_MASK | NERF_EPI_ACCUM | NERF_EPI_GAUSS_BWD))) {
 #pragma unroll
                     for (int u = 0; u < UB; ++u) {
                         int m = tm0 + r0 + erow + RS * (qb + u);
                         m = m < a.M ? m : a.M - 1;
-                        if (MSK && !mbits) xa[u] = *reinterpret_cast<const f4*>(a.aux + (int64_t)m * a.ldaux + en);
+                        if ((MSK && !mbits) || GB) xa[u] = *reinterpret_cast<const f4*>(a.aux + (int64_t)m * a.ldaux + en);
                         if (EPI & NERF_EPI_ACCUM) xo[u] = *reinterpret_cast<const f4*>(a.out + (int64_t)m * a.ldo + en);
                     }
                 }
@@ -543,7 +622,13 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
                     const float* Cr = row < 32 ? C0 + row * BN : C1 + (row - 32) * BN;
                     f4 v = *reinterpret_cast<const f4*>(Cr + en);
                     unsigned nib = 0;
-                    if (ok && vec) {
+                    if (ok && vec && GF) {
+                        // pre-activation to out (kept for the backward), activation to y2
+                        if (EPI & NERF_EPI_BIAS) v += bias4;
+                        gauss_fwd_store(a.out + (int64_t)m * a.ldo + en, a.y2 + (int64_t)m * a.ldy2 + en, v, gv4);
+                    } else if (ok && vec && GB) {
+                        gauss_bwd_store(a.out + (int64_t)m * a.ldo + en, v, xa[u], gv4, gp);
+                    } else if (ok && vec) {
                         float* o = a.out + (int64_t)m * a.ldo + en;
                         if (EPI & NERF_EPI_BIAS) v += bias4;
                         if (EPI & NERF_EPI_RELU) {
@@ -572,6 +657,24 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
                 // compile-time acc indices once unrolled
                 pass(32 * p, p >> 2, acc[p & 3], acc[p & 3]);
             }
+        }
+        if (GB) {
+            // the tile's inverse-std gradient column partials: the RS row groups of each column
+            // quad added in order through the free A stage, one fp64 row per 256-row tile
+            double* R = reinterpret_cast<double*>(C0);
+            static_assert(RS * BN * 8 <= ABYTES, "partials staging");
+#pragma unroll
+            for (int e = 0; e < 4; ++e) R[erow * BN + en + e] = gp[e];
+            barrier();
+            if (t < BN && t < a.N) {
+                double sum = 0.0;
+#pragma unroll
+                for (int r = 0; r < RS; ++r) sum += R[r * BN + t];
+                a.part[(int64_t)c_tile * a.N + t] = sum;
+            }
+            barrier();
+#pragma unroll
+            for (int e = 0; e < 4; ++e) gp[e] = 0.0;
         }
     };
 
@@ -1064,6 +1167,74 @@ extern "C" int nerf_linear_fwd_x3(const nerf_seg* segs, int32_t n_segs, int64_t 
     hipLaunchKernelGGL(linear_nt_x3_kernel, dim3((unsigned)grid), dim3(256), 0, st, a, ntm, ntiles);
     NERF_CHECK_LAUNCH();
     return NERF_OK;
+}
+
+extern "C" size_t nerf_linear_gauss_workspace(int64_t M, int32_t N) {
+    if (M <= 0 || N <= 0) return 0;
+    // one fp64 row per 128-row tile (the 256-row tile kernel uses half) + the reduction's chunk sums
+    return (size_t)((M + 127) / 128) * (size_t)N * sizeof(double) + nerf::gauss_reduce_scratch(N);
+}
+
+extern "C" int nerf_linear_gauss_x3(const nerf_seg* segs, int32_t n_segs, int64_t M, const void* W_x, int32_t ldw,
+                                    int32_t N, const float* bias, float* out, int64_t ldo, int32_t mode,
+                                    const float* inv_std, float* y, int64_t ld_y, const float* z, int64_t ld_z,
+                                    float* grad_inv_std, int32_t accumulate, void* workspace, size_t workspace_bytes,
+                                    void* stream) {
+    NERF_REQUIRE(M >= 0 && M < (1ll << 31) && N >= 1 && (mode == NERF_GAUSS_FWD || mode == NERF_GAUSS_BWD));
+    NERF_REQUIRE(inv_std != nullptr && out != nullptr);
+    const bool fwd = mode == NERF_GAUSS_FWD;
+    if (fwd) NERF_REQUIRE(y != nullptr && ld_y >= N);
+    else NERF_REQUIRE(bias == nullptr && z != nullptr && ld_z >= N && grad_inv_std != nullptr);
+    hipStream_t st = as_stream(stream);
+    if (M == 0) {
+        if (!fwd && !accumulate && hipMemsetAsync(grad_inv_std, 0, (size_t)N * sizeof(float), st) != hipSuccess)
+            return NERF_ERR_LAUNCH;
+        return NERF_OK;
+    }
+    // whole 16-byte quads everywhere, or the caller takes the unfused path
+    if ((N % 4) != 0 || !aligned16(out) || (ldo % 4) != 0 || ldo < N || !aligned16(inv_std) ||
+        (bias && !aligned16(bias)) || (fwd && (!aligned16(y) || (ld_y % 4) != 0)) ||
+        (!fwd && (!aligned16(z) || (ld_z % 4) != 0)))
+        return NERF_ERR_UNSUPPORTED;
+    if (!fwd && (workspace == nullptr || workspace_bytes < nerf_linear_gauss_workspace(M, N) ||
+                 (reinterpret_cast<uintptr_t>(workspace) & 7) != 0))
+        return NERF_ERR_WORKSPACE;
+    SegList L;
+    NERF_REQUIRE(build_segs(segs, n_segs, L));
+    NERF_REQUIRE(W_x && aligned16(W_x) && ldw == L.ktot && (ldw % BK) == 0);
+    const int epi = fwd ? (NERF_EPI_GAUSS | (bias ? NERF_EPI_BIAS : 0)) : NERF_EPI_GAUSS_BWD;
+    double* part = static_cast<double*>(workspace);
+    NTArgs a{L, (int)M, reinterpret_cast<const __bf16*>(W_x), ldw, N, bias, out, ldo, epi, z, ld_z, 1,
+             inv_std, y, ld_y, part};
+    int64_t slabs;
+    if (N <= 256) {
+        const int ntiles = (int)((M + 255) / 256);
+        int grid = cu_count_x3();
+        if (grid > ntiles) grid = ntiles;
+        const dim3 g3((unsigned)grid), b3(512);
+#define NERF_GLDS_LAUNCH(E)                                                                          \
+    do {                                                                                            \
+        if (N > 128) hipLaunchKernelGGL((linear_nt_x3_glds_kernel<E, 2>), g3, b3, 0, st, a, ntiles); \
+        else hipLaunchKernelGGL((linear_nt_x3_glds_kernel<E, 1>), g3, b3, 0, st, a, ntiles);         \
+    } while (0)
+        if (epi == (NERF_EPI_GAUSS | NERF_EPI_BIAS)) NERF_GLDS_LAUNCH(NERF_EPI_GAUSS | NERF_EPI_BIAS);
+        else if (epi == NERF_EPI_GAUSS) NERF_GLDS_LAUNCH(NERF_EPI_GAUSS);
+        else NERF_GLDS_LAUNCH(NERF_EPI_GAUSS_BWD);
+#undef NERF_GLDS_LAUNCH
+        slabs = ntiles;
+    } else {
+        const int ntm = (int)((M + 127) / 128);
+        const int ntn = (N + 127) / 128;
+        const int ntiles = (ntm + 7) / 8 * 8 * ntn;
+        int grid = ntiles;
+        const int cap = 2 * cu_count_x3();
+        if (grid > cap) grid = cap;
+        hipLaunchKernelGGL(linear_nt_x3_kernel, dim3((unsigned)grid), dim3(256), 0, st, a, ntm, ntiles);
+        slabs = ntm;
+    }
+    NERF_CHECK_LAUNCH();
+    if (fwd) return NERF_OK;
+    return nerf::gauss_reduce(part, slabs, N, inv_std, grad_inv_std, accumulate, part + slabs * N, st);
 }
 
 extern "C" int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N, const nerf_seg* segs, int32_t n_segs,

@@ -32,6 +32,9 @@ NERF_EPI_MASKBITS = 16
 NERF_EPI_MASKOUT = 32
 NERF_EPI_NO_PERSIST = 256
 NERF_EPI_NARROW_TILE = 512
+NERF_ERR_UNSUPPORTED = -2
+NERF_GAUSS_FWD = 0
+NERF_GAUSS_BWD = 1
 
 
 class NerfSeg(ctypes.Structure):
@@ -155,6 +158,9 @@ _SIGNATURES = {
     "nerf_pack_weight": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
     "nerf_linear_fwd_x3": (c_i32, [ctypes.POINTER(NerfSeg), c_i32, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp,
                                    c_i64, c_i32, c_vp, c_i64, c_vp]),
+    "nerf_linear_gauss_workspace": (c_sz, [c_i64, c_i32]),
+    "nerf_linear_gauss_x3": (c_i32, [ctypes.POINTER(NerfSeg), c_i32, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp, c_i64,
+                                     c_i32, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_sz, c_vp]),
     "nerf_linear_wgrad_x3": (c_i32, [c_vp, c_i64, c_i32, ctypes.POINTER(NerfSeg), c_i32, c_i64, c_vp, c_sz, c_vp]),
     "nerf_pack_weight_x3": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
     "nerf_mlp_fused_fwd": (c_i32, [ctypes.POINTER(NerfFusedLayer), c_i32, c_vp, c_i64, c_vp]),
@@ -186,7 +192,7 @@ def load(path: str | None = None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.nerf_abi_version() != 2:
+    if lib.nerf_abi_version() != 3:
         raise RuntimeError("nerf_amd: ABI version mismatch between Python binding and libnerf_amd.so")
     if path is None:
         _lib = lib

@@ -315,8 +315,12 @@ def adam_step(entries, beta1: float, beta2: float, eps: float, device) -> None:
 # ----------------------------------------------------------------------------- gaussian activation
 def gauss_act_fwd(z: torch.Tensor, N: int, inv_std: torch.Tensor, y: torch.Tensor) -> None:
     _require_cuda_f32("inv_standard_deviation", inv_std)
+    end = TIMER.bracket("gauss_act_fwd", 0.0, 8.0 * z.shape[0] * N, fn="gauss_fwd_kernel") \
+        if TIMER is not None else None
     st = _lib.load().nerf_gauss_act_fwd(_ptr(z), z.stride(0), _ptr(inv_std), z.shape[0], N, _ptr(y), y.stride(0),
                                         _stream(z.device))
+    if end is not None:
+        end.record()
     _lib.check(st, "nerf_gauss_act_fwd")
 
 
@@ -326,9 +330,12 @@ def gauss_act_bwd(grad_y: torch.Tensor, z: torch.Tensor, N: int, inv_std: torch.
     lib = _lib.load()
     ws = torch.empty(max(1, (int(lib.nerf_gauss_act_workspace(M, N)) + 7) // 8), device=z.device,
                      dtype=torch.float64)
+    end = TIMER.bracket("gauss_act_bwd", 0.0, 12.0 * M * N, fn="gauss_bwd_kernel") if TIMER is not None else None
     st = lib.nerf_gauss_act_bwd(_ptr(grad_y), grad_y.stride(0), _ptr(z), z.stride(0), _ptr(inv_std), M, N,
                                 _ptr(grad_z), grad_z.stride(0), _ptr(grad_inv_std), 0, _ptr(ws),
                                 ws.numel() * 8, _stream(z.device))
+    if end is not None:
+        end.record()
     _lib.check(st, "nerf_gauss_act_bwd")
 
 
@@ -408,6 +415,40 @@ def linear_fwd_x3(segs, M: int, Wx: torch.Tensor, ldw: int, N: int, bias: torch.
     if end is not None:
         end.record()
     _lib.check(st, "nerf_linear_fwd_x3")
+
+
+def linear_gauss_x3(segs, M: int, Wx: torch.Tensor, ldw: int, N: int, out: torch.Tensor, inv_std: torch.Tensor, *,
+                    bias: torch.Tensor | None = None, y: torch.Tensor | None = None, z: torch.Tensor | None = None,
+                    grad_inv_std: torch.Tensor | None = None, w_row_offset: int = 0) -> bool:
+    """Split-precision linear layer with the Gaussian activation fused into its epilogue
+    (nerf_linear_gauss_x3).  Forward (y given): out = z = x W^T + b, y = exp(-z^2 (s^2 + 1e-6)).
+    Input gradient (z, grad_inv_std given): out = dL/dz of the layer whose pre-activation is z,
+    from the product (= dL/dy), and grad_inv_std = its inverse-std gradient.  Returns False when the
+    shapes need the unfused path (N % 4, alignment)."""
+    _require_cuda_f32("inv_standard_deviation", inv_std)
+    arr = make_segs(segs)
+    off = w_row_offset * ldw * 2 * 2
+    fwd = y is not None
+    lib = _lib.load()
+    ws = None
+    if not fwd:
+        ws = torch.empty(max(1, (int(lib.nerf_linear_gauss_workspace(M, N)) + 7) // 8), device=out.device,
+                         dtype=torch.float64)
+    nbytes = _segs_bytes(segs, M) + 4.0 * N * ldw + (8.0 * M * N if fwd else 12.0 * M * N)
+    end = TIMER.bracket("linear_gauss_x3" if fwd else "linear_gauss_bwd_x3", 2.0 * M * N * ldw, nbytes,
+                        fn="linear_nt_x3_glds_kernel" if N <= 256 else "linear_nt_x3_kernel") \
+        if TIMER is not None else None
+    st = lib.nerf_linear_gauss_x3(arr, len(segs), M, Wx.data_ptr() + off, ldw, N, _ptr(bias), _ptr(out),
+                                  out.stride(0), _lib.NERF_GAUSS_FWD if fwd else _lib.NERF_GAUSS_BWD,
+                                  _ptr(inv_std), _ptr(y), y.stride(0) if fwd else 0, _ptr(z),
+                                  z.stride(0) if z is not None else 0, _ptr(grad_inv_std), 0, _ptr(ws),
+                                  ws.numel() * 8 if ws is not None else 0, _stream(out.device))
+    if end is not None:
+        end.record()
+    if st == _lib.NERF_ERR_UNSUPPORTED:
+        return False
+    _lib.check(st, "nerf_linear_gauss_x3")
+    return True
 
 
 def linear_wgrad_x3(dY: torch.Tensor, N4: int, segs, M: int, workspace: torch.Tensor) -> None:

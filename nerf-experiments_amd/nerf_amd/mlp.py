@@ -45,6 +45,10 @@ def matmul_precision() -> str:
 
 PRECISION_OVERRIDE: str | None = None
 
+# Gaussian activation fused into the split-precision GEMM epilogues (nerf_linear_gauss_x3); False
+# runs the separate nerf_gauss_act_fwd / _bwd passes (tests compare the two)
+GAUSS_EPILOGUE = True
+
 # test hook: when a list, every MLPFunction.forward appends (layer outputs, ReLU mask bits)
 CAPTURE: list | None = None
 
@@ -164,12 +168,22 @@ class MLPPlan:
         self.fused_dgrad = {}      # device -> mlp_fused.FusedInputGrad
         self.infer = False         # set per call by MLPFunction.apply: no autograd graph is recorded
         self.consumed = [False] * len(layers)
+        # terms of each layer's output gradient (consumer GEMMs, residual adds, autograd outputs):
+        # a Gaussian layer with exactly one consumer GEMM gets its activation backward in that
+        # GEMM's epilogue
+        self.contributors = [0] * len(layers)
         for lp in layers:
             for s in lp.sources:
                 if s.kind == "act":
                     self.consumed[s.layer] = True
+                    self.contributors[s.layer] += 1
             if lp.residual >= 0:
                 self.consumed[lp.residual] = True
+                self.contributors[lp.residual] += 1
+        for i in outputs:
+            self.contributors[i] += 1
+        for li, _ in self.column_outputs:
+            self.contributors[li] += 1
 
     def to_device(self, device):
         if self.device != device:
@@ -241,9 +255,17 @@ class MLPFunction(torch.autograd.Function):
                     t, rd = _src_tensor(s, pos, dirs, acts, dir_rd)
                     segs.append((t, s.k_seg, rd))
                 out = torch.empty(M, lp.out_ld, device=pos.device, dtype=torch.float32)
-                # Gaussian layers: the GEMM writes the pre-activation z (kept for the backward),
-                # nerf_gauss_act_fwd then writes exp(-z^2 v) into the layer's output
+                # Gaussian layers: the GEMM writes the pre-activation z (kept for the backward) and,
+                # in split precision, exp(-z^2 v) into the layer's output from the same epilogue;
+                # otherwise nerf_gauss_act_fwd applies the activation in a second pass
                 target = torch.empty_like(out) if lp.gauss is not None else out
+                if (GAUSS_EPILOGUE and lp.gauss is not None and prec == "x3" and lp.N > 32 and lp.residual < 0
+                        and not lp.relu and K.linear_gauss_x3(segs, M, lp.Wpx, lp.Kp, lp.N, target, lp.gauss, bias=lp.module.bias,
+                                              y=out)):
+                    pre.append(target)
+                    acts.append(out)
+                    masks.append(None)
+                    continue
                 epi = NERF_EPI_BIAS | (NERF_EPI_RELU if lp.relu else 0)
                 mask = None
                 if lp.relu and plan.consumed[idx] and lp.N <= 256:
@@ -314,6 +336,7 @@ class MLPFunction(torch.autograd.Function):
         dpos = None
         ddir = None
         layer_grads: list[list[torch.Tensor]] = [[] for _ in range(L)]
+        gauss_done: list[torch.Tensor | None] = [None] * L   # inverse-std gradients formed in an epilogue
 
         # the input-gradient chain in one launch (csrc/mlp_fused.hip): every dY[l], l < L-1, from
         # the head gradient through the stored ReLU bits, when nothing else feeds the backward
@@ -377,7 +400,9 @@ class MLPFunction(torch.autograd.Function):
                     layer_grads[li].append(torch.zeros_like(lp.gauss))
                 continue
             gs = None
-            if lp.gauss is not None:
+            if gauss_done[li] is not None:
+                gs = gauss_done[li]          # dY[li] already is dL/dz (the consumer's epilogue)
+            elif lp.gauss is not None:
                 # dY -> dZ through the Gaussian activation (+ the inverse-std gradient)
                 gs = torch.empty_like(lp.gauss)
                 dz = dZ if owned[li] else torch.empty_like(dZ)
@@ -411,6 +436,16 @@ class MLPFunction(torch.autograd.Function):
                 if s.kind == "act":
                     j = s.layer
                     prod = plan.layers[j]
+                    if (GAUSS_EPILOGUE and prod.gauss is not None and plan.contributors[j] == 1 and dY[j] is None
+                            and not prod.relu and ctx.prec == "x3" and s.k_valid > 32):
+                        # sole consumer: dL/dz of the Gaussian layer straight from this GEMM's epilogue
+                        dz = torch.empty(M, prod.out_ld, device=dev, dtype=torch.float32)
+                        gsj = torch.empty_like(prod.gauss)
+                        if K.linear_gauss_x3(a_seg, M, lp.Wtx, lp.ldwt, s.k_valid, dz, prod.gauss, z=pre[j],
+                                             grad_inv_std=gsj, w_row_offset=koff):
+                            dY[j] = dz
+                            gauss_done[j] = gsj
+                            continue
                     epi = 0
                     aux = None
                     if prod.relu:

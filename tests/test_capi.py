@@ -44,7 +44,7 @@ def test_exported_dynamic_symbols_with_nm():
 def test_abi_version_and_status_strings():
     from nerf_amd import _lib
     lib = _lib.load()
-    assert lib.nerf_abi_version() == 2
+    assert lib.nerf_abi_version() == 3
     assert lib.nerf_status_string(0) == b"ok"
     assert b"invalid" in lib.nerf_status_string(-1)
     assert b"workspace" in lib.nerf_status_string(-4)
@@ -82,6 +82,17 @@ def test_argument_validation_returns_status_without_launch():
     assert lib.nerf_gauss_act_fwd(None, 16, None, 0, 16, None, 16, None) == 0
     assert lib.nerf_gauss_act_workspace(1000, 64) >= 64 * 8
     assert lib.nerf_gauss_act_bwd(16, 16, 16, 16, 16, 10, 16, 16, 16, 16, 0, None, 0, None) == -4
+    # linear + Gaussian epilogue: bad mode, empty batch, N not a multiple of 4 (-> unfused path),
+    # backward without workspace
+    assert lib.nerf_linear_gauss_x3(None, 0, 10, 256, 32, 8, None, 256, 8, 2, 256, 256, 8, None, 0, None, 0,
+                                    None, 0, None) == -1
+    assert lib.nerf_linear_gauss_x3(None, 0, 0, 256, 32, 8, None, 256, 8, 0, 256, 256, 8, None, 0, None, 0,
+                                    None, 0, None) == 0
+    assert lib.nerf_linear_gauss_x3(None, 0, 10, 256, 32, 6, None, 256, 8, 0, 256, 256, 8, None, 0, None, 0,
+                                    None, 0, None) == -2
+    assert lib.nerf_linear_gauss_x3(None, 0, 10, 256, 32, 8, None, 256, 8, 1, 256, None, 0, 256, 8, 256, 0,
+                                    None, 0, None) == -4
+    assert lib.nerf_linear_gauss_workspace(1000, 64) >= 8 * 64 * 8
     # ray-mode encoding backward: missing rays / outputs
     p.kind = 0
     assert lib.nerf_encode_bwd_rays(ctypes.byref(p), None, 16, 16, 16, None, 16, 64, 4, 8, 16, 16, 0, None) == -1
