@@ -212,6 +212,9 @@ typedef struct nerf_seg {
                                 multiple of 16); bit b of word 2e+h <-> column 4(32h+b)+e */
 #define NERF_EPI_NO_PERSIST 256  /* tuning: one tile per workgroup instead of a persistent grid */
 #define NERF_EPI_NARROW_TILE 512 /* tuning: force the 128-column tile of the split-precision kernel for N > 128 */
+#define NERF_EPI_TANH      4096  /* tanh(.) after the bias (2d-reconstruction/model.py:48-56) */
+#define NERF_EPI_TANH_BWD  8192  /* * (1 - y*y), y = aux[m, n] (fp32, row stride ld_aux): tanh backward;
+                                    not with MASK (both read aux) */
 #define NERF_EPI_GAUSS     1024  /* internal (nerf_linear_gauss_x3): Gaussian activation forward */
 #define NERF_EPI_GAUSS_BWD 2048  /* internal (nerf_linear_gauss_x3): Gaussian activation backward */
 

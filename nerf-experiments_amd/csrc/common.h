@@ -218,6 +218,13 @@ struct EpiOut {
     int M; int N; int epi; int vec_ok;
 };
 
+// torch's tanh_backward: g * (1 - y * y), no contraction
+__device__ __forceinline__ float tanh_bwd(float g, float y) {
+#pragma clang fp contract(off)
+    const float yy = y * y;
+    return g * (1.0f - yy);
+}
+
 // Epilogue of one lane's quad (ok: the quad is in range); returns its (out > 0) bits.
 __device__ __forceinline__ unsigned epi_quad_lane(const EpiOut& E, int m, int n, epi_f4 v) {
     const bool bits = (E.epi & (NERF_EPI_MASKBITS | NERF_EPI_MASKOUT)) != 0;
@@ -227,6 +234,13 @@ __device__ __forceinline__ unsigned epi_quad_lane(const EpiOut& E, int m, int n,
         if (E.epi & NERF_EPI_BIAS) v += *reinterpret_cast<const epi_f4*>(E.bias + n);
         if (E.epi & NERF_EPI_RELU) {
             v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        }
+        if (E.epi & NERF_EPI_TANH) {
+            v.x = tanhf(v.x); v.y = tanhf(v.y); v.z = tanhf(v.z); v.w = tanhf(v.w);
+        }
+        if (E.epi & NERF_EPI_TANH_BWD) {
+            const epi_f4 y = *reinterpret_cast<const epi_f4*>((const float*)E.aux + (int64_t)m * E.ldaux + n);
+            v.x = tanh_bwd(v.x, y.x); v.y = tanh_bwd(v.y, y.y); v.z = tanh_bwd(v.z, y.z); v.w = tanh_bwd(v.w, y.w);
         }
         if (E.epi & NERF_EPI_MASK)
             v = bits ? apply_bits(v, load_quad_bits(mrow, n >> 2))
@@ -243,6 +257,8 @@ __device__ __forceinline__ unsigned epi_quad_lane(const EpiOut& E, int m, int n,
         float x = e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
         if (E.epi & NERF_EPI_BIAS) x = x + E.bias[n + e];
         if (E.epi & NERF_EPI_RELU) x = fmaxf(x, 0.f);
+        if (E.epi & NERF_EPI_TANH) x = tanhf(x);
+        if (E.epi & NERF_EPI_TANH_BWD) x = tanh_bwd(x, ((const float*)E.aux)[(int64_t)m * E.ldaux + n + e]);
         if (E.epi & NERF_EPI_MASK)
             x = (bits ? ((mb >> e) & 1u) != 0u : ((const float*)E.aux)[(int64_t)m * E.ldaux + n + e] > 0.f) ? x : 0.f;
         if (E.epi & NERF_EPI_ACCUM) x = o[e] + x;

@@ -559,8 +559,11 @@ extern "C" int nerf_linear_fwd(const nerf_seg* segs, int32_t n_segs, int64_t M, 
     if (mbits) NERF_REQUIRE(aux != nullptr && N <= 256 && ld_aux >= 32 && (ld_aux % 16) == 0 && aligned16(aux));
     if (epilogue & NERF_EPI_MASK) NERF_REQUIRE(aux != nullptr && (mbits || ld_aux >= N));
     if (epilogue & NERF_EPI_MASKOUT) NERF_REQUIRE(!(epilogue & NERF_EPI_MASK));
+    if (epilogue & NERF_EPI_TANH_BWD) NERF_REQUIRE(aux != nullptr && ld_aux >= N && !(epilogue & (NERF_EPI_MASK | NERF_EPI_MASKBITS | NERF_EPI_MASKOUT)));
+    NERF_REQUIRE(!(epilogue & (NERF_EPI_GAUSS | NERF_EPI_GAUSS_BWD)));     // nerf_linear_gauss_x3 only
     const int vec_ok = aligned16(out) && (ldo % 4) == 0 && (!(epilogue & NERF_EPI_BIAS) || aligned16(bias)) &&
-                       (!(epilogue & NERF_EPI_MASK) || mbits || (aligned16(aux) && (ld_aux % 4) == 0));
+                       (!(epilogue & NERF_EPI_MASK) || mbits || (aligned16(aux) && (ld_aux % 4) == 0)) &&
+                       (!(epilogue & NERF_EPI_TANH_BWD) || (aligned16(aux) && (ld_aux % 4) == 0));
     NTArgs a{L, (int)M, W, ldw, N, bias, out, ldo, epilogue, aux, ld_aux, vec_ok};
     const int ntm = (int)((M + 127) / 128);
     const int ntn = N <= 32 ? 1 : (N + 127) / 128;

@@ -8,6 +8,7 @@ from .model_interpolation_architecture import NerfBaseModel, NerfModel  # noqa: 
 from .model_interpolation import MAGIC_NUMBER, NerfInterpolation, SchedulerLeNice  # noqa: F401
 from .model_garf import GaussAct, ProposalNetwork, RadianceNetwork  # noqa: F401
 from .model_ingp import INGPEncoding, INGPTable, NerfModelINGP  # noqa: F401
+from .model_2d import FourierFeatures2d, Nerf2d  # noqa: F401
 from .optim import FusedAdam  # noqa: F401
 
 __version__ = "0.1.0"

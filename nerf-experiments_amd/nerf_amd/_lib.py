@@ -32,6 +32,8 @@ NERF_EPI_MASKBITS = 16
 NERF_EPI_MASKOUT = 32
 NERF_EPI_NO_PERSIST = 256
 NERF_EPI_NARROW_TILE = 512
+NERF_EPI_TANH = 4096
+NERF_EPI_TANH_BWD = 8192
 NERF_ERR_UNSUPPORTED = -2
 NERF_GAUSS_FWD = 0
 NERF_GAUSS_BWD = 1

@@ -28,7 +28,7 @@ import torch.nn as nn
 from . import kernels as K
 from . import mlp_fused
 from ._lib import (NERF_EPI_ACCUM, NERF_EPI_BIAS, NERF_EPI_MASK, NERF_EPI_MASKBITS, NERF_EPI_MASKOUT,
-                   NERF_EPI_RELU)
+                   NERF_EPI_RELU, NERF_EPI_TANH, NERF_EPI_TANH_BWD)
 
 
 def matmul_precision() -> str:
@@ -59,6 +59,14 @@ class Source:
     k_valid: int       # columns of the source consumed (reference layout width)
     k_pad: int         # columns the source occupies in the packed weight layout (multiple of 32)
     layer: int = -1    # producing layer for "act"
+    # optional: Linear input column of each buffer column (-1 = unused, zero weight); len = k_valid.
+    # Default: buffer column j feeds input column j.  (Nerf2d's [cos xy | cos 0 | sin xy | sin 0]
+    # encoding of 2-D points padded to 3-D feeds its 40 inputs from one buffer.)
+    cols: list[int] | None = None
+
+    @property
+    def n_inputs(self) -> int:
+        return self.k_valid if self.cols is None else sum(1 for c in self.cols if c >= 0)
 
     @property
     def k_seg(self) -> int:
@@ -84,6 +92,7 @@ class LayerPlan:
     gauss: nn.Parameter | None = None
     residual: int = -1
     residual_cols: int = 0
+    tanh: bool = False     # tanh in the epilogue (2d-reconstruction/model.py:48-56); backward reads the output
     N: int = 0
     out_ld: int = 0
     Kp: int = 0
@@ -108,8 +117,11 @@ class LayerPlan:
         for s in self.sources:
             self.koffs.append(kp)
             for j in range(s.k_pad):
-                cm.append(orig + j if j < s.k_valid else -1)
-            orig += s.k_valid
+                if s.cols is None:
+                    cm.append(orig + j if j < s.k_valid else -1)
+                else:
+                    cm.append(orig + s.cols[j] if j < len(s.cols) and s.cols[j] >= 0 else -1)
+            orig += s.n_inputs
             kp += s.k_pad
         if orig != self.module.in_features:
             raise ValueError(f"layer input width mismatch: sources give {orig}, Linear expects "
@@ -266,7 +278,7 @@ class MLPFunction(torch.autograd.Function):
                     acts.append(out)
                     masks.append(None)
                     continue
-                epi = NERF_EPI_BIAS | (NERF_EPI_RELU if lp.relu else 0)
+                epi = NERF_EPI_BIAS | (NERF_EPI_RELU if lp.relu else 0) | (NERF_EPI_TANH if lp.tanh else 0)
                 mask = None
                 if lp.relu and plan.consumed[idx] and lp.N <= 256:
                     # the ReLU-backward mask of this output as bits (32 bytes a row): the input-
@@ -448,6 +460,9 @@ class MLPFunction(torch.autograd.Function):
                             continue
                     epi = 0
                     aux = None
+                    if prod.tanh:
+                        epi |= NERF_EPI_TANH_BWD       # * (1 - y^2) from the stored activation
+                        aux = acts[j]
                     if prod.relu:
                         if ctx.masks[j] is not None:
                             epi |= NERF_EPI_MASK | NERF_EPI_MASKBITS

@@ -48,7 +48,7 @@ ENABLED = os.environ.get("NERF_FUSED", "1") != "0"     # A/B switch (bench, test
 def _layer_shape(plan, idx):
     """(kbr, hbm sources, act source) of layer idx, or None if the kernel cannot run it."""
     lp = plan.layers[idx]
-    if lp.gauss is not None or lp.residual >= 0:
+    if lp.gauss is not None or lp.tanh or lp.residual >= 0:
         return None
     acts = [s for s in lp.sources if s.kind == "act"]
     hbm = [s for s in lp.sources if s.kind != "act"]

@@ -23,6 +23,7 @@ Fixtures:
                  parameters' gradients through the whole rendering path (BarfModel's training input)
   mipnerf.npz    mip_NeRF API: IntegratedFourierFeatures (both variance modes), MipNerfModel forward /
                  gradients, MipNerf coarse+fine forward with injected coarse t
+  nerf2d.npz     2d-reconstruction Nerf2d (C1): init, Fourier features, forward, loss, gradients, 3 Adam steps
   feed.npz       ImagePoseDataset rays + __getitem__ (DataLoader collation) + get_blurred_pixel_colors
                  on a small in-memory image set; the notebook's 4x2 meshgrid known answer
 
@@ -509,7 +510,38 @@ def gen_feed():
     np.savez_compressed(os.path.join(OUT, "feed.npz"), **out)
 
 
-GENERATORS = {"pe": gen_pe, "composite": gen_composite, "resample": gen_resample, "model": gen_model,
+def gen_nerf2d():
+    """2d-reconstruction (C1): Nerf2d with the reference's default init under th.manual_seed(0),
+    fourier_levels 10 (main.py:43-51) — forward on pixel-centre-style points in [0, 1)^2, the MSE
+    training-step loss, every parameter gradient, and the parameters after three Adam steps
+    (lr 1e-3) on the same batch."""
+    (m2d,) = _import_from("2d-reconstruction", ["model"])
+    g = th.Generator().manual_seed(21)
+    th.manual_seed(0)
+    model = m2d.Nerf2d(width=64, height=48, fourier_levels=10)
+    out = {f"init_sum.{k}": np.array([v.double().sum().item(), v.double().abs().sum().item()])
+           for k, v in model.state_dict().items()}
+    x = th.rand(300, 2, generator=g)
+    y = th.rand(300, 3, generator=g)
+    y_hat = model(x)
+    loss = th.nn.functional.mse_loss(y_hat, y)
+    loss.backward()
+    out.update({"x": f32(x), "y": f32(y), "y_hat": f32(y_hat), "loss": np.array([loss.item()], np.float32),
+                "pe": f32(model.model[0](x))})
+    out.update({f"grad.{k}": f32(p.grad) for k, p in model.named_parameters()})
+    opt = th.optim.Adam(model.parameters(), lr=1e-3)
+    for _ in range(3):
+        opt.zero_grad()
+        th.nn.functional.mse_loss(model(x), y).backward()
+        opt.step()
+    out.update({f"adam3_sum.{k}": np.array([v.double().sum().item(), v.double().abs().sum().item()])
+                for k, v in model.state_dict().items()})
+    out.update({f"adam3_head.{k}": f32(v.reshape(-1)[:256]) for k, v in model.state_dict().items()})
+    sys.modules.pop("model", None)
+    np.savez_compressed(os.path.join(OUT, "nerf2d.npz"), **out)
+
+
+GENERATORS = {"nerf2d": gen_nerf2d, "pe": gen_pe, "composite": gen_composite, "resample": gen_resample, "model": gen_model,
               "color": gen_color, "cos_kat": gen_cos_kat, "ipe_grad": gen_ipe_grad, "garf": gen_garf,
               "pose": gen_pose, "pose_render": gen_pose_render, "mipnerf": gen_mipnerf, "feed": gen_feed}
 

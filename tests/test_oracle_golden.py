@@ -222,3 +222,37 @@ def test_mipnerf_model_init_matches_reference(golden):
     assert keys[0].startswith("model_fine.") and any(k.startswith("model_coarse.") for k in keys)
     assert not any(k.startswith(("model_radiance.", "model_proposal.")) for k in keys)
     assert ren.model_radiance is ren.model_fine and ren.model_proposal is ren.model_coarse
+
+
+def test_nerf2d_oracle_vs_reference(golden):
+    """C1 (2d-reconstruction): the oracle's Nerf2d forward, loss and gradients against the
+    reference run (tests/golden/nerf2d.npz, make_golden.py gen_nerf2d); the reference's init under
+    th.manual_seed(0) is reproduced by nerf_amd.Nerf2d's constructor (state_dict checksums)."""
+    import math
+    import sys
+    sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[1] / "nerf-experiments_amd"))
+    from nerf_amd import Nerf2d
+    g = golden("nerf2d")
+    torch.manual_seed(0)
+    m = Nerf2d(64, 48, 10)
+    for k, v in m.state_dict().items():
+        ref = g[f"init_sum.{k}"]
+        assert abs(v.double().sum().item() - ref[0]) <= 1e-9 * max(1.0, ref[1]), k
+        assert abs(v.double().abs().sum().item() - ref[1]) <= 1e-9 * max(1.0, ref[1]), k
+    sd = {k: v.clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    x, y = t(g["x"]), t(g["y"])
+    np.testing.assert_allclose(O.fourier_features(x, 10, math.pi).numpy(), g["pe"], atol=1e-6)
+    y_hat = O.nerf2d_forward(sd, x, 10)
+    np.testing.assert_allclose(y_hat.detach().numpy(), g["y_hat"], atol=1e-6)
+    loss = torch.nn.functional.mse_loss(y_hat, y)
+    np.testing.assert_allclose(loss.item(), g["loss"][0], rtol=1e-6)
+    loss.backward()
+    for k, v in sd.items():
+        np.testing.assert_allclose(v.grad.numpy(), g[f"grad.{k}"], atol=1e-7, rtol=1e-5, err_msg=k)
+    opt = torch.optim.Adam(list(sd.values()), lr=1e-3)
+    for _ in range(3):
+        opt.zero_grad()
+        torch.nn.functional.mse_loss(O.nerf2d_forward(sd, x, 10), y).backward()
+        opt.step()
+    for k, v in sd.items():
+        np.testing.assert_allclose(v.detach().reshape(-1)[:256].numpy(), g[f"adam3_head.{k}"], atol=1e-6, err_msg=k)
