@@ -459,6 +459,21 @@ int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float* x, const 
                       int32_t samples_per_ray, const float* grad_out, int64_t g_ld, float* grad_table,
                       int32_t accumulate, void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Camera-pose alignment: CameraCalibrationModel.kabsch_algorithm
+ * (barf/model_camera_calibration.py:69-156) and compute_pose_error (:340-345).
+ * from, to: [n][3] fp32 device points, 3 <= n <= NERF_KABSCH_MAX_POINTS.  Writes R [3][3]
+ * (row-major), t [3], c [1] with R from_i c + t ~ to_i: centred clouds, c = |to_c| / |from_c|,
+ * R from the SVD of from_c^T to_c with the reflection fix on the smallest singular value,
+ * t = mean_to - c R mean_from.  remove_outliers: keep the points whose aligned distance is below
+ * the 0.9 quantile (torch.quantile's linear interpolation) and solve again.  err (optional):
+ * mean_i |to_i - (R from_i c + t)| over all n points — compute_pose_error with from = predicted
+ * and to = raw camera origins.  One workgroup, fp64 fixed-order sums (deterministic).
+ * ------------------------------------------------------------------------- */
+#define NERF_KABSCH_MAX_POINTS 4096
+int nerf_kabsch(const float* from, const float* to, int32_t n, int32_t remove_outliers, float* R, float* t,
+                float* c, float* err, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

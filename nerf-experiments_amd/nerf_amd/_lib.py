@@ -35,6 +35,7 @@ NERF_EPI_NARROW_TILE = 512
 NERF_EPI_TANH = 4096
 NERF_EPI_TANH_BWD = 8192
 NERF_ERR_UNSUPPORTED = -2
+NERF_KABSCH_MAX_POINTS = 4096
 NERF_GAUSS_FWD = 0
 NERF_GAUSS_BWD = 1
 
@@ -169,6 +170,7 @@ _SIGNATURES = {
     "nerf_fused_pack": (c_i32, [ctypes.POINTER(c_vp), c_i32, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "nerf_hashgrid_fwd": (c_i32, [ctypes.POINTER(NerfHashgridParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
                                   c_vp, c_vp, c_i64, c_vp]),
+    "nerf_kabsch": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "nerf_hashgrid_workspace": (c_sz, [ctypes.POINTER(NerfHashgridParams)]),
     "nerf_hashgrid_bwd": (c_i32, [ctypes.POINTER(NerfHashgridParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
                                   c_vp, c_i64, c_vp, c_i32, c_vp, c_sz, c_vp]),

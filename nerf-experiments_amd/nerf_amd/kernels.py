@@ -549,3 +549,21 @@ def hashgrid_bwd(params, grad_out: torch.Tensor, grad_table: torch.Tensor, works
     if end is not None:
         end.record()
     _lib.check(st, "nerf_hashgrid_bwd")
+
+
+# ----------------------------------------------------------------------------- pose alignment
+def kabsch(p_from: torch.Tensor, p_to: torch.Tensor, remove_outliers: bool = True, error: bool = False):
+    """nerf_kabsch: (R [3, 3], t [1, 3], c [] (, mean aligned distance [])) on the device."""
+    for name, x in (("point_cloud_from", p_from), ("point_cloud_to", p_to)):
+        _require_cuda_f32(name, x)
+    p_from, p_to = p_from.contiguous(), p_to.contiguous()
+    n = p_from.shape[0]
+    if not 3 <= n <= _lib.NERF_KABSCH_MAX_POINTS:
+        raise ValueError(f"kabsch needs 3 .. {_lib.NERF_KABSCH_MAX_POINTS} points (got {n})")
+    out = torch.empty(14, device=p_from.device, dtype=torch.float32)
+    st = _lib.load().nerf_kabsch(p_from.data_ptr(), p_to.data_ptr(), n, int(remove_outliers), out.data_ptr(),
+                                 out.data_ptr() + 36, out.data_ptr() + 48, out.data_ptr() + 52 if error else None,
+                                 _stream(p_from.device))
+    _lib.check(st, "nerf_kabsch")
+    R, t, c = out[:9].view(3, 3), out[9:12].view(1, 3), out[12]
+    return (R, t, c, out[13]) if error else (R, t, c)

@@ -24,6 +24,7 @@ Fixtures:
   mipnerf.npz    mip_NeRF API: IntegratedFourierFeatures (both variance modes), MipNerfModel forward /
                  gradients, MipNerf coarse+fine forward with injected coarse t
   nerf2d.npz     2d-reconstruction Nerf2d (C1): init, Fourier features, forward, loss, gradients, 3 Adam steps
+  kabsch.npz     CameraCalibrationModel.kabsch_algorithm (outlier removal on / off) and compute_pose_error
   feed.npz       ImagePoseDataset rays + __getitem__ (DataLoader collation) + get_blurred_pixel_colors
                  on a small in-memory image set; the notebook's 4x2 meshgrid known answer
 
@@ -541,7 +542,45 @@ def gen_nerf2d():
     np.savez_compressed(os.path.join(OUT, "nerf2d.npz"), **out)
 
 
-GENERATORS = {"nerf2d": gen_nerf2d, "pe": gen_pe, "composite": gen_composite, "resample": gen_resample, "model": gen_model,
+def gen_kabsch():
+    """Kabsch alignment with outlier removal and the pose error of BARF's calibration model
+    (barf/model_camera_calibration.py:69-156, 340-345), run by the reference on synthetic camera
+    origins: a similarity transform of points on a sphere plus noise, a few gross outliers, a
+    reflected cloud, and the no-outlier-removal branch."""
+    (cc,) = _import_from("barf", ["model_camera_calibration"])
+    M = cc.CameraCalibrationModel
+    obj = M.__new__(M)
+    g = th.Generator().manual_seed(31)
+    out = {}
+
+    def rot(v):
+        return th.matrix_exp(th.cross(-th.eye(3).view(1, 3, 3), v.view(-1, 3, 1), dim=1))[0]
+
+    cases = {"noisy": (100, 0.01, 0, False), "outliers": (100, 0.005, 6, False), "reflect": (60, 0.01, 0, True),
+             "small": (12, 0.02, 1, False)}
+    for name, (n, noise, n_out, reflect) in cases.items():
+        raw = th.nn.functional.normalize(th.randn(n, 3, generator=g), dim=1) * 4.03
+        R0 = rot(th.randn(3, generator=g))
+        c0 = 0.5 + th.rand(1, generator=g).item()
+        t0 = th.randn(1, 3, generator=g)
+        src = raw * th.tensor([1.0, 1.0, -1.0]) if reflect else raw
+        pred = (R0 @ src.T).T * c0 + t0 + noise * th.randn(n, 3, generator=g)
+        if n_out:
+            pred[:n_out] += 3.0 * th.randn(n_out, 3, generator=g)
+        out[f"{name}.raw"], out[f"{name}.pred"] = f32(raw), f32(pred)
+        for ro in (True, False):
+            R, t, c = obj.kabsch_algorithm(raw, pred, remove_outliers=ro)
+            out[f"{name}.ro{int(ro)}.R"], out[f"{name}.ro{int(ro)}.t"] = f32(R), f32(t)
+            out[f"{name}.ro{int(ro)}.c"] = np.array([float(c)], np.float32)
+        # compute_pose_error: kabsch(pred -> raw) with outlier removal, mean distance over all cameras
+        obj.compute_post_transform_params = (
+            lambda from_raw_to_pred=True, return_origs=False, remove_outliers=True, raw=raw, pred=pred:
+            (obj.kabsch_algorithm(pred, raw, remove_outliers=remove_outliers), raw, pred))
+        out[f"{name}.pose_error"] = np.array([float(M.compute_pose_error(obj))], np.float32)
+    np.savez_compressed(os.path.join(OUT, "kabsch.npz"), **out)
+
+
+GENERATORS = {"kabsch": gen_kabsch, "nerf2d": gen_nerf2d, "pe": gen_pe, "composite": gen_composite, "resample": gen_resample, "model": gen_model,
               "color": gen_color, "cos_kat": gen_cos_kat, "ipe_grad": gen_ipe_grad, "garf": gen_garf,
               "pose": gen_pose, "pose_render": gen_pose_render, "mipnerf": gen_mipnerf, "feed": gen_feed}
 

@@ -93,6 +93,10 @@ def test_argument_validation_returns_status_without_launch():
     assert lib.nerf_linear_gauss_x3(None, 0, 10, 256, 32, 8, None, 256, 8, 1, 256, None, 0, 256, 8, 256, 0,
                                     None, 0, None) == -4
     assert lib.nerf_linear_gauss_workspace(1000, 64) >= 8 * 64 * 8
+    # Kabsch: too few / too many points, missing outputs
+    assert lib.nerf_kabsch(16, 16, 2, 1, 16, 16, 16, None, None) == -1
+    assert lib.nerf_kabsch(16, 16, 5000, 1, 16, 16, 16, None, None) == -1
+    assert lib.nerf_kabsch(16, 16, 10, 1, None, 16, 16, None, None) == -1
     # ray-mode encoding backward: missing rays / outputs
     p.kind = 0
     assert lib.nerf_encode_bwd_rays(ctypes.byref(p), None, 16, 16, 16, None, 16, 64, 4, 8, 16, 16, 0, None) == -1

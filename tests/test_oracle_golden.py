@@ -256,3 +256,15 @@ def test_nerf2d_oracle_vs_reference(golden):
         opt.step()
     for k, v in sd.items():
         np.testing.assert_allclose(v.detach().reshape(-1)[:256].numpy(), g[f"adam3_head.{k}"], atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize("case", ["noisy", "outliers", "reflect", "small"])
+def test_kabsch_oracle_vs_reference(golden, case):
+    g = golden("kabsch")
+    raw, pred = t(g[f"{case}.raw"]), t(g[f"{case}.pred"])
+    for ro in (1, 0):
+        R, tt, c = O.kabsch(raw, pred, bool(ro))
+        np.testing.assert_allclose(R.numpy(), g[f"{case}.ro{ro}.R"], atol=2e-6)
+        np.testing.assert_allclose(tt.numpy(), g[f"{case}.ro{ro}.t"], atol=1e-5)
+        np.testing.assert_allclose(float(c), g[f"{case}.ro{ro}.c"][0], rtol=1e-6)
+    np.testing.assert_allclose(float(O.pose_error(raw, pred)), g[f"{case}.pose_error"][0], rtol=1e-5)
