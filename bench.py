@@ -430,13 +430,21 @@ def cpu_baseline(workload: str, seconds: float = 15.0):
             "sample": f"{n} {desc}; oracle/nerf_oracle.py on torch CPU fp32, {el:.1f} s on {_cpu_model_name()}"}
 
 
+def evidence_tag(workload: str, fn: str) -> str:
+    """File tag of a kernel function's committed PMC evidence (tools/roofline_evidence.py):
+    profiles/traffic_<tag>.json and profiles/pmc_<tag>.json."""
+    return f"{workload}_" + "".join(c if c.isalnum() or c == "_" else "_" for c in fn).strip("_")
+
+
 def _roofline(ks_fn: dict, x3: bool, steps: int, workload: str):
     """Roofline object for the MFMA kernel FUNCTION with the most device time in the timed region
     (launches grouped by HIP kernel function, as rocprofv3 reports them: the fused kernel's forward
     and input-gradient-chain launches are one entry)."""
     peak = X3_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
-    mfma_fns = ("mlp_fused_fwd_kernel", "linear_nt_x3_glds_kernel", "linear_nt_x3_kernel", "linear_wgrad_x3_wide_kernel",
-                "linear_wgrad_x3_kernel", "linear_nt_kernel", "linear_wgrad_kernel")
+    # HIP kernel functions as rocprofv3 names them (template instantiations separately: the fused
+    # kernel's forward is mlp_fused_kernel<0>, its input-gradient chain mlp_fused_kernel<1>)
+    mfma_fns = ("mlp_fused_kernel<0>", "mlp_fused_kernel<1>", "linear_nt_x3_glds_kernel", "linear_nt_x3_kernel",
+                "linear_wgrad_x3_wide_kernel", "linear_wgrad_x3_kernel", "linear_nt_kernel", "linear_wgrad_kernel")
     cands = [k for k in mfma_fns if k in ks_fn]
     if not cands:
         return None
@@ -450,12 +458,13 @@ def _roofline(ks_fn: dict, x3: bool, steps: int, workload: str):
     hbm_bound = intensity < ridge
     achieved_gbs = avg_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic = None
-    tfile = os.path.join(ROOT, "profiles", f"traffic_{workload}_{dom}.json")
+    tag = evidence_tag(workload, dom)
+    tfile = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
     if os.path.exists(tfile):
         with open(tfile) as f:
             traffic = json.load(f).get("bytes_per_launch")
     pmc = None
-    pfile = os.path.join(ROOT, "profiles", f"pmc_{workload}_{dom}.json")
+    pfile = os.path.join(ROOT, "profiles", f"pmc_{tag}.json")
     if os.path.exists(pfile):
         with open(pfile) as f:
             pmc = json.load(f)

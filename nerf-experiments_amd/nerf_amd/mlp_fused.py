@@ -244,7 +244,7 @@ class FusedForward:
             nbytes += (4.0 * M * acts[idx].shape[1] if acts[idx] is not None else 0.0) \
                 + (32.0 * M if masks[idx] is not None else 0.0) + (4.0 * M if idx in col_outs else 0.0)
         end = K.TIMER.bracket("mlp_fused_fwd", flops, nbytes + self.image.numel() * self.image.element_size(),
-                              fn="mlp_fused_fwd_kernel") \
+                              fn="mlp_fused_kernel<0>") \
             if K.TIMER is not None else None
         st = _lib.load().nerf_mlp_fused_fwd(descs, L, self.image.data_ptr(), M, K._stream(self.device))
         if end is not None:
@@ -434,7 +434,7 @@ class FusedInputGrad:
             nbytes += (4.0 * d.seg_k[0] * d.seg_rows[0] if kbh else 0.0) + (32.0 * M if d.mask_in else 0.0)
             nbytes += 4.0 * M * min(d.ldo, n_out) + (4.0 * M * d.ldo2 if x is not None else 0.0)
         end = K.TIMER.bracket("mlp_fused_dgrad", flops, nbytes + self.image.numel() * self.image.element_size(),
-                              fn="mlp_fused_fwd_kernel") \
+                              fn="mlp_fused_kernel<1>") \
             if K.TIMER is not None else None
         st = _lib.load().nerf_mlp_fused_fwd(descs, S, self.image.data_ptr(), M, K._stream(self.device))
         if end is not None:

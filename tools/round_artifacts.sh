@@ -15,7 +15,7 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/
 timeout -k 10 300 python -u bench.py > "$OUT/bench_default.json" 2> "$OUT/bench_default.err" \
   || { echo "bench failed"; tail -20 "$OUT/bench_default.err"; exit 1; }
 cat "$OUT/bench_default.json"
-for w in n2v barf; do
+for w in n2v barf garf ingp; do
   timeout -k 10 300 python -u bench.py --workload $w --no-cpu-baseline > "$OUT/bench_$w.json" 2> "$OUT/bench_$w.err" \
     || { echo "bench $w failed"; tail -20 "$OUT/bench_$w.err"; exit 1; }
 done
