@@ -2,7 +2,7 @@
 
 Reads the FETCH_SIZE (bench_p1) and WRITE_SIZE (bench_p2) rocprofv3 --pmc passes and writes
   profiles/<round>/pmc_bench_n2v_traffic.json   all kernels of interest
-  profiles/traffic_<kernel>.json                 the file bench.py reads for roofline.traffic
+  (bench.py reads profiles/traffic_<workload>_<fn>.json: tools/roofline_evidence.py writes those)
 bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE counts half of wide streaming
 reads; MI355X_MICROARCH.md HBM section).
 Usage: python tools/traffic_json.py gpurun_out/<tag> profiles/<round>"""
