@@ -2,8 +2,9 @@
 // (a7, barf/model_interpolation_architecture.py:96-141; contract in include/nerf_amd.h).
 //
 // Layer-by-layer GEMMs move each 256-wide fp32 activation through HBM twice (written by
-// one launch, read by the next: 536 MB per layer at 262 144 samples).  Here a wave owns 32
-// samples and keeps their layer input in registers across the whole network:
+// one launch, read by the next: 536 MB per layer at 262 144 samples).  Here a wave owns 16 * SB
+// samples (NERF_FUSED_SB, default 1: 8 waves of 16 samples, two per SIMD; SB = 2: 4 waves of 32)
+// and keeps their layer input in registers across the whole network:
 //
 //   out^T[n][s] = W[n][:] . x^T[:][s]    A operand = weights (rows n), B = activations (cols s)
 //
@@ -14,21 +15,22 @@
 // (element j of lane group g <-> feature 32q + 16(j >> 2) + 4g + (j & 3)).  bias + ReLU + the bf16
 // hi/lo split (3 x bf16 products, as linear_x3.hip) are applied in registers.
 //
-// One wave per SIMD (4 per workgroup) holds two 16-sample column blocks: every weight fragment
-// read from LDS feeds both (6 MFMAs per 2 ds_read_b128 and k-block).  A chunk is 16 output rows:
-// its MFMA stages interleave the previous chunk's epilogue (bias, ReLU, fp32 stores, mask bits,
-// hi/lo split), whose split halves go to the wave's 32 KB LDS image of the next layer's operand;
-// at the end of the layer that image is read back into the operand registers (compile-time
-// indices: no register array is ever indexed at run time).
+// A chunk is 16 output rows: its MFMA steps interleave the previous chunk's epilogue (bias, ReLU,
+// fp32 stores, mask bits, hi/lo split) in four parts, whose split halves go to the wave's
+// SB x 16 KB LDS image of the next layer's operand; at the end of the layer that image is read
+// back into the operand registers (compile-time indices: no register array is ever indexed at run
+// time).  MODE_DGRAD runs the backward's input-gradient chain with the same loop: W^T images, the
+// forward's ReLU bits applied to each incoming gradient row, dY of every layer stored.
 //
 // Weights (2.6 MB for NerfModel) stream through LDS: the register-fed k-blocks of a chunk
 // ([kb][hi 1 KB | lo 1 KB], lane-linear 16 B per lane: one conflict-free ds_read_b128 each) are
-// LDS-DMA'd (global_load_lds_dwordx4) into a 2 x 16 KB ring one chunk ahead and shared by the 4
-// waves, so the weights cross L2 -> LDS once per 128 samples.  The k-blocks fed by HBM inputs
-// (encodings, or the head / density gradients of the backward chain) and the biases are read by
-// each wave from L2 (2 KB + 64 B per chunk).  LDS: 32 KB ring + 4 x 32 KB operand images = 160 KB.
-// Only HBM-fed inputs are loaded and only what the backward needs (each layer's output, its ReLU
-// mask bits, the density column) is stored.
+// LDS-DMA'd (buffer-addressed) into a 2 x 16 KB ring one chunk ahead and shared by the waves, so
+// the weights cross L2 -> LDS once per 128 samples.  The k-blocks fed by HBM inputs (encodings,
+// or the head / density gradients of the backward chain) and the biases are read by each wave
+// from L2.  LDS: 32 KB ring + 8 x 16 KB operand images = 160 KB.  Only HBM-fed inputs are loaded
+// and only what the backward needs (each layer's output, its ReLU mask bits, the density column)
+// is stored; waits are counted (asm fragment reads, a per-layer DMA table in VGPRs) so the
+// prefetch is never drained.
 #include <stddef.h>
 
 #include "common.h"
