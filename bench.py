@@ -17,8 +17,8 @@ Other BASELINE.json configs as extra workloads (same JSON line, their own `confi
                    CameraExtrinsics (100 views) whose gradients come back through the fused
                    ray-mode encoding backward, 4096 rays per GPU
 
-  --workload garf  garf Gaussian-activation fields (RadianceNetwork / ProposalNetwork): proposal
-                   sampler on 64 samples -> pdf resample -> radiance on 192 samples, 4096 rays per GPU
+  --workload garf  garf GarfModel (SURVEY §8 a8 + f3): proposal estimator on 64 samples (interlevel loss) ->
+                   inverse-cdf 192 samples -> radiance network, 4096 rays per GPU
   --workload ingp  configs[4]: 3d-ingp hash-grid NeRF (16-level hash encoding + NerfModelINGP on the fused
                    MLP), coarse 64 + fine 192 (round/argmax resample), 5120 rays per GPU
 
@@ -57,10 +57,11 @@ WORKLOADS = {
     "mip": {"config": "mip-NeRF masked integrated PE, coarse 64 + fine 128 samples (pdf resample), shared "
                       "NerfModel, Lego 800x800, 4096 rays per GPU (BASELINE.json configs[2])",
             "rays": 4096, "coarse": 64, "fine": 128},
-    "garf": {"config": "garf Gaussian-activation fields: ProposalNetwork (3-512-256-128-1) on 64 stratified samples as "
-                       "the sampler (forward only: its nerfacc interlevel loss is out of scope) -> pdf resample -> "
-                       "RadianceNetwork (601,604 params) on 192 samples, fwd+bwd, Adam; near/far 2/7 "
-                       "(garf/main.py:168-171), 4096 rays per GPU (the reference trains at 1024)",
+    "garf": {"config": "garf GarfModel step: nerfacc-equivalent PropNetEstimator (lindisp, stratified) with "
+                       "ProposalNetwork (3-512-256-128-1) on 64 samples -> inverse-cdf 192 samples -> RadianceNetwork "
+                       "(601,604 params) -> rendering; MSE + interlevel loss, both networks fwd+bwd, Adam; near/far "
+                       "2/7 (garf/main.py:168-171, model_garf.py:194-260), 4096 rays per GPU (the reference trains "
+                       "at 1024)",
              "rays": 4096, "coarse": 64, "fine": 192},
     "ingp": {"config": "3d-ingp hash-grid NeRF: 16-level hash encoding (16 x 2^16 x 2 fp32 table), NerfModelINGP "
                        "(8 x 256 MLP, softplus(z - 1)), coarse 64 + fine 192 samples (round/argmax resample), "
@@ -275,51 +276,61 @@ def build_workload(name: str, device, rank: int, feed: bool = False):
             return ren.training_loss(o, d, pw, target)[0]
         return ren, [ren], opt, loss_fn, lambda: ren(o, d, pw)
     if name == "garf":
+        import types
         from nerf_amd import ProposalNetwork, RadianceNetwork
-        from nerf_amd.model_interpolation import _RenderRaysFn
+        from nerf_amd.prop_sampler import PropNetEstimator, rendering
         torch.manual_seed(0)
         # garf/main.py:24-39,168-175: gaussian init [0.5, 2], gaussian lr factor 16
         radiance = RadianceNetwork(0.5, 2.0, 2e-4, 2e-5, 0, 16.0).to(device)
         proposal = ProposalNetwork(0.5, 2.0, 5e-4, 5e-5, 0, 16.0).to(device)
-        helper = NerfInterpolation(2.0, 7.0, radiance, w["fine"], "stratified_uniform", 0.0, "middle").to(device)
+        estimator = PropNetEstimator()
         groups = [{"params": list(g["parameters"]), "lr": g["learning_rate_start"], "weight_decay": g["weight_decay"]}
-                  for g in radiance.param_groups]
+                  for g in proposal.param_groups + radiance.param_groups]
         opt = FusedAdam(groups, eps=1e-5)
         o, d, pw, target, _ = synthetic_batch_lego(w["rays"], 1000 + rank, device, 400)
         B, P, S = w["rays"], w["coarse"], w["fine"]
 
-        def points(o_, d_, t0, t1, n):
-            t = (t0 + t1) / 2
-            pos = (o_.unsqueeze(1) + t.unsqueeze(2) * d_.unsqueeze(1)).reshape(B * n, 3)
-            return pos, d_.unsqueeze(1).expand(B, n, 3).reshape(B * n, 3)
+        def points(o_, d_, t0, t1):
+            # garf/model_garf.py:87-111: o + d (t0 + t1) / 2
+            pos = o_[:, None] + d_[:, None] * (t0 + t1)[..., None] / 2
+            return pos.reshape(-1, 3), d_[:, None].expand(pos.shape).reshape(-1, 3)
 
         def render(o_, d_):
-            tp0, tp1 = helper._sample_t_stratified_uniform(B, P, "stratified_uniform", 0.0)
-            with torch.no_grad():
-                pos, _ = points(o_, d_, tp0, tp1, P)
-                sigma = proposal(pos).view(B, P)
-                _, wts = _RenderRaysFn.apply(sigma, torch.zeros(B, P, 3, device=device), tp1 - tp0, 1.0, 1.0)
-            tf0, tf1 = helper._sample_t_pdf_weighted(tp0, wts, tp1 - tp0, S)
-            pos, dirs = points(o_, d_, tf0, tf1, S)
-            rgb, density = radiance(pos, dirs)
-            out, _ = _RenderRaysFn.apply(density.view(B, S), rgb.view(B, S, 3), tf1 - tf0, 1.0, 1.0)
-            return out, None
+            # GarfModel.forward (garf/model_garf.py:194-236) on nerf_amd's nerfacc-equivalent estimator
+            def prop_fn(t0, t1):
+                return proposal(points(o_, d_, t0, t1)[0]).view(t0.shape)
 
+            def rad_fn(t0, t1, _):
+                pos, dirs = points(o_, d_, t0, t1)
+                rgb, dens = radiance(pos, dirs)
+                return rgb.view(*t0.shape, 3), dens.view(t0.shape)
+
+            t0, t1 = estimator.sampling([prop_fn], [P], S, B, 2.0, 7.0, "lindisp", stratified=True,
+                                        requires_grad=torch.is_grad_enabled())
+            rgb, _, _, extras = rendering(t0, t1, rgb_sigma_fn=rad_fn)
+            return rgb, extras
+
+        def loss_of(o_, d_, c_):
+            rgb, extras = render(o_, d_)
+            # GarfModel._forward_loss (:239-260): interlevel loss for the proposal + MSE for the radiance
+            return torch.nn.functional.mse_loss(rgb, c_) + estimator.compute_loss(extras["trans"])
+
+        ren = types.SimpleNamespace(model_radiance=radiance)
         if feed:
             nxt = _feed_stream(device_feed(name, device, rank, w["rays"]))
 
             def loss_fn():
                 o_, _, d_, _, c_, _, _ = next(nxt)
-                return torch.nn.functional.mse_loss(render(o_, d_)[0], c_[:, -1])
+                return loss_of(o_, d_, c_[:, -1])
 
             def render_fn():
                 o_, _, d_, _, _, _, _ = next(nxt)
                 return render(o_, d_)
-            return helper, [radiance, proposal], opt, loss_fn, render_fn
+            return ren, [radiance, proposal], opt, loss_fn, render_fn
 
         def loss_fn():
-            return torch.nn.functional.mse_loss(render(o, d)[0], target)
-        return helper, [radiance, proposal], opt, loss_fn, lambda: render(o, d)
+            return loss_of(o, d, target)
+        return ren, [radiance, proposal], opt, loss_fn, lambda: render(o, d)
     raise ValueError(name)
 
 

@@ -471,6 +471,35 @@ int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float* x, const 
  * and to = raw camera origins.  One workgroup, fp64 fixed-order sums (deterministic).
  * ------------------------------------------------------------------------- */
 #define NERF_KABSCH_MAX_POINTS 4096
+
+/* ---------------------------------------------------------------------------
+ * Proposal-network sampling and interlevel loss: nerfacc's
+ * PropNetEstimator.sampling / compute_loss as GARF calls them (garf/model_garf.py:81,210-230,257).
+ * nerfacc is not vendored (environment.yml:26, unpinned): restated from its published algorithm,
+ * parity unpinned.  One wave per ray; rows of at most NERF_PROP_MAX_EDGES edges.
+ *
+ * nerf_prop_cdf: cdf [R][K+1] of weights w [R][K]: cdf[0] = 0, cdf[i] = sum_{j<i} w[j] (fp64),
+ *   cdf[K] = 1 — nerfacc's 1 - [trans, 0] with trans = 1 - the exclusive weight sum.
+ * nerf_prop_sample: n intervals (n + 1 edges) per ray by inverting the piecewise-linear cdf over
+ *   the ray's edges vals [R][K+1] (s-space, increasing) at u_0 = 0, u_n = 1 and u_i = i/n, or
+ *   (i - 1/2 + U_i)/n when stratified (Philox(seed, counter)); s_out = the s edges, t_out =
+ *   transform(s): 0 uniform t = s far + (1-s) near, 1 lindisp 1/t = s/far + (1-s)/near.
+ * nerf_prop_loss: interlevel loss between query intervals (q_vals, q_cdf [R][n+1], no gradient)
+ *   and key intervals (k_vals, k_cdf [R][K+1]): per query interval j, w = q_cdf[j+1] - q_cdf[j],
+ *   w_outer = k_cdf[right(q_vals[j+1])] - k_cdf[left(q_vals[j])] (right = #k_vals <= x clamped to
+ *   K, left = that - 1 clamped to 0), loss_j = max(w - w_outer, 0)^2 / (w + eps).  loss_ray [R]
+ *   (optional) = sum_j loss_j (fp64, fixed order).  grad_k_w (optional) [R][K] = d(grad_scale *
+ *   sum loss) / d key weights (k_cdf as nerf_prop_cdf forms it), gathered in a fixed order.
+ * ------------------------------------------------------------------------- */
+#define NERF_PROP_MAX_EDGES 512
+int nerf_prop_cdf(const float* w, int64_t ld_w, int64_t n_rays, int32_t K, float* cdf, int64_t ld_cdf,
+                  void* stream);
+int nerf_prop_sample(const float* vals, int64_t ld_vals, const float* cdf, int64_t ld_cdf, int64_t n_rays,
+                     int32_t K, int32_t n, int32_t stratified, uint64_t seed, uint64_t counter, int32_t transform,
+                     float near_plane, float far_plane, float* s_out, float* t_out, int64_t ld_out, void* stream);
+int nerf_prop_loss(const float* q_vals, const float* q_cdf, int64_t ld_q, const float* k_vals, const float* k_cdf,
+                   int64_t ld_k, int64_t n_rays, int32_t n, int32_t K, float eps, float* loss_ray,
+                   float grad_scale, float* grad_k_w, int64_t ld_gw, void* stream);
 int nerf_kabsch(const float* from, const float* to, int32_t n, int32_t remove_outliers, float* R, float* t,
                 float* c, float* err, void* stream);
 

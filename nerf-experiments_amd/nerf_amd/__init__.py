@@ -11,5 +11,6 @@ from .model_ingp import INGPEncoding, INGPTable, NerfModelINGP  # noqa: F401
 from .model_2d import FourierFeatures2d, Nerf2d  # noqa: F401
 from .optim import FusedAdam  # noqa: F401
 from .pose import compute_pose_error, kabsch_algorithm, validation_transform_rays  # noqa: F401
+from .prop_sampler import PropNetEstimator, rendering  # noqa: F401
 
 __version__ = "0.1.0"

@@ -36,6 +36,7 @@ NERF_EPI_TANH = 4096
 NERF_EPI_TANH_BWD = 8192
 NERF_ERR_UNSUPPORTED = -2
 NERF_KABSCH_MAX_POINTS = 4096
+NERF_PROP_MAX_EDGES = 512
 NERF_GAUSS_FWD = 0
 NERF_GAUSS_BWD = 1
 
@@ -171,6 +172,11 @@ _SIGNATURES = {
     "nerf_hashgrid_fwd": (c_i32, [ctypes.POINTER(NerfHashgridParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
                                   c_vp, c_vp, c_i64, c_vp]),
     "nerf_kabsch": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "nerf_prop_cdf": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp]),
+    "nerf_prop_sample": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i32, c_u64, c_u64, c_i32, c_f,
+                                 c_f, c_vp, c_vp, c_i64, c_vp]),
+    "nerf_prop_loss": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f, c_vp, c_f, c_vp,
+                               c_i64, c_vp]),
     "nerf_hashgrid_workspace": (c_sz, [ctypes.POINTER(NerfHashgridParams)]),
     "nerf_hashgrid_bwd": (c_i32, [ctypes.POINTER(NerfHashgridParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
                                   c_vp, c_i64, c_vp, c_i32, c_vp, c_sz, c_vp]),

@@ -567,3 +567,49 @@ def kabsch(p_from: torch.Tensor, p_to: torch.Tensor, remove_outliers: bool = Tru
     _lib.check(st, "nerf_kabsch")
     R, t, c = out[:9].view(3, 3), out[9:12].view(1, 3), out[12]
     return (R, t, c, out[13]) if error else (R, t, c)
+
+
+# ----------------------------------------------------------------------------- proposal sampler
+def prop_cdf(w: torch.Tensor) -> torch.Tensor:
+    """[R, K] weights -> [R, K+1] cdf (0, exclusive sums, 1) — nerf_prop_cdf."""
+    _require_cuda_f32("weights", w)
+    R, Kb = w.shape
+    if w.stride(1) != 1:
+        w = w.contiguous()
+    cdf = torch.empty(R, Kb + 1, device=w.device, dtype=torch.float32)
+    _lib.check(_lib.load().nerf_prop_cdf(w.data_ptr(), w.stride(0), R, Kb, cdf.data_ptr(), cdf.stride(0),
+                                         _stream(w.device)), "nerf_prop_cdf")
+    return cdf
+
+
+def prop_sample(vals: torch.Tensor, cdf: torch.Tensor, n: int, stratified: bool, seed: int, transform: int,
+                near: float, far: float):
+    """Inverse-cdf sampling of n intervals per ray: (s edges, t edges), each [R, n+1] — nerf_prop_sample."""
+    for name, t in (("vals", vals), ("cdf", cdf)):
+        _require_cuda_f32(name, t)
+        if t.stride(1) != 1:
+            raise ValueError(f"{name} must be row-major")
+    R, E = vals.shape
+    if cdf.shape != (R, E) or E > _lib.NERF_PROP_MAX_EDGES or n + 1 > _lib.NERF_PROP_MAX_EDGES:
+        raise ValueError(f"vals / cdf must be [R, K+1] with K+1 and n+1 <= {_lib.NERF_PROP_MAX_EDGES}")
+    s = torch.empty(R, n + 1, device=vals.device, dtype=torch.float32)
+    t = torch.empty_like(s)
+    _lib.check(_lib.load().nerf_prop_sample(vals.data_ptr(), vals.stride(0), cdf.data_ptr(), cdf.stride(0), R, E - 1,
+                                            n, int(stratified), seed, 0, transform, float(near), float(far),
+                                            s.data_ptr(), t.data_ptr(), s.stride(0), _stream(vals.device)),
+               "nerf_prop_sample")
+    return s, t
+
+
+def prop_loss(q_vals, q_cdf, k_vals, k_cdf, eps: float, grad_scale: float = 0.0, want_loss: bool = True,
+              want_grad: bool = False):
+    """Interlevel loss of query vs key intervals: (per-ray loss sums [R] or None, d/d key weights [R, K] or None)."""
+    R, E = q_vals.shape
+    Kb = k_vals.shape[1] - 1
+    lr = torch.empty(R, device=q_vals.device, dtype=torch.float32) if want_loss else None
+    gw = torch.empty(R, Kb, device=q_vals.device, dtype=torch.float32) if want_grad else None
+    _lib.check(_lib.load().nerf_prop_loss(q_vals.data_ptr(), q_cdf.data_ptr(), q_vals.stride(0), k_vals.data_ptr(),
+                                          k_cdf.data_ptr(), k_vals.stride(0), R, E - 1, Kb, float(eps), _ptr(lr),
+                                          float(grad_scale), _ptr(gw), gw.stride(0) if gw is not None else 0,
+                                          _stream(q_vals.device)), "nerf_prop_loss")
+    return lr, gw

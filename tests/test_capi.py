@@ -97,6 +97,14 @@ def test_argument_validation_returns_status_without_launch():
     assert lib.nerf_kabsch(16, 16, 2, 1, 16, 16, 16, None, None) == -1
     assert lib.nerf_kabsch(16, 16, 5000, 1, 16, 16, 16, None, None) == -1
     assert lib.nerf_kabsch(16, 16, 10, 1, None, 16, 16, None, None) == -1
+    # proposal sampler: too many edges, bad transform, lindisp with near 0, no outputs; empty batches
+    assert lib.nerf_prop_sample(16, 600, 16, 600, 4, 599, 8, 0, 0, 0, 1, 2.0, 7.0, 16, 16, 16, None) == -1
+    assert lib.nerf_prop_sample(16, 65, 16, 65, 4, 64, 8, 0, 0, 0, 2, 2.0, 7.0, 16, 16, 16, None) == -1
+    assert lib.nerf_prop_sample(16, 65, 16, 65, 4, 64, 8, 0, 0, 0, 1, 0.0, 7.0, 16, 16, 16, None) == -1
+    assert lib.nerf_prop_sample(16, 65, 16, 65, 0, 64, 8, 0, 0, 0, 1, 2.0, 7.0, 16, 16, 16, None) == 0
+    assert lib.nerf_prop_loss(16, 16, 193, 16, 16, 65, 4, 192, 64, 1e-7, None, 0.0, None, 0, None) == -1
+    assert lib.nerf_prop_cdf(16, 63, 4, 64, 16, 65, None) == -1
+    assert lib.nerf_prop_cdf(None, 64, 0, 64, None, 65, None) == 0
     # ray-mode encoding backward: missing rays / outputs
     p.kind = 0
     assert lib.nerf_encode_bwd_rays(ctypes.byref(p), None, 16, 16, 16, None, 16, 64, 4, 8, 16, 16, 0, None) == -1
