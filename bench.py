@@ -568,8 +568,11 @@ def main():
     args = ap.parse_args()
     torch.set_float32_matmul_precision(args.matmul_precision)
 
-    world, rank, local_rank, dist = init_distributed("nccl")
-    device = torch.device("cuda", local_rank)
+    # NERF_DIST_BACKEND=gloo rehearses the multi-process step on fewer GPUs than ranks (ranks share
+    # devices round-robin); the driver's runs use RCCL ("nccl"), one GPU per rank
+    backend = os.environ.get("NERF_DIST_BACKEND", "nccl")
+    world, rank, local_rank, dist = init_distributed(backend)
+    device = torch.device("cuda", local_rank if backend == "nccl" else local_rank % torch.cuda.device_count())
     torch.cuda.set_device(device)
 
     import nerf_amd
