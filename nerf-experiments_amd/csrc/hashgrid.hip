@@ -44,7 +44,7 @@ __device__ __forceinline__ void sample_position(const HashArgs& a, int64_t n, fl
 }
 
 struct Corners {
-    int64_t idx[8];
+    int idx[8];           // table rows (< T < 2^31)
     float w[8];
 };
 
@@ -59,6 +59,7 @@ __device__ __forceinline__ Corners level_corners(const float* p, int r, int T) {
         base[j] = (long long)floorf(xh[j]);
     }
     const bool bij = (long long)(r + 1) * (r + 1) * (r + 1) <= (long long)T;
+    const bool pow2 = (T & (T - 1)) == 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         long long cc[3];
@@ -70,19 +71,20 @@ __device__ __forceinline__ Corners level_corners(const float* p, int r, int T) {
         }
         c.w[k] = (dw[0] * dw[1]) * dw[2];
         if (bij) {
-            const long long r1 = r + 1;
-            long long q[3];
+            const int r1 = r + 1;
+            int q[3];
 #pragma unroll
-            for (int j = 0; j < 3; ++j) q[j] = cc[j] < 0 ? 0 : (cc[j] > r ? r : cc[j]);
+            for (int j = 0; j < 3; ++j) q[j] = cc[j] < 0 ? 0 : (cc[j] > r ? r : (int)cc[j]);
             c.idx[k] = q[0] + r1 * q[1] + r1 * r1 * q[2];
+        } else if (pow2) {
+            // the int64 product-xor modulo a power of two is its low bits, which only the low 32
+            // bits of the corners and primes determine (two's complement): 32-bit arithmetic
+            const unsigned h = (unsigned)cc[0] ^ ((unsigned)cc[1] * 2654435761u) ^ ((unsigned)cc[2] * 805459861u);
+            c.idx[k] = (int)(h & (unsigned)(T - 1));
         } else {
             const long long h = (cc[0] * 1LL) ^ (cc[1] * 2654435761LL) ^ (cc[2] * 805459861LL);
-            if ((T & (T - 1)) == 0) {
-                c.idx[k] = h & (long long)(T - 1);  // two's complement: the non-negative remainder
-            } else {
-                const long long m = h % (long long)T;
-                c.idx[k] = m < 0 ? m + T : m;
-            }
+            const long long m = h % (long long)T;
+            c.idx[k] = (int)(m < 0 ? m + T : m);
         }
     }
     return c;
@@ -107,7 +109,7 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(HashArgs a, const flo
     for (int k = 0; k < 8; ++k) {
 #pragma unroll
         for (int f = 0; f < NERF_HASHGRID_MAX_FEATURES; ++f)
-            if (f < F) acc[f] = acc[f] + c.w[k] * tab[c.idx[k] * F + f];
+            if (f < F) acc[f] = acc[f] + c.w[k] * tab[(int64_t)c.idx[k] * F + f];
     }
     float* o = out + n * ld + (int64_t)l * F;
 #pragma unroll
@@ -145,7 +147,17 @@ __global__ __launch_bounds__(256) void hashgrid_gmax_kernel(const float* __restr
         const unsigned o = __shfl_xor(m, off, 64);
         m = o > m ? o : m;
     }
-    if ((threadIdx.x & 63) == 0 && m != 0) atomicMax(gmax, m);
+    // one atomic per block: same-address atomics serialise at the memory side (one per wave of
+    // 16 K waves took ~190 us)
+    __shared__ unsigned wm[4];
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = wm[0] > wm[1] ? wm[0] : wm[1];
+        m = m > wm[2] ? m : wm[2];
+        m = m > wm[3] ? m : wm[3];
+        if (m != 0) atomicMax(gmax, m);
+    }
 }
 
 // fixed-point exponent s with 8 * n * gmax * 2^s < 2^62 (no entry can overflow); -1000 flags a
@@ -210,7 +222,9 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_kernel(HashArgs a, B
     __syncthreads();
     const bool rays = a.x == nullptr, mid = a.p.query != 0, small = a.n < ((int64_t)1 << 31);
     const int64_t n1 = (slab + 1) * pl.slab < a.n ? (slab + 1) * pl.slab : a.n;
-    for (int64_t nb = slab * pl.slab + threadIdx.x; nb < n1; nb += BWD_UNROLL * BWD_THREADS) {
+    // samples past the slab are masked, their loads clamped into it
+    for (int64_t base = slab * pl.slab; base < n1; base += BWD_UNROLL * BWD_THREADS) {
+        const int64_t nb = base + threadIdx.x;
         float p[BWD_UNROLL][3], gv[BWD_UNROLL][F];
         // loads first (indices clamped into the slab, so every load is in bounds) ...
         if (rays) {
@@ -258,7 +272,7 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_kernel(HashArgs a, B
             int rel[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                const int64_t r = c.idx[k] - row0;
+                const int64_t r = (int64_t)c.idx[k] - row0;
                 rel[k] = (int)r;
                 if ((uint64_t)r < (uint64_t)prow) pend |= 1u << k;
             }
@@ -364,7 +378,7 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
         const int cols = params->levels * params->features;
         const bool vec = cols % 4 == 0 && g_ld % 4 == 0 && (reinterpret_cast<uintptr_t>(grad_out) & 15) == 0;
         int64_t blocks = (n_samples * (vec ? cols / 4 : cols) + 255) / 256;
-        blocks = blocks < 4096 ? blocks : 4096;
+        blocks = blocks < 1024 ? blocks : 1024;
         if (vec)
             hipLaunchKernelGGL(hashgrid_gmax_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, s, grad_out, g_ld,
                                n_samples, cols, gmax);
