@@ -503,6 +503,29 @@ int nerf_prop_loss(const float* q_vals, const float* q_cdf, int64_t ld_q, const 
 int nerf_kabsch(const float* from, const float* to, int32_t n, int32_t remove_outliers, float* R, float* t,
                 float* c, float* err, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * BARF camera refinement in front of the ray path:
+ * CameraExtrinsics.forward (barf/model_camera_extrinsics.py:61-85, so3_to_SO3 :23-43).
+ * Replaces the torch chain matrix_exp([rotation]_x) -> [img_idx] gather -> R @ d, o + t / MAGIC
+ * and its autograd backward (index_add + matrix_exp's block-matrix backward).
+ *
+ * nerf_pose_rays_fwd: rotation, translation [n_images][3] (so3 / translation parameters),
+ *   img_idx [n_rays] int64, o, d [n_rays][3].  Writes new_o = o + translation[i] / magic,
+ *   new_d = R_i d (R_i = exp of the skew matrix of rotation[i], Rodrigues in fp64 rounded to fp32),
+ *   and optionally R [n_rays][3][3] (row-major) and t [n_rays][3] = translation[i] / magic.
+ *   An out-of-range image index yields NaN outputs for that ray.
+ * nerf_pose_rays_bwd: gradients of the per-ray outputs (g_new_o, g_new_d, g_R, g_t; any may be
+ *   NULL = zero) to g_rotation, g_translation [n_images][3] (overwritten; zero for images without
+ *   rays).  One workgroup per image, fixed-order fp64 sums, the analytic derivative of Rodrigues'
+ *   formula: deterministic.
+ * ------------------------------------------------------------------------- */
+int nerf_pose_rays_fwd(const float* rotation, const float* translation, int32_t n_images, const int64_t* img_idx,
+                       const float* o, const float* d, int64_t n_rays, float magic, float* new_o, float* new_d,
+                       float* R, float* t, void* stream);
+int nerf_pose_rays_bwd(const float* rotation, int32_t n_images, const int64_t* img_idx, const float* d,
+                       int64_t n_rays, float magic, const float* g_new_o, const float* g_new_d, const float* g_R,
+                       const float* g_t, float* g_rotation, float* g_translation, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -172,6 +172,8 @@ _SIGNATURES = {
     "nerf_hashgrid_fwd": (c_i32, [ctypes.POINTER(NerfHashgridParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
                                   c_vp, c_vp, c_i64, c_vp]),
     "nerf_kabsch": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "nerf_pose_rays_fwd": (c_i32, [c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_i64, c_f, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "nerf_pose_rays_bwd": (c_i32, [c_vp, c_i32, c_vp, c_vp, c_i64, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "nerf_prop_cdf": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp]),
     "nerf_prop_sample": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i32, c_u64, c_u64, c_i32, c_f,
                                  c_f, c_vp, c_vp, c_i64, c_vp]),

@@ -569,6 +569,69 @@ def kabsch(p_from: torch.Tensor, p_to: torch.Tensor, remove_outliers: bool = Tru
     return (R, t, c, out[13]) if error else (R, t, c)
 
 
+# ----------------------------------------------------------------------------- camera refinement
+def _check_pose_inputs(rotation, translation, img_idx, o, d):
+    for name, x in (("rotation", rotation), ("translation", translation), ("o", o), ("d", d)):
+        _require_cuda_f32(name, x)
+    if img_idx.device != o.device or img_idx.dtype != torch.int64:
+        raise ValueError("img_idx must be an int64 tensor on the rays' device")
+    n_img = rotation.shape[0]
+    if rotation.shape != (n_img, 3) or translation.shape != (n_img, 3):
+        raise ValueError("rotation / translation must be [n_images, 3]")
+    B = img_idx.numel()
+    if o.shape != (B, 3) or d.shape != (B, 3):
+        raise ValueError(f"o / d must be [{B}, 3] (one row per image index)")
+
+
+class _PoseRays(torch.autograd.Function):
+    """CameraExtrinsics.forward on nerf_pose_rays_fwd / _bwd (csrc/camera.hip)."""
+
+    @staticmethod
+    def forward(ctx, rotation, translation, img_idx, o, d, magic):
+        rotation, translation = rotation.contiguous(), translation.contiguous()
+        idx, o, d = img_idx.reshape(-1).contiguous(), o.contiguous(), d.contiguous()
+        B = idx.numel()
+        new_o = torch.empty(B, 3, device=o.device, dtype=torch.float32)
+        new_d = torch.empty_like(new_o)
+        R = torch.empty(B, 3, 3, device=o.device, dtype=torch.float32)
+        t = torch.empty_like(new_o)
+        _lib.check(_lib.load().nerf_pose_rays_fwd(rotation.data_ptr(), translation.data_ptr(), rotation.shape[0],
+                                                  idx.data_ptr(), o.data_ptr(), d.data_ptr(), B, float(magic),
+                                                  new_o.data_ptr(), new_d.data_ptr(), R.data_ptr(), t.data_ptr(),
+                                                  _stream(o.device)), "nerf_pose_rays_fwd")
+        ctx.save_for_backward(rotation, idx, d, R)
+        ctx.magic = magic
+        ctx.set_materialize_grads(False)          # unused outputs reach the kernel as NULL
+        return new_o, new_d, R, t
+
+    @staticmethod
+    def backward(ctx, g_o, g_d, g_R, g_t):
+        rotation, idx, d, R = ctx.saved_tensors
+        B = idx.numel()
+        grads = [None] * 6
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            gr = [None if g is None else g.contiguous() for g in (g_o, g_d, g_R, g_t)]
+            g_rot = torch.empty_like(rotation)
+            g_trans = torch.empty_like(rotation)
+            _lib.check(_lib.load().nerf_pose_rays_bwd(rotation.data_ptr(), rotation.shape[0], idx.data_ptr(),
+                                                      d.data_ptr(), B, float(ctx.magic), *[_ptr(g) for g in gr],
+                                                      g_rot.data_ptr(), g_trans.data_ptr(), _stream(d.device)),
+                       "nerf_pose_rays_bwd")
+            grads[0], grads[1] = g_rot, g_trans
+        if ctx.needs_input_grad[3]:
+            grads[3] = g_o
+        if ctx.needs_input_grad[4] and g_d is not None:          # d new_d / d d = R^T
+            grads[4] = torch.bmm(R.transpose(1, 2), g_d.unsqueeze(-1)).squeeze(-1)
+        return tuple(grads)
+
+
+def pose_rays(rotation, translation, img_idx, o, d, magic: float = 1.0):
+    """(new_o [B,3], new_d [B,3], R [B,3,3], t [B,3]) of CameraExtrinsics.forward, differentiable
+    in rotation / translation (and o / d)."""
+    _check_pose_inputs(rotation, translation, img_idx, o, d)
+    return _PoseRays.apply(rotation, translation, img_idx, o, d, magic)
+
+
 # ----------------------------------------------------------------------------- proposal sampler
 def prop_cdf(w: torch.Tensor) -> torch.Tensor:
     """[R, K] weights -> [R, K+1] cdf (0, exclusive sums, 1) — nerf_prop_cdf."""

@@ -2,15 +2,19 @@
 
 Mirrors barf/model_camera_extrinsics.py:7-85 (``CameraExtrinsics``: so3 rotation and translation
 per training image, ``so3_to_SO3`` by the matrix exponential of the skew matrix, ``forward``
-returning the refined origins / directions).  Plain torch ops on tiny [n_images, 3] tensors —
-the gradient reaching ``rotation`` / ``translation`` comes out of the fused ray-mode encoding
-backward (nerf_encode_bwd_rays) and the direction encoding's backward.
+returning the refined origins / directions and the per-ray R, t).  ``forward`` is one HIP launch
+(nerf_pose_rays_fwd, csrc/camera.hip) and its backward one more (nerf_pose_rays_bwd: per-image
+fixed-order sums and the analytic so3 derivative); the gradient reaching it comes out of the fused
+ray-mode encoding backward (nerf_encode_bwd_rays) and the direction encoding's backward.
+``so3_to_SO3`` / ``get_rotations`` stay the reference's torch expressions (the noise generation
+of the ray feed calls them on host tensors).
 """
 from __future__ import annotations
 
 import torch as th
 import torch.nn as nn
 
+from . import kernels as K
 from .model_interpolation_architecture import NerfBaseModel
 
 # barf/magic.py:1
@@ -33,21 +37,17 @@ class CameraExtrinsics(NerfBaseModel):
         return th.matrix_exp(th.cross(-th.eye(3, device=so3.device).view(1, 3, 3), so3.view(-1, 3, 1), dim=1))
 
     def get_rotations(self, img_idx: th.Tensor) -> th.Tensor:
-        # index_select == [img_idx] for a 1-D index; its backward is an index_add (the advanced-
-        # indexing backward sorts the indices: three extra kernels per step)
         return CameraExtrinsics.so3_to_SO3(self.rotation).index_select(0, img_idx.reshape(-1)).view(
             *img_idx.shape, 3, 3)
 
     def forward_origins(self, i: th.Tensor, o: th.Tensor) -> tuple[th.Tensor, th.Tensor]:
-        t = self.translation.index_select(0, i.reshape(-1)).view(*i.shape, 3) / MAGIC_NUMBER_THE_SECOND
-        return o + t, t
+        new_o, _, _, t = K.pose_rays(self.rotation, self.translation, i, o, o, MAGIC_NUMBER_THE_SECOND)
+        return new_o, t
 
     def forward(self, i: th.Tensor, o: th.Tensor, d: th.Tensor):
-        new_o, t = self.forward_origins(i, o)
-        R = self.get_rotations(i)
-        # R @ d per ray as a 3-term elementwise sum (a batched 3x3 GEMM on hipBLASLt is ~4 kernels)
-        new_d = (R * d.unsqueeze(-2)).sum(-1)
-        return new_o, new_d, R, t
+        """(new_o, new_d, R, t) as model_camera_extrinsics.py:77-85 returns them ([B, 3], [B, 3],
+        [B, 3, 3], [B, 3]); ROCm tensors only (nerf_amd has no CPU path)."""
+        return K.pose_rays(self.rotation, self.translation, i, o, d, MAGIC_NUMBER_THE_SECOND)
 
 
 __all__ = ["CameraExtrinsics"]

@@ -221,25 +221,31 @@ def test_shard_rays_partition():
         assert idx == list(range(n))
 
 
-def test_camera_extrinsics_matches_reference(golden):
-    """CameraExtrinsics (barf/model_camera_extrinsics.py:7-85): refined origins / directions,
-    rotations and parameter gradients vs the reference run (torch ops; index_select and the
-    elementwise R @ d agree with the reference's indexing and matmul to fp32 rounding)."""
-    from nerf_amd.model_camera_extrinsics import CameraExtrinsics
+def test_camera_extrinsics_oracle_matches_reference(golden):
+    """Oracle restatement of CameraExtrinsics.forward (barf/model_camera_extrinsics.py:7-85):
+    refined origins / directions, rotations and parameter gradients vs the reference run."""
+    from oracle import nerf_oracle as O
     g = golden("pose")
-    m = CameraExtrinsics(10, 1e-3, 1e-5, 100)
-    with torch.no_grad():
-        m.rotation.copy_(torch.from_numpy(g["rotation"]))
-        m.translation.copy_(torch.from_numpy(g["translation"]))
+    rot = torch.from_numpy(g["rotation"]).requires_grad_()
+    trans = torch.from_numpy(g["translation"]).requires_grad_()
     idx = torch.from_numpy(g["idx"])
-    new_o, new_d, R, t = m(idx, torch.from_numpy(g["o"]), torch.from_numpy(g["d"]))
+    new_o, new_d, R, t = O.camera_extrinsics(rot, trans, idx, torch.from_numpy(g["o"]), torch.from_numpy(g["d"]))
     np.testing.assert_allclose(new_o.detach().numpy(), g["new_o"], atol=1e-6)
     np.testing.assert_allclose(new_d.detach().numpy(), g["new_d"], atol=1e-6)
     np.testing.assert_allclose(R.detach().numpy(), g["R"], atol=1e-6)
     ((new_o * torch.from_numpy(g["go"])).sum() + (new_d * torch.from_numpy(g["gd"])).sum()).backward()
-    np.testing.assert_allclose(m.rotation.grad.numpy(), g["drot"], atol=1e-4, rtol=1e-5)
-    np.testing.assert_allclose(m.translation.grad.numpy(), g["dtrans"], atol=1e-5, rtol=1e-6)
+    np.testing.assert_allclose(rot.grad.numpy(), g["drot"], atol=1e-4, rtol=1e-5)
+    np.testing.assert_allclose(trans.grad.numpy(), g["dtrans"], atol=1e-5, rtol=1e-6)
+
+
+def test_camera_extrinsics_module_api_and_no_cpu_path():
+    """The module keeps the reference's parameters / param_groups; forward refuses host tensors."""
+    from nerf_amd.model_camera_extrinsics import CameraExtrinsics
+    m = CameraExtrinsics(10, 1e-3, 1e-5, 100)
+    assert [n for n, _ in m.named_parameters()] == ["rotation", "translation"]
     assert len(m.param_groups) == 1
+    with pytest.raises(ValueError):
+        m(torch.zeros(4, dtype=torch.int64), torch.zeros(4, 3), torch.zeros(4, 3))
 
 
 def _emulate_fused(plan, fused, image_f64, x_pos, x_dir, dir_rd, relu_floor=True):
