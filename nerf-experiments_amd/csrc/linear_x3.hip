@@ -1048,6 +1048,195 @@ __global__ __launch_bounds__(512, 1) void linear_wgrad_x3_wide_kernel(TNArgs a, 
     }
 }
 
+// ------------------------------------------------------------------- TN stream
+// The 256 x 256 weight-gradient tile (N, K <= 256: one tile per layer) with the operands
+// streamed by LDS-DMA instead of register loads.  The register-staged kernel above has 64 KB
+// per CU in flight only while its MFMAs run; the split and the transposed LDS writes then wait
+// for the loads, with nothing in flight, and the kernel reaches ~0.4 of HBM.  Here the raw fp32
+// rows (16 samples x 256 columns of dY and of X: 32 KB per step) land in a 3-stage ring two
+// steps ahead of the step being multiplied, so two steps (64 KB) are always in flight; the only
+// vector-memory ops in the loop are these DMAs, so the counted waits track them alone.  Each
+// step, thread (operand, column c) reads its column's 16 samples from the ring (conflict-free:
+// a wave reads 64 consecutive columns of a row), splits them into bf16 hi/lo and writes one
+// 64-byte image row [hi 0-7 | hi 8-15 | lo 0-7 | lo 8-15] (the swz layout of the 128-tile
+// kernel) while the waves multiply the other image stage.  The MFMA sequence is that of the
+// wide kernel (16-sample k-steps in sample order, lo*hi + hi*lo + hi*hi): identical slabs.  The
+// bias gradient is the dY thread's own column sum over the split, in sample order.
+// LDS: 3 x 32 KB ring + 2 x 32 KB images = 160 KB.
+constexpr int WS_T = 16;                        // samples per step
+constexpr int WS_RAW = 2 * WS_T * 1024;         // ring stage: dY rows then X rows, 1 KB each
+constexpr int WS_IMG = 2 * 256 * 64;            // image stage: Y rows then X rows, 64 B each
+__global__ __launch_bounds__(512, 1) void linear_wgrad_x3_stream_kernel(TNArgs a, int npad, int kpad) {
+    __shared__ __attribute__((aligned(16))) char smem[3 * WS_RAW + 2 * WS_IMG];
+    char* const ring = smem;
+    char* const img = smem + 3 * WS_RAW;
+
+    const int split = blockIdx.x;
+    const int mbeg = split * a.m_per_split;
+    int mend = mbeg + a.m_per_split;
+    if (mend > a.M) mend = a.M;
+    const int steps = mbeg < mend ? (mend - mbeg + WS_T - 1) / WS_T : 0;
+
+    const int t = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
+    const int wr = wave >> 2, wc = wave & 3;
+    const int li = lane & 31, lh = lane >> 5;
+
+    // X segment of packed column kx (segments span multiples of 32 columns)
+    auto x_seg = [&](int kx, int& xs, int& xoff) __attribute__((always_inline)) {
+        xs = -1;
+        xoff = 0;
+#pragma unroll
+        for (int q = 0; q < MAX_SEGS; ++q)
+            if (q < a.X.n && kx >= a.X.koff[q] && kx < a.X.koff[q] + a.X.kp[q]) { xs = q; xoff = kx - a.X.koff[q]; }
+    };
+    // ---- DMA sources of this lane: columns 4 lane .. 4 lane + 3 of dY and of X (invalid
+    // columns read column 0: finite data, zeroed when converted)
+    const int ycol = 4 * lane < a.N ? 4 * lane : 0;
+    int dxs, dxoff;
+    x_seg(4 * lane, dxs, dxoff);
+    const bool dx_ok = dxs >= 0 && dxoff < pick4(a.X.k, dxs);
+    const float* dxp = dx_ok ? pick4(a.X.ptr, dxs) + dxoff : a.X.ptr[0];
+    const int64_t dxld = dx_ok ? pick4(a.X.ld, dxs) : a.X.ld[0];
+    const unsigned dxrd = dx_ok ? (unsigned)pick4(a.X.row_div, dxs) : (unsigned)a.X.row_div[0];
+    // wave w brings rows 2w, 2w + 1 of both operands
+    auto issue = [&](int step) __attribute__((always_inline)) {
+        char* st = ring + (step % 3) * WS_RAW;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int r = 2 * wave + q;
+            int m = mbeg + step * WS_T + r;
+            m = m < mend ? m : mbeg;                       // past the split: any valid row (zeroed)
+            const float* ys = a.dY + (int64_t)m * a.lddy + ycol;
+            __builtin_amdgcn_global_load_lds((glb_void_t*)ys, (lds_void_t*)(st + r * 1024), 16, 0, 0);
+            const unsigned xr = dxrd == 1u ? (unsigned)m : (unsigned)m / dxrd;
+            const float* xsrc = dxp + (int64_t)xr * dxld;
+            __builtin_amdgcn_global_load_lds((glb_void_t*)xsrc, (lds_void_t*)(st + (WS_T + r) * 1024), 16, 0, 0);
+        }
+    };
+
+    // ---- conversion role: operand op (0 dY, 1 X), column c
+    const int op = t >> 8, c = t & 255;
+    bool c_ok;
+    if (op == 0) {
+        c_ok = c < a.N;
+    } else {
+        int xs, xoff;
+        x_seg(c, xs, xoff);
+        c_ok = xs >= 0 && xoff < pick4(a.X.k, xs);
+    }
+    float db = 0.f;
+    auto convert = [&](int step) __attribute__((always_inline)) {
+        const float* src = reinterpret_cast<const float*>(ring + (step % 3) * WS_RAW + op * WS_T * 1024) + c;
+        __bf16* dst = reinterpret_cast<__bf16*>(img + (step & 1) * WS_IMG + op * 256 * 64);
+        const int valid = mend - (mbeg + step * WS_T);      // rows of this step inside the split
+        // every row is read (the ring rows past the split hold finite data) and masked after, so
+        // the reads issue back to back (a select per read becomes a branch around it)
+        float v[WS_T];
+#pragma unroll
+        for (int r = 0; r < WS_T; ++r) v[r] = src[r * 256];
+        const unsigned cm = c_ok ? ~0u : 0u;
+#pragma unroll
+        for (int r = 0; r < WS_T; ++r)
+            v[r] = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, v[r]) & (r < valid ? cm : 0u));
+        if (op == 0) {
+#pragma unroll
+            for (int r = 0; r < WS_T; ++r) db += v[r];
+        }
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            bf16x8 h, l;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const float x = v[8 * hh + r];
+                const __bf16 hb = (__bf16)x;
+                h[r] = hb;
+                l[r] = (__bf16)(x - (float)hb);
+            }
+            *reinterpret_cast<bf16x8*>(dst + swz(c, hh)) = h;
+            *reinterpret_cast<bf16x8*>(dst + swz(c, 2 + hh)) = l;
+        }
+    };
+    auto barrier = []() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    // waves whose k columns lie wholly past the packed K skip the MFMAs (wave-uniform)
+    const bool active = wc * 64 < a.X.ktot && wr * 128 < a.N;
+
+    if (steps > 0) {
+        // prologue: steps 0 and 1 in flight; step 0 converted; step 2 issued; step 1 landed
+        issue(0);
+        if (steps > 1) {
+            issue(1);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        barrier();
+        convert(0);
+        if (steps > 2) {
+            issue(2);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        barrier();
+        for (int i = 0; i < steps; ++i) {
+            if (active) {
+                const __bf16* Yb = reinterpret_cast<const __bf16*>(img + (i & 1) * WS_IMG);
+                const __bf16* Xb = Yb + 256 * 32;
+                bf16x8 xh[2], xl[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int row = wc * 64 + j * 32 + li;
+                    xh[j] = *reinterpret_cast<const bf16x8*>(Xb + swz(row, lh));
+                    xl[j] = *reinterpret_cast<const bf16x8*>(Xb + swz(row, 2 + lh));
+                }
+#pragma unroll
+                for (int ii = 0; ii < 4; ++ii) {
+                    const int row = wr * 128 + ii * 32 + li;
+                    const bf16x8 yh = *reinterpret_cast<const bf16x8*>(Yb + swz(row, lh));
+                    const bf16x8 yl = *reinterpret_cast<const bf16x8*>(Yb + swz(row, 2 + lh));
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) acc[ii][j] = mfma_x3(yh, yl, xh[j], xl[j], acc[ii][j]);
+                }
+            }
+            if (i + 1 < steps) convert(i + 1);
+            if (i + 3 < steps) {
+                issue(i + 3);                                   // into the stage step i held
+                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // step i + 2 landed
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            barrier();
+        }
+    }
+
+    float* slab = a.slab + (size_t)split * npad * kpad;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int k = wc * 64 + j * 32 + li;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int n = wr * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (n < npad && k < kpad) slab[(size_t)n * kpad + k] = acc[i][j][r];
+            }
+        }
+    if (op == 0 && c < npad) a.db_slab[(size_t)split * npad + c] = db;
+}
+
 // Interleaved split weights: element (r, c) of a [rows][ld] matrix goes to
 // Wx[r][c / 32][c % 32] (hi) and Wx[r][c / 32][32 + c % 32] (lo), i.e. each 32-column
 // chunk of a row is 128 contiguous bytes: 32 hi then 32 lo.
@@ -1258,8 +1447,13 @@ extern "C" int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N, c
     TNArgs a{dY, ld_dy, N, L, (int)M, (int)mps, splits, slab, db_slab};
     if ((N > 128 || L.ktot > 128) && N <= 256 && L.ktot <= 256) {   // one 256 x 256 tile covers the layer
         const int64_t blocks = (int64_t)splits * ((N + 255) / 256) * ((L.ktot + 255) / 256);
-        hipLaunchKernelGGL(linear_wgrad_x3_wide_kernel, dim3((unsigned)blocks), dim3(512), 0, as_stream(stream), a,
-                           ntn * TB, ntk * TB);
+        static const int kern = [] { const char* e = getenv("NERF_WGRAD_KERNEL"); return e ? atoi(e) : 0; }();
+        if (kern == 1)
+            hipLaunchKernelGGL(linear_wgrad_x3_stream_kernel, dim3((unsigned)blocks), dim3(512), 0, as_stream(stream),
+                               a, ntn * TB, ntk * TB);
+        else
+            hipLaunchKernelGGL(linear_wgrad_x3_wide_kernel, dim3((unsigned)blocks), dim3(512), 0, as_stream(stream), a,
+                               ntn * TB, ntk * TB);
         NERF_CHECK_LAUNCH();
         return NERF_OK;
     }

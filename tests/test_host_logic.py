@@ -388,3 +388,44 @@ def test_ray_feed_blur_selection():
     mode, lo, hi, a, b = blur_selection(sig, 3.0)
     assert (mode, lo, hi) == (3, 1, 2)
     assert abs(a - (3.0 - 2.0) / (4.0 - 2.0 + 1e-8)) < 1e-12 and abs(a + b - 1) < 1e-12
+
+
+def test_lightning_style_mixin():
+    """INTEGRATION.md's Lightning recipe: the renderer mixed with a LightningModule-like base
+    (stand-in: pytorch_lightning is not installed) constructs once, keeps the reference's
+    attributes and hands the trainer FusedAdam + SchedulerLeNice."""
+    import torch.nn as nn
+    from nerf_amd import FourierFeatures, NerfModel
+    from nerf_amd.model_interpolation import NerfInterpolation as _Renderer, SchedulerLeNice
+    from nerf_amd.optim import FusedAdam
+
+    class LightningModule(nn.Module):              # what the recipe relies on of pl.LightningModule
+        inits = 0
+
+        def __init__(self):
+            super().__init__()
+            LightningModule.inits += 1
+            self.logged = {}
+
+        def log_dict(self, d, **kw):
+            self.logged.update(d)
+
+    class NerfInterpolation(_Renderer, LightningModule):
+        def training_step(self, batch, batch_idx):
+            return self._step_helper(batch, batch_idx, "train")
+
+    class BarfLike(NerfInterpolation):             # an experiment's subclass, unchanged
+        def _step_helper(self, batch, batch_idx, purpose):
+            self.log_dict({f"{purpose}_called": 1.0})
+            return batch_idx
+
+    torch.manual_seed(0)
+    model = NerfModel(4, 256, True, True, 2, FourierFeatures(10, 6.28), FourierFeatures(4, 1.0))
+    m = BarfLike(2.0, 8.0, model, 64)
+    assert LightningModule.inits == 1
+    assert m.training_step(None, 7) == 7 and m.logged == {"train_called": 1.0}
+    opt = m.configure_optimizers()
+    # torch Adam for host parameters, its FusedAdam subclass once the model is on the GPU
+    assert isinstance(opt["optimizer"], torch.optim.Adam) and issubclass(FusedAdam, torch.optim.Adam)
+    assert isinstance(opt["lr_scheduler"]["scheduler"], SchedulerLeNice)
+    assert [n for n, _ in m.named_parameters()][0].startswith("model_radiance.")

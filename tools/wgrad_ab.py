@@ -1,0 +1,78 @@
+"""A/B of the single-tile split-precision weight-gradient kernels (nerf_linear_wgrad_x3 for N, K
+<= 256): the register-staged kernel (NERF_WGRAD_KERNEL=0) vs the LDS-DMA streamed one (=1).
+Each run times every shape (HIP events, cold-ish inputs: a 512 MB buffer is written between
+launches) and saves dW / db; with --compare it checks the two runs' results bitwise (dW) and
+to fp32 summation order (db).
+
+    NERF_WGRAD_KERNEL=0 python tools/wgrad_ab.py --out /tmp/a.pt
+    NERF_WGRAD_KERNEL=1 python tools/wgrad_ab.py --out /tmp/b.pt --compare /tmp/a.pt
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "nerf-experiments_amd"))
+from nerf_amd import kernels as K  # noqa: E402
+
+SHAPES = [  # (M, N, [(k, row_div)])
+    (262144, 256, [(256, 1)]),
+    (524288, 256, [(256, 1)]),
+    (524288, 256, [(64, 1)]),
+    (524288, 128, [(256, 1)]),
+    (524288, 4, [(128, 1)]),
+    (524288, 128, [(128, 1), (32, 128)]),
+    (100003, 256, [(256, 1)]),
+    (1000, 256, [(256, 1)]),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--compare")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    flush = torch.empty(128 * 1024 * 1024, device=dev)
+    res = {}
+    for M, N, ks in SHAPES:
+        g = torch.Generator(device=dev).manual_seed(M + N)
+        dY = torch.randn(M, N, device=dev, generator=g)
+        segs = [((torch.randn((M + r - 1) // r, k, device=dev, generator=g)), k, r) for k, r in ks]
+        Kp = sum(K.pad32(k) for k, _ in ks)
+        ws = torch.empty((K.linear_wgrad_workspace_bytes(M, N, Kp) + 3) // 4, device=dev)
+        col_map = torch.arange(Kp, dtype=torch.int32, device=dev)
+        dW = torch.empty(N, Kp, device=dev)
+        db = torch.empty(N, device=dev)
+        ts = []
+        for it in range(12):
+            flush.fill_(float(it))
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            K.linear_wgrad_x3(dY, N, segs, M, ws)
+            e.record()
+            K.linear_wgrad_reduce(M, N, Kp, N, ws, col_map, dW, db)
+            torch.cuda.synchronize()
+            if it >= 2:
+                ts.append(s.elapsed_time(e) * 1e3)
+        ts.sort()
+        us = ts[len(ts) // 2]
+        nbytes = 4.0 * M * N + sum(4.0 * ((M + r - 1) // r) * k for k, r in ks)
+        key = f"M{M}_N{N}_" + "_".join(f"{k}r{r}" for k, r in ks)
+        print(f"{key}: {us:8.1f} us  {nbytes / us / 1e3:7.0f} GB/s", flush=True)
+        res[key] = (dW.cpu(), db.cpu())
+    torch.save(res, args.out)
+    if args.compare:
+        ref = torch.load(args.compare, weights_only=True)
+        for k, (w, b) in res.items():
+            w0, b0 = ref[k]
+            same = torch.equal(w, w0)
+            db_err = ((b - b0).abs().max() / b0.abs().max().clamp_min(1e-30)).item()
+            print(f"{k}: dW bitwise {'equal' if same else 'DIFFERENT max ' + str((w - w0).abs().max().item())}, "
+                  f"db rel {db_err:.2e}")
+            assert same and db_err < 1e-5, k
+
+
+if __name__ == "__main__":
+    main()
