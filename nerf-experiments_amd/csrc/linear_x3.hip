@@ -23,7 +23,8 @@
 // TN (weight gradient): slab[s][n][k] = sum_m dY[m][n] X[m][k]; the sample index
 // is the MFMA reduction dimension, so dY and X are staged TRANSPOSED ([n][m],
 // [k][m]): a thread loads 8 rows x 4 columns and writes four 8-sample bf16
-// vectors per plane (ds_write_b128).
+// vectors per plane (ds_write_b128).  Layers with N, K <= 256 take one 256 x 256 tile whose
+// operands stream through an LDS-DMA ring (linear_wgrad_x3_stream_kernel).
 #include "common.h"
 
 using namespace nerf;
@@ -887,172 +888,12 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
     }
 }
 
-// ------------------------------------------------------------------- TN wide
-// 256 (n) x 256 (k) weight-gradient tile per workgroup (8 waves, 2 x 4 of 128 x 64): dY and
-// X are each read from HBM once per M split (the 128 x 128 tiling reads them twice).  Both
-// operands are staged transposed through registers: a thread loads 8 samples x 2 columns
-// (8-byte loads, a wave covers 512 contiguous bytes of a row) and writes one 8-sample hi
-// and lo vector per column into the [column][32 samples hi | 32 lo] image (the 128-byte
-// row swizzle of the NT kernels; the writes of 8 consecutive threads hit 8 distinct slots).
-// Slab layout, bias-gradient slab and split policy are those of the fp32 kernel, so
-// nerf_linear_wgrad_reduce combines either.
-__global__ __launch_bounds__(512, 1) void linear_wgrad_x3_wide_kernel(TNArgs a, int npad, int kpad) {
-    constexpr int T2 = 256;
-    constexpr int IMG = T2 * 128;              // one operand image (bytes)
-    constexpr int STAGE = 2 * IMG;
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
-
-    const int ntn = (a.N + T2 - 1) / T2;
-    const int ntk = (a.X.ktot + T2 - 1) / T2;
-    const int tiles = ntn * ntk;
-    const int bid = blockIdx.x;
-    const int split = bid / tiles;
-    const int tile = bid - split * tiles;
-    const int tn = tile / ntk, tk = tile - (tile / ntk) * ntk;
-    const int n0 = tn * T2, k0 = tk * T2;
-    const int mbeg = split * a.m_per_split;
-    int mend = mbeg + a.m_per_split;
-    if (mend > a.M) mend = a.M;
-
-    const int t = threadIdx.x;
-    const int wave = t >> 6, lane = t & 63;
-    const int wr = wave >> 2, wc = wave & 3;
-    const int li = lane & 31, lh = lane >> 5;
-    const int cp = t & 127, rg = t >> 7;      // staging: columns 2cp, 2cp+1; samples 8rg .. 8rg+7
-
-    // dY columns
-    const int ycol = n0 + 2 * cp;
-    const bool y_ok = ycol < a.N;
-    const int ycl = y_ok ? ycol : 0;
-    // X columns: the segment holding packed column k0 + 2cp (segments span multiples of 32)
-    const int kx = k0 + 2 * cp;
-    int xs = -1, xoff = 0;
-#pragma unroll
-    for (int q = 0; q < MAX_SEGS; ++q)
-        if (q < a.X.n && kx >= a.X.koff[q] && kx < a.X.koff[q] + a.X.kp[q]) { xs = q; xoff = kx - a.X.koff[q]; }
-    const bool x_ok = xs >= 0 && xoff < (xs >= 0 ? pick4(a.X.k, xs) : 0);
-    const float* xptr = x_ok ? pick4(a.X.ptr, xs) : a.dY;
-    const int64_t xld = x_ok ? pick4(a.X.ld, xs) : 0;
-    const unsigned xrd = x_ok ? (unsigned)pick4(a.X.row_div, xs) : 1u;
-    const int xcl = x_ok ? xoff : 0;
-
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    f2 ry[8], rx[8];
-    unsigned mmask = 0;
-    auto gload = [&](int mc) __attribute__((always_inline)) {
-        mmask = 0;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const int m = mc + rg * 8 + r;
-            const bool mok = m < mend;
-            mmask |= (mok ? 1u : 0u) << r;
-            const unsigned mm = (unsigned)(mok ? m : mbeg);
-            ry[r] = *reinterpret_cast<const f2*>(a.dY + (int64_t)mm * a.lddy + ycl);
-            rx[r] = *reinterpret_cast<const f2*>(xptr + (int64_t)(xrd == 1u ? mm : mm / xrd) * xld + xcl);
-        }
-    };
-    f2 dbacc = f2{0.f, 0.f};
-    auto put = [&](char* img, const f2 (&v)[8], bool ok, int e) __attribute__((always_inline)) {
-        bf16x8 h, l;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const float x = (ok && ((mmask >> r) & 1u)) ? (e == 0 ? v[r].x : v[r].y) : 0.f;
-            const __bf16 hb = (__bf16)x;
-            h[r] = hb;
-            l[r] = (__bf16)(x - (float)hb);
-        }
-        const int row = 2 * cp + e;
-        *reinterpret_cast<bf16x8*>(img + swz128(row, rg)) = h;
-        *reinterpret_cast<bf16x8*>(img + swz128(row, 4 + rg)) = l;
-    };
-    auto sstore = [&](int stage) __attribute__((always_inline)) {
-        char* Yi = smem + stage * STAGE;
-        char* Xi = Yi + IMG;
-#pragma unroll
-        for (int r = 0; r < 8; ++r)
-            if (y_ok && ((mmask >> r) & 1u)) dbacc += ry[r];
-        put(Yi, ry, y_ok, 0);
-        put(Yi, ry, y_ok, 1);
-        put(Xi, rx, x_ok, 0);
-        put(Xi, rx, x_ok, 1);
-    };
-
-    f32x16 acc[4][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    // waves whose k columns lie wholly past the packed K skip the MFMAs (wave-uniform)
-    const bool active = k0 + wc * 64 < a.X.ktot && n0 + wr * 128 < a.N;
-
-    if (mbeg < mend) {
-        gload(mbeg);
-        sstore(0);
-        __syncthreads();
-        int cur = 0;
-        for (int mc = mbeg; mc < mend; mc += TBM) {
-            const bool has_next = mc + TBM < mend;
-            gload(has_next ? mc + TBM : mc);
-            __builtin_amdgcn_sched_barrier(0);
-            if (active) {
-                const char* Yb = smem + cur * STAGE;
-                const char* Xb = Yb + IMG;
-#pragma unroll
-                for (int s = 0; s < TBM / 16; ++s) {
-                    bf16x8 xh[2], xl[2];
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        const int row = wc * 64 + j * 32 + li;
-                        xh[j] = *reinterpret_cast<const bf16x8*>(Xb + swz128(row, 2 * s + lh));
-                        xl[j] = *reinterpret_cast<const bf16x8*>(Xb + swz128(row, 4 + 2 * s + lh));
-                    }
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int row = wr * 128 + i * 32 + li;
-                        const bf16x8 yh = *reinterpret_cast<const bf16x8*>(Yb + swz128(row, 2 * s + lh));
-                        const bf16x8 yl = *reinterpret_cast<const bf16x8*>(Yb + swz128(row, 4 + 2 * s + lh));
-#pragma unroll
-                        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x3(yh, yl, xh[j], xl[j], acc[i][j]);
-                    }
-                }
-            }
-            if (has_next) sstore(cur ^ 1);
-            __syncthreads();
-            cur ^= 1;
-        }
-    }
-
-    float* slab = a.slab + (size_t)split * npad * kpad;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int k = k0 + wc * 64 + j * 32 + li;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int n = n0 + wr * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                if (n < npad && k < kpad) slab[(size_t)n * kpad + k] = acc[i][j][r];
-            }
-        }
-    // bias gradient: the 4 sample groups reduce through LDS in a fixed order
-    if (tk == 0) {
-        float* dbred = reinterpret_cast<float*>(smem);   // [4][256]; the loop ended on a barrier
-        dbred[rg * T2 + 2 * cp] = dbacc.x;
-        dbred[rg * T2 + 2 * cp + 1] = dbacc.y;
-        __syncthreads();
-        if (t < T2 && n0 + t < npad)
-            a.db_slab[(size_t)split * npad + n0 + t] =
-                ((dbred[t] + dbred[T2 + t]) + dbred[2 * T2 + t]) + dbred[3 * T2 + t];
-    }
-}
-
 // ------------------------------------------------------------------- TN stream
-// The 256 x 256 weight-gradient tile (N, K <= 256: one tile per layer) with the operands
-// streamed by LDS-DMA instead of register loads.  The register-staged kernel above has 64 KB
-// per CU in flight only while its MFMAs run; the split and the transposed LDS writes then wait
-// for the loads, with nothing in flight, and the kernel reaches ~0.4 of HBM.  Here the raw fp32
+// The 256 x 256 weight-gradient tile (N, K <= 256: one tile per layer, dY and X each read from
+// HBM once per M split) with the operands streamed by LDS-DMA.  (It replaced a register-staged
+// kernel — 8-sample loads, split, transposed LDS writes — that had 64 KB per CU in flight only
+// while its MFMAs ran: 343-368 vs 326-336 us at M = 524 288, bitwise equal weight gradients;
+// tools/wgrad_ab.py.)  The raw fp32
 // rows (16 samples x 256 columns of dY and of X: 32 KB per step) land in a 3-stage ring two
 // steps ahead of the step being multiplied, so two steps (64 KB) are always in flight; the only
 // vector-memory ops in the loop are these DMAs, so the counted waits track them alone.  Each
@@ -1060,16 +901,18 @@ __global__ __launch_bounds__(512, 1) void linear_wgrad_x3_wide_kernel(TNArgs a, 
 // a wave reads 64 consecutive columns of a row), splits them into bf16 hi/lo and writes one
 // 64-byte image row [hi 0-7 | hi 8-15 | lo 0-7 | lo 8-15] (the swz layout of the 128-tile
 // kernel) while the waves multiply the other image stage.  The MFMA sequence is that of the
-// wide kernel (16-sample k-steps in sample order, lo*hi + hi*lo + hi*hi): identical slabs.  The
+// register-staged kernel (16-sample k-steps in sample order, lo*hi + hi*lo + hi*hi): identical slabs.  The
 // bias gradient is the dY thread's own column sum over the split, in sample order.
 // LDS: 3 x 32 KB ring + 2 x 32 KB images = 160 KB.
 constexpr int WS_T = 16;                        // samples per step
 constexpr int WS_RAW = 2 * WS_T * 1024;         // ring stage: dY rows then X rows, 1 KB each
 constexpr int WS_IMG = 2 * 256 * 64;            // image stage: Y rows then X rows, 64 B each
+template <int NRAW, int NIMG>
 __global__ __launch_bounds__(512, 1) void linear_wgrad_x3_stream_kernel(TNArgs a, int npad, int kpad) {
-    __shared__ __attribute__((aligned(16))) char smem[3 * WS_RAW + 2 * WS_IMG];
+    static_assert(NRAW * WS_RAW + NIMG * WS_IMG <= 160 * 1024, "LDS");
+    __shared__ __attribute__((aligned(16))) char smem[NRAW * WS_RAW + NIMG * WS_IMG];
     char* const ring = smem;
-    char* const img = smem + 3 * WS_RAW;
+    char* const img = smem + NRAW * WS_RAW;
 
     const int split = blockIdx.x;
     const int mbeg = split * a.m_per_split;
@@ -1101,7 +944,7 @@ __global__ __launch_bounds__(512, 1) void linear_wgrad_x3_stream_kernel(TNArgs a
     const unsigned dxrd = dx_ok ? (unsigned)pick4(a.X.row_div, dxs) : (unsigned)a.X.row_div[0];
     // wave w brings rows 2w, 2w + 1 of both operands
     auto issue = [&](int step) __attribute__((always_inline)) {
-        char* st = ring + (step % 3) * WS_RAW;
+        char* st = ring + (step % NRAW) * WS_RAW;
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int r = 2 * wave + q;
@@ -1126,23 +969,25 @@ __global__ __launch_bounds__(512, 1) void linear_wgrad_x3_stream_kernel(TNArgs a
         c_ok = xs >= 0 && xoff < pick4(a.X.k, xs);
     }
     float db = 0.f;
-    auto convert = [&](int step) __attribute__((always_inline)) {
-        const float* src = reinterpret_cast<const float*>(ring + (step % 3) * WS_RAW + op * WS_T * 1024) + c;
-        __bf16* dst = reinterpret_cast<__bf16*>(img + (step & 1) * WS_IMG + op * 256 * 64);
-        const int valid = mend - (mbeg + step * WS_T);      // rows of this step inside the split
-        // every row is read (the ring rows past the split hold finite data) and masked after, so
-        // the reads issue back to back (a select per read becomes a branch around it)
-        float v[WS_T];
+    // the conversion in two halves, so that a step's ring reads can be issued ahead of the MFMAs
+    // and its split / image writes scheduled between them (one basic block: no branch inside);
+    // past the last step it converts stale ring rows into an image stage nobody reads again, all
+    // masked to zero (no bias-gradient contribution).  db accumulates in every thread, only the
+    // dY threads' sums are written.
+    auto conv_load = [&](int step, float (&v)[WS_T]) __attribute__((always_inline)) {
+        const float* src = reinterpret_cast<const float*>(ring + (step % NRAW) * WS_RAW + op * WS_T * 1024) + c;
 #pragma unroll
         for (int r = 0; r < WS_T; ++r) v[r] = src[r * 256];
+    };
+    auto conv_store = [&](int step, float (&v)[WS_T]) __attribute__((always_inline)) {
+        __bf16* dst = reinterpret_cast<__bf16*>(img + (step % NIMG) * WS_IMG + op * 256 * 64);
+        const int valid = mend - (mbeg + step * WS_T);      // rows of this step inside the split
         const unsigned cm = c_ok ? ~0u : 0u;
 #pragma unroll
         for (int r = 0; r < WS_T; ++r)
             v[r] = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, v[r]) & (r < valid ? cm : 0u));
-        if (op == 0) {
 #pragma unroll
-            for (int r = 0; r < WS_T; ++r) db += v[r];
-        }
+        for (int r = 0; r < WS_T; ++r) db += v[r];
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
             bf16x8 h, l;
@@ -1156,6 +1001,11 @@ __global__ __launch_bounds__(512, 1) void linear_wgrad_x3_stream_kernel(TNArgs a
             *reinterpret_cast<bf16x8*>(dst + swz(c, hh)) = h;
             *reinterpret_cast<bf16x8*>(dst + swz(c, 2 + hh)) = l;
         }
+    };
+    auto convert = [&](int step) __attribute__((always_inline)) {
+        float v[WS_T];
+        conv_load(step, v);
+        conv_store(step, v);
     };
     auto barrier = []() __attribute__((always_inline)) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1173,51 +1023,60 @@ __global__ __launch_bounds__(512, 1) void linear_wgrad_x3_stream_kernel(TNArgs a
     // waves whose k columns lie wholly past the packed K skip the MFMAs (wave-uniform)
     const bool active = wc * 64 < a.X.ktot && wr * 128 < a.N;
 
-    if (steps > 0) {
-        // prologue: steps 0 and 1 in flight; step 0 converted; step 2 issued; step 1 landed
-        issue(0);
-        if (steps > 1) {
-            issue(1);
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // wait until at most `ahead` steps' DMAs (4 per wave each) are outstanding
+    auto wait_dma = [](int ahead) __attribute__((always_inline)) {
+        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    auto mfma_step = [&](int i) __attribute__((always_inline)) {
+        const __bf16* Yb = reinterpret_cast<const __bf16*>(img + (i % NIMG) * WS_IMG);
+        const __bf16* Xb = Yb + 256 * 32;
+        bf16x8 xh[2], xl[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int row = wc * 64 + j * 32 + li;
+            xh[j] = *reinterpret_cast<const bf16x8*>(Xb + swz(row, lh));
+            xl[j] = *reinterpret_cast<const bf16x8*>(Xb + swz(row, 2 + lh));
         }
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+            const int row = wr * 128 + ii * 32 + li;
+            const bf16x8 yh = *reinterpret_cast<const bf16x8*>(Yb + swz(row, lh));
+            const bf16x8 yl = *reinterpret_cast<const bf16x8*>(Yb + swz(row, 2 + lh));
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[ii][j] = mfma_x3(yh, yl, xh[j], xl[j], acc[ii][j]);
+        }
+    };
+    if (steps > 0) {
+        // prologue: steps 0 .. NRAW-1 issued, step 0 converted, step 1 landed
+        for (int q = 0; q < NRAW - 1 && q < steps; ++q) issue(q);
+        wait_dma(min(steps, NRAW - 1) - 1);
         barrier();
         convert(0);
-        if (steps > 2) {
-            issue(2);
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        if (NRAW - 1 < steps) issue(NRAW - 1);
+        wait_dma(min(steps, NRAW) - 2);
         barrier();
         for (int i = 0; i < steps; ++i) {
-            if (active) {
-                const __bf16* Yb = reinterpret_cast<const __bf16*>(img + (i & 1) * WS_IMG);
-                const __bf16* Xb = Yb + 256 * 32;
-                bf16x8 xh[2], xl[2];
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int row = wc * 64 + j * 32 + li;
-                    xh[j] = *reinterpret_cast<const bf16x8*>(Xb + swz(row, lh));
-                    xl[j] = *reinterpret_cast<const bf16x8*>(Xb + swz(row, 2 + lh));
+            // NIMG = 2: step i + 1's conversion overlaps step i's MFMAs (other image stage)
+            if (NIMG == 2) {
+                if (active) {
+                    float v[WS_T];
+                    conv_load(i + 1, v);
+                    mfma_step(i);
+                    conv_store(i + 1, v);
+                } else {
+                    convert(i + 1);
                 }
-#pragma unroll
-                for (int ii = 0; ii < 4; ++ii) {
-                    const int row = wr * 128 + ii * 32 + li;
-                    const bf16x8 yh = *reinterpret_cast<const bf16x8*>(Yb + swz(row, lh));
-                    const bf16x8 yl = *reinterpret_cast<const bf16x8*>(Yb + swz(row, 2 + lh));
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) acc[ii][j] = mfma_x3(yh, yl, xh[j], xl[j], acc[ii][j]);
-                }
-            }
-            if (i + 1 < steps) convert(i + 1);
-            if (i + 3 < steps) {
-                issue(i + 3);                                   // into the stage step i held
-                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // step i + 2 landed
             } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (active) mfma_step(i);
+                barrier();                                  // the single image stage is free
+                convert(i + 1);
             }
+            // the stage step i held was converted before the previous barrier
+            if (i + NRAW < steps) issue(i + NRAW);
+            // step i + 2 landed (it is converted in the next iteration)
+            wait_dma(min(steps - 1, i + NRAW) - (i + 2));
             barrier();
         }
     }
@@ -1447,13 +1306,8 @@ extern "C" int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N, c
     TNArgs a{dY, ld_dy, N, L, (int)M, (int)mps, splits, slab, db_slab};
     if ((N > 128 || L.ktot > 128) && N <= 256 && L.ktot <= 256) {   // one 256 x 256 tile covers the layer
         const int64_t blocks = (int64_t)splits * ((N + 255) / 256) * ((L.ktot + 255) / 256);
-        static const int kern = [] { const char* e = getenv("NERF_WGRAD_KERNEL"); return e ? atoi(e) : 0; }();
-        if (kern == 1)
-            hipLaunchKernelGGL(linear_wgrad_x3_stream_kernel, dim3((unsigned)blocks), dim3(512), 0, as_stream(stream),
-                               a, ntn * TB, ntk * TB);
-        else
-            hipLaunchKernelGGL(linear_wgrad_x3_wide_kernel, dim3((unsigned)blocks), dim3(512), 0, as_stream(stream), a,
-                               ntn * TB, ntk * TB);
+        hipLaunchKernelGGL((linear_wgrad_x3_stream_kernel<3, 2>), dim3((unsigned)blocks), dim3(512), 0,
+                           as_stream(stream), a, ntn * TB, ntk * TB);
         NERF_CHECK_LAUNCH();
         return NERF_OK;
     }

@@ -1,11 +1,11 @@
-"""A/B of the single-tile split-precision weight-gradient kernels (nerf_linear_wgrad_x3 for N, K
-<= 256): the register-staged kernel (NERF_WGRAD_KERNEL=0) vs the LDS-DMA streamed one (=1).
-Each run times every shape (HIP events, cold-ish inputs: a 512 MB buffer is written between
-launches) and saves dW / db; with --compare it checks the two runs' results bitwise (dW) and
-to fp32 summation order (db).
+"""Times the split-precision weight gradient (nerf_linear_wgrad_x3 + reduce) per layer shape
+(HIP events, cold-ish inputs: a 512 MB buffer is written between launches) and saves dW / db;
+with --compare it checks two builds' results bitwise (dW) and to fp32 summation order (db) —
+how the LDS-DMA streamed single-tile kernel was A/B'd against the register-staged one it
+replaced.
 
-    NERF_WGRAD_KERNEL=0 python tools/wgrad_ab.py --out /tmp/a.pt
-    NERF_WGRAD_KERNEL=1 python tools/wgrad_ab.py --out /tmp/b.pt --compare /tmp/a.pt
+    python tools/wgrad_ab.py --out /tmp/a.pt          # build A
+    python tools/wgrad_ab.py --out /tmp/b.pt --compare /tmp/a.pt   # build B
 """
 import argparse
 import os
