@@ -455,7 +455,7 @@ def _roofline(ks_fn: dict, x3: bool, steps: int, workload: str):
     # HIP kernel functions as rocprofv3 names them (template instantiations separately: the fused
     # kernel's forward is mlp_fused_kernel<0>, its input-gradient chain mlp_fused_kernel<1>)
     mfma_fns = ("mlp_fused_kernel<0>", "mlp_fused_kernel<1>", "linear_nt_x3_glds_kernel", "linear_nt_x3_kernel",
-                "linear_wgrad_x3_wide_kernel", "linear_wgrad_x3_kernel", "linear_nt_kernel", "linear_wgrad_kernel")
+                "linear_wgrad_x3_stream_kernel<3, 2>", "linear_wgrad_x3_kernel", "linear_nt_kernel", "linear_wgrad_kernel")
     cands = [k for k in mfma_fns if k in ks_fn]
     if not cands:
         return None
@@ -496,6 +496,56 @@ def _roofline(ks_fn: dict, x3: bool, steps: int, workload: str):
             "avg_bytes_per_launch": avg_bytes, "launches_per_step": r["launches"] / steps,
             "share_of_timed_kernel_time": r["ms"] / total_ms if total_ms > 0 else None,
             "pmc": pmc}
+
+
+def frame_roofline(ren, wl: dict, device, H: int = 800, W: int = 800, reps: int = 3):
+    """HBM roofline of the same positional-encoding and compositing kernels at ONE full-frame
+    launch: H*W rays (800 x 800: the C3 view size) x the workload's coarse and fine sample counts,
+    the size a full-view render hands them on a 288 GB GPU (the training batch is 4096 rays: a
+    latency-bound 6-20 MB per compositing launch).  Same kernel parameters as the step (the
+    model's own encoders; density factors and fused activations of its renderer); synthetic
+    rays and raw heads; untimed warm-up, then `reps` event-timed launches each."""
+    from nerf_amd import kernels as K
+    from nerf_amd.positional_encodings import PositionalEncoding
+    model = getattr(ren, "model_radiance", None)
+    enc = getattr(model, "position_encoder", None)
+    if not isinstance(enc, PositionalEncoding):
+        return None                                   # hash grid (ingp) / garf: no PE kernel
+    B = H * W
+    g = torch.Generator(device=device).manual_seed(7)
+    o = torch.randn(B, 3, device=device, generator=g) * 0.1 + torch.tensor([0.0, 0.0, 4.0], device=device)
+    d = torch.nn.functional.normalize(torch.randn(B, 3, device=device, generator=g) * 0.2
+                                      - torch.tensor([0.0, 0.0, 1.0], device=device), dim=1)
+    pw = torch.full((B,), 1 / 1111.1, device=device)
+    sa, sb = ren.density_factor
+    counts = sorted({wl["coarse"], wl["fine"]} - {0})
+    timer, prev = K.KernelTimer(), K.TIMER
+    with torch.no_grad():
+        for S in counts:
+            t = torch.linspace(ren.near_sphere_normalized, ren.far_sphere_normalized, S + 1, device=device)
+            t0, t1 = t[:-1].expand(B, S).contiguous(), t[1:].expand(B, S).contiguous()
+            dist = t1 - t0
+            dens = torch.randn(B * S, device=device, generator=g)
+            col = torch.randn(B * S, 4, device=device, generator=g)
+            g_rgb = torch.randn(B, 3, device=device, generator=g)
+            gd, gc = torch.empty_like(dens), torch.empty_like(col)
+            for rep in range(reps + 1):
+                K.TIMER = timer if rep > 0 else None
+                enc.encode_rays(o, d, t0, t1, pw, S, 1, 1)
+                K.composite_fwd(dens, 1, col, 4, dist, B, S, sa, sb, True, 0.0)
+                K.composite_bwd(dens, 1, col, 4, dist, B, S, sa, sb, True, 0.0, g_rgb, None, gd, 1, gc, 4)
+            K.TIMER = prev
+            del t0, t1, dist, dens, col, gd, gc
+    torch.cuda.synchronize()
+    ks = timer.summary()
+    per = {k: {"gbs": v["bytes"] / (v["ms"] * 1e-3) / 1e9, "us_per_launch": v["ms"] * 1e3 / v["launches"],
+               "bytes_per_launch": v["bytes"] / v["launches"]} for k, v in ks.items()}
+    nb, ms = sum(v["bytes"] for v in ks.values()), sum(v["ms"] for v in ks.values())
+    gbs = nb / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    return {"kernel": "encode_fwd + composite_fwd + composite_bwd, one launch per full %dx%d frame "
+                      "(%d rays x %s samples; algorithmic bytes per launch)" % (H, W, B, "/".join(map(str, counts))),
+            "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+            "per_kernel": per}
 
 
 def init_distributed(backend: str = "nccl"):
@@ -560,6 +610,8 @@ def main():
                     help="device: every step draws a fresh shuffled batch from 100 synthetic views through "
                          "the on-device ray feed (nerf_ray_batch); fixed: one resident batch reused")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-frame-roofline", action="store_true",
+                    help="skip the full-frame launch measurement of the PE / compositing kernels")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--matmul-precision", default="high", choices=("highest", "high", "medium"),
                     help="torch.set_float32_matmul_precision for the MLP GEMMs: highest = fp32 MFMA, "
@@ -664,6 +716,11 @@ def main():
                                    / (elapsed / args.steps) / 1e12,
             ("mean_rgb" if render else "final_loss"): final_loss,
         }
+        if world == 1 and not args.no_frame_roofline:
+            try:          # an auxiliary measurement: its failure must not cost the bench line
+                out["roofline_hbm_frame"] = frame_roofline(ren, wl, device)
+            except Exception as e:      # noqa: BLE001
+                out["roofline_hbm_frame"] = {"error": f"{type(e).__name__}: {e}"}
         if world == 1 and not args.no_cpu_baseline and not render:
             cb = cpu_baseline(args.workload, args.cpu_seconds)
             if cb is not None:
