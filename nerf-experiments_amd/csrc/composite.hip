@@ -6,11 +6,15 @@
 //   alpha_int    = [1, exp(cumsum(blocking_neg[:, :-1]))]
 //   weights      = alpha_int * alpha;  rgb = sum(weights[..., None] * colors, 1)
 //
-// Design: one 64-lane wavefront per ray; lane l owns R consecutive samples
-// s = l*R + r.  The exclusive prefix of b is a per-lane serial scan plus a
-// wave shuffle scan, both in fp64 (torch's CPU cumsum accumulates fp32 input
-// in double, which is what the reference's CPU path computes).  No LDS, no
-// atomics; HBM traffic = the algorithmic bytes (sigma, rgb, delta in; w, rgb out).
+// Design: one 64-lane wavefront per ray; lane l owns the R samples s = 64 r + l,
+// so every load and store instruction covers 64 consecutive samples (256 B of a
+// per-sample scalar, 1 KB of 16-byte colour rows: the round-1 layout, R consecutive
+// samples per lane, touched 8x the cache lines per instruction and streamed at
+// 2.6 TB/s on a full 800x800 frame).  The exclusive prefix of b is one fp64 wave
+// scan per 64-sample segment plus the running segment total (torch's CPU cumsum
+// accumulates fp32 input in double, which is what the reference's CPU path
+// computes).  No LDS, no atomics; HBM traffic = the algorithmic bytes (sigma,
+// rgb, delta in; w, rgb out).
 #include "common.h"
 
 using namespace nerf;
@@ -31,13 +35,14 @@ constexpr bool prefetch_rays(int R) { return R <= 2; }
 constexpr int64_t kMaxBlocks = 2048;  // 256 CUs x 32 waves / 4 waves per block
 
 // One ray's samples into registers: raw density, interval length, raw colour (zeros past S).
-template <int R, bool PK>
+// PK: [rgb | sigma] rows; C4: colour rows of stride 4, 16-byte aligned (one dwordx4 each).
+template <int R, bool PK, bool C4>
 __device__ __forceinline__ void load_samples(const CompositeArgs& a, int64_t ray, int lane, float (&rd)[R],
                                              float (&del)[R], float (&rc)[R][3]) {
     const int64_t base = ray * a.S;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int s = lane * R + r;
+        const int s = r * NERF_WAVE + lane;
         rd[r] = 0.f; del[r] = 0.f;
         rc[r][0] = rc[r][1] = rc[r][2] = 0.f;
         if (s < a.S) {
@@ -48,59 +53,52 @@ __device__ __forceinline__ void load_samples(const CompositeArgs& a, int64_t ray
                 rc[r][0] = v.x; rc[r][1] = v.y; rc[r][2] = v.z; rd[r] = v.w;
             } else {
                 rd[r] = a.density[n * a.ds];
-                const float* cp = a.color + n * a.cs;
-                rc[r][0] = cp[0]; rc[r][1] = cp[1]; rc[r][2] = cp[2];
+                if (C4) {
+                    const float4 v = *reinterpret_cast<const float4*>(a.color + n * 4);
+                    rc[r][0] = v.x; rc[r][1] = v.y; rc[r][2] = v.z;
+                } else {
+                    const float* cp = a.color + n * a.cs;
+                    rc[r][0] = cp[0]; rc[r][1] = cp[1]; rc[r][2] = cp[2];
+                }
             }
         }
     }
 }
 
-template <int R, bool PK>
+template <int R>
 __device__ __forceinline__ void composite_fwd_ray(const CompositeArgs& a, int64_t ray, int lane, const float (&rd)[R],
                                                   const float (&del)[R], const float (&rc)[R][3],
                                                   float* __restrict__ rgb_out, float* __restrict__ w_out) {
 #pragma clang fp contract(off)
     const int64_t base = ray * a.S;
-
-    float b[R], e[R], c[R][3];
-    double pre[R];
-    double run = 0.0;
+    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
+    double carry = 0.0;            // sum of b over the previous 64-sample segments
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int s = lane * R + r;
+        const int s = r * NERF_WAVE + lane;
         float sig = rd[r];
-        c[r][0] = rc[r][0]; c[r][1] = rc[r][1]; c[r][2] = rc[r][2];
+        float c0 = rc[r][0], c1 = rc[r][1], c2 = rc[r][2];
         if (a.act && s < a.S) {
             sig = softplus_thr8(sig - a.shift);
-            c[r][0] = sigmoidf_(c[r][0]);
-            c[r][1] = sigmoidf_(c[r][1]);
-            c[r][2] = sigmoidf_(c[r][2]);
+            c0 = sigmoidf_(c0);
+            c1 = sigmoidf_(c1);
+            c2 = sigmoidf_(c2);
         }
         // ((-sigma * delta) * 3) * MAGIC — two fp32 multiplies, as the reference.
         float bb = ((-sig) * del[r]) * a.sa;
         bb = bb * a.sb;
         if (s >= a.S) bb = 0.f;
-        b[r] = bb;
-        e[r] = expf(bb);
-        pre[r] = run;            // exclusive within lane
-        run += (double)bb;
-    }
-    const double incl = wave_inclusive_scan(run);
-    const double lane_off = incl - run;
-
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int s = lane * R + r;
-        const double ex = lane_off + pre[r];
+        const double incl = wave_inclusive_scan((double)bb);
+        const double ex = carry + (incl - (double)bb);      // exclusive prefix
+        carry += __shfl(incl, NERF_WAVE - 1, NERF_WAVE);
         const float T = (s == 0) ? 1.0f : expf((float)ex);
-        const float alpha = 1.0f - e[r];
+        const float alpha = 1.0f - expf(bb);
         const float w = T * alpha;
         if (s < a.S) {
             if (w_out) w_out[base + s] = w;
-            acc0 += w * c[r][0];
-            acc1 += w * c[r][1];
-            acc2 += w * c[r][2];
+            acc0 += w * c0;
+            acc1 += w * c1;
+            acc2 += w * c2;
         }
     }
     acc0 = wave_sum_f(acc0);
@@ -116,24 +114,24 @@ __device__ __forceinline__ void composite_fwd_ray(const CompositeArgs& a, int64_
 // Each wave walks rays ray, ray + 4*gridDim.x, ... and loads the next ray's samples before
 // compositing the current one, so the loads of one ray overlap the scan of the previous one
 // (prefetch_rays; otherwise one ray per wave, as the grid is not capped).
-template <int R, bool PK>
+template <int R, bool PK, bool C4>
 __global__ __launch_bounds__(256) void composite_fwd_kernel(CompositeArgs a, float* __restrict__ rgb_out,
                                                             float* __restrict__ w_out) {
     const int lane = lane_id();
     int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (ray >= a.n_rays) return;
     float rd[R], del[R], rc[R][3];
-    load_samples<R, PK>(a, ray, lane, rd, del, rc);
+    load_samples<R, PK, C4>(a, ray, lane, rd, del, rc);
     if constexpr (!prefetch_rays(R)) {
-        composite_fwd_ray<R, PK>(a, ray, lane, rd, del, rc, rgb_out, w_out);
+        composite_fwd_ray<R>(a, ray, lane, rd, del, rc, rgb_out, w_out);
     } else {
         const int64_t step = (int64_t)gridDim.x * 4;
         for (;;) {
             const int64_t next = ray + step;
             const bool more = next < a.n_rays;
             float nd[R], ndel[R], nc[R][3];
-            load_samples<R, PK>(a, more ? next : ray, lane, nd, ndel, nc);
-            composite_fwd_ray<R, PK>(a, ray, lane, rd, del, rc, rgb_out, w_out);
+            load_samples<R, PK, C4>(a, more ? next : ray, lane, nd, ndel, nc);
+            composite_fwd_ray<R>(a, ray, lane, rd, del, rc, rgb_out, w_out);
             if (!more) break;
             ray = next;
             for (int r = 0; r < R; ++r) {  // R <= 2: unrolled by the compiler
@@ -148,7 +146,7 @@ __global__ __launch_bounds__(256) void composite_fwd_kernel(CompositeArgs a, flo
 //   dL/db_k = -g_w(k) * T_k * exp(b_k) + sum_{i>k} g_w(i) * w_i
 //   dL/dsigma_k = dL/db_k * (-(delta_k) * sa * sb) ;  dL/dc_k = w_k * g_rgb
 // Same ray walk and next-ray prefetch as the forward.
-template <int R, bool PK, bool PKG>
+template <int R, bool PKG>
 __device__ __forceinline__ void composite_bwd_ray(const CompositeArgs& a, int64_t ray, int lane, const float (&rawd)[R],
                                                   const float (&del)[R], const float (&rawc)[R][3], float g0,
                                                   float g1, float g2, const float* __restrict__ g_w,
@@ -157,39 +155,30 @@ __device__ __forceinline__ void composite_bwd_ray(const CompositeArgs& a, int64_
 #pragma clang fp contract(off)
     const int64_t base = ray * a.S;
 
-    float sig[R], c[R][3], b[R], e[R];
-    double pre[R];
-    double run = 0.0;
+    float c[R][3], T[R], w[R], e[R], gw[R];
+    double qincl[R];               // inclusive prefix of q = g_w * w over the ray, in sample order
+    double carry = 0.0, qcarry = 0.0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int s = lane * R + r;
+        const int s = r * NERF_WAVE + lane;
+        float sig;
         if (a.act) {
-            sig[r] = softplus_thr8(rawd[r] - a.shift);
+            sig = softplus_thr8(rawd[r] - a.shift);
             c[r][0] = sigmoidf_(rawc[r][0]);
             c[r][1] = sigmoidf_(rawc[r][1]);
             c[r][2] = sigmoidf_(rawc[r][2]);
         } else {
-            sig[r] = rawd[r];
+            sig = rawd[r];
             c[r][0] = rawc[r][0]; c[r][1] = rawc[r][1]; c[r][2] = rawc[r][2];
         }
-        float bb = ((-sig[r]) * del[r]) * a.sa;
+        float bb = ((-sig) * del[r]) * a.sa;
         bb = bb * a.sb;
         if (s >= a.S) bb = 0.f;
-        b[r] = bb;
         e[r] = expf(bb);
-        pre[r] = run;
-        run += (double)bb;
-    }
-    const double incl = wave_inclusive_scan(run);
-    const double lane_off = incl - run;
-
-    float T[R], w[R], gw[R];
-    double q[R];
-    double qrun = 0.0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int s = lane * R + r;
-        T[r] = (s == 0) ? 1.0f : expf((float)(lane_off + pre[r]));
+        const double incl = wave_inclusive_scan((double)bb);
+        const double ex = carry + (incl - (double)bb);
+        carry += __shfl(incl, NERF_WAVE - 1, NERF_WAVE);
+        T[r] = (s == 0) ? 1.0f : expf((float)ex);
         w[r] = T[r] * (1.0f - e[r]);
         float gwr = 0.f;
         if (s < a.S) {
@@ -197,19 +186,17 @@ __device__ __forceinline__ void composite_bwd_ray(const CompositeArgs& a, int64_
             if (g_w) gwr += g_w[base + s];
         }
         gw[r] = gwr;
-        q[r] = (double)gwr * (double)w[r];
-        qrun += q[r];
+        const double qi = wave_inclusive_scan((double)gwr * (double)w[r]);
+        qincl[r] = qcarry + qi;
+        qcarry += __shfl(qi, NERF_WAVE - 1, NERF_WAVE);
     }
     // suffix sums: sum_{i>k} q_i = total - inclusive_prefix(k)
-    const double qincl = wave_inclusive_scan(qrun);
-    const double qtotal = __shfl(qincl, NERF_WAVE - 1, NERF_WAVE);
-    double qpre = qincl - qrun;  // exclusive lane offset
+    const double qtotal = qcarry;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int s = lane * R + r;
-        qpre += q[r];
-        const double suffix = qtotal - qpre;
+        const int s = r * NERF_WAVE + lane;
         if (s >= a.S) continue;
+        const double suffix = qtotal - qincl[r];
         const int64_t n = base + s;
         const float dldb = (float)((double)(-gw[r] * T[r] * e[r]) + suffix);
         float dsig = 0.f;
@@ -235,7 +222,7 @@ __device__ __forceinline__ void composite_bwd_ray(const CompositeArgs& a, int64_
     }
 }
 
-template <int R, bool PK, bool PKG>
+template <int R, bool PK, bool C4, bool PKG>
 __global__ __launch_bounds__(256) void composite_bwd_kernel(CompositeArgs a, const float* __restrict__ g_rgb,
                                                             const float* __restrict__ g_w,
                                                             float* __restrict__ gd, int64_t gds,
@@ -244,10 +231,10 @@ __global__ __launch_bounds__(256) void composite_bwd_kernel(CompositeArgs a, con
     int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (ray >= a.n_rays) return;
     float rawd[R], del[R], rawc[R][3];
-    load_samples<R, PK>(a, ray, lane, rawd, del, rawc);
+    load_samples<R, PK, C4>(a, ray, lane, rawd, del, rawc);
     float g0 = g_rgb[ray * 3 + 0], g1 = g_rgb[ray * 3 + 1], g2 = g_rgb[ray * 3 + 2];
     if constexpr (!prefetch_rays(R)) {
-        composite_bwd_ray<R, PK, PKG>(a, ray, lane, rawd, del, rawc, g0, g1, g2, g_w, gd, gds, gc, gcs);
+        composite_bwd_ray<R, PKG>(a, ray, lane, rawd, del, rawc, g0, g1, g2, g_w, gd, gds, gc, gcs);
     } else {
         const int64_t step = (int64_t)gridDim.x * 4;
         for (;;) {
@@ -255,9 +242,9 @@ __global__ __launch_bounds__(256) void composite_bwd_kernel(CompositeArgs a, con
             const bool more = next < a.n_rays;
             const int64_t pf = more ? next : ray;
             float nd[R], ndel[R], nc[R][3];
-            load_samples<R, PK>(a, pf, lane, nd, ndel, nc);
+            load_samples<R, PK, C4>(a, pf, lane, nd, ndel, nc);
             const float ng0 = g_rgb[pf * 3 + 0], ng1 = g_rgb[pf * 3 + 1], ng2 = g_rgb[pf * 3 + 2];
-            composite_bwd_ray<R, PK, PKG>(a, ray, lane, rawd, del, rawc, g0, g1, g2, g_w, gd, gds, gc, gcs);
+            composite_bwd_ray<R, PKG>(a, ray, lane, rawd, del, rawc, g0, g1, g2, g_w, gd, gds, gc, gcs);
             if (!more) break;
             ray = next;
             g0 = ng0; g1 = ng1; g2 = ng2;
@@ -301,9 +288,11 @@ extern "C" int nerf_composite_fwd(const float* density, int64_t density_stride, 
     if (R <= 2) grid.x = (unsigned)std::min<int64_t>(grid.x, kMaxBlocks);
     hipStream_t st = as_stream(stream);
     const bool pk = packed_rows(density, density_stride, color, color_stride);
+    const bool c4 = !pk && color_stride == 4 && aligned16(color);
     switch (R) {
-#define CASE(RR) case RR: if (pk) hipLaunchKernelGGL((composite_fwd_kernel<RR, true>), grid, block, 0, st, a, rgb_out, weights_out); \
-                          else hipLaunchKernelGGL((composite_fwd_kernel<RR, false>), grid, block, 0, st, a, rgb_out, weights_out); break;
+#define CASE(RR) case RR: if (pk) hipLaunchKernelGGL((composite_fwd_kernel<RR, true, false>), grid, block, 0, st, a, rgb_out, weights_out); \
+                          else if (c4) hipLaunchKernelGGL((composite_fwd_kernel<RR, false, true>), grid, block, 0, st, a, rgb_out, weights_out); \
+                          else hipLaunchKernelGGL((composite_fwd_kernel<RR, false, false>), grid, block, 0, st, a, rgb_out, weights_out); break;
         CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(8) CASE(16)
 #undef CASE
         default: return NERF_ERR_UNSUPPORTED;
@@ -330,10 +319,12 @@ extern "C" int nerf_composite_bwd(const float* density, int64_t density_stride, 
     hipStream_t st = as_stream(stream);
     const bool pk = packed_rows(density, density_stride, color, color_stride);
     const bool pkg = packed_rows(grad_density, gd_stride, grad_color, gc_stride);
+    const bool c4 = !pk && color_stride == 4 && aligned16(color);
     switch (R) {
-#define LAUNCH(RR, P, PG) hipLaunchKernelGGL((composite_bwd_kernel<RR, P, PG>), grid, block, 0, st, a, grad_rgb, grad_weights, grad_density, gd_stride, grad_color, gc_stride)
-#define CASE(RR) case RR: if (pk && pkg) LAUNCH(RR, true, true); else if (pk) LAUNCH(RR, true, false); \
-                          else if (pkg) LAUNCH(RR, false, true); else LAUNCH(RR, false, false); break;
+#define LAUNCH(RR, P, C, PG) hipLaunchKernelGGL((composite_bwd_kernel<RR, P, C, PG>), grid, block, 0, st, a, grad_rgb, grad_weights, grad_density, gd_stride, grad_color, gc_stride)
+#define CASE(RR) case RR: if (pk && pkg) LAUNCH(RR, true, false, true); else if (pk) LAUNCH(RR, true, false, false); \
+                          else if (c4 && pkg) LAUNCH(RR, false, true, true); else if (c4) LAUNCH(RR, false, true, false); \
+                          else if (pkg) LAUNCH(RR, false, false, true); else LAUNCH(RR, false, false, false); break;
         CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(8) CASE(16)
 #undef CASE
 #undef LAUNCH
