@@ -459,7 +459,7 @@ def linear_wgrad_x3(dY: torch.Tensor, N4: int, segs, M: int, workspace: torch.Te
     kpad = sum(pad32(k) for _, k, _ in segs)
     wide = (N4 > 128 or kpad > 128) and N4 <= 256 and kpad <= 256
     end = TIMER.bracket("linear_wgrad_x3", 2.0 * M * N4 * kt, 4.0 * M * N4 + _segs_bytes(segs, M) + 4.0 * N4 * kt,
-                        fn="linear_wgrad_x3_stream_kernel<3, 2>" if wide else "linear_wgrad_x3_kernel") \
+                        fn="linear_wgrad_x3_stream_kernel" if wide else "linear_wgrad_x3_kernel") \
         if TIMER is not None else None
     st = _lib.load().nerf_linear_wgrad_x3(_ptr(dY), dY.stride(0), N4, arr, len(segs), M, _ptr(workspace),
                                           workspace.numel() * workspace.element_size(), _stream(dY.device))
