@@ -7,7 +7,7 @@ OUT=${1:?outdir}; shift
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run --output-format csv \
-  -- python3 bench.py --no-cpu-baseline --steps 50 --warmup 10 "$@" > "$OUT/stats.log" 2>&1 \
+  -- python3 bench.py --no-cpu-baseline --no-frame-roofline --steps 50 --warmup 10 "$@" > "$OUT/stats.log" 2>&1 \
   || { echo "stats pass failed"; exit 1; }
 i=0
 for group in "FETCH_SIZE" "WRITE_SIZE" \
@@ -15,7 +15,7 @@ for group in "FETCH_SIZE" "WRITE_SIZE" \
              "SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS"; do
   i=$((i+1))
   timeout -s KILL 180 rocprofv3 --kernel-trace --pmc $group -d "$OUT/bench_p$i" -o run --output-format csv \
-    -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 "$@" > "$OUT/bench_p$i.log" 2>&1 \
+    -- python3 bench.py --no-cpu-baseline --no-frame-roofline --steps 5 --warmup 2 "$@" > "$OUT/bench_p$i.log" 2>&1 \
     || { echo "pmc pass $i failed"; exit 1; }
 done
 echo done
