@@ -106,6 +106,13 @@ int nerf_sample_uniform(int64_t n_rays, int32_t samples_per_ray, float near_, fl
  * equidistant sampling with a per-ray offset of -U_r * D (model_interpolation.py:274-275),
  * using (seed, counter) for U_r.  status (device int32, caller-zeroed) gets
  * bit 0 set in that case.
+ * mode 2 (nerf-siren/model.py:106-112, _sample_t_fine(linspace=False); the multinomial
+ *   branch of 3d-ingp/model.py:306-312): n_fine = n_samples - n_bins bins drawn with
+ *   replacement with probability w_i / sum w (inverse of the fp64 cumulative weights at
+ *   U_j * sum, U_j = Philox(seed, counter, ray * n_fine + j)), t = t_coarse[bin] +
+ *   U'_j * dist[bin] (U' from counter ^ 2^62), concatenated with t_coarse and sorted
+ *   ascending (stable).  n_samples <= 512.  A row torch.multinomial would reject (negative /
+ *   non-finite weight, zero sum) draws its bins uniformly and sets bit 1 of status.
  * ------------------------------------------------------------------------- */
 int nerf_resample_pdf(const float* t_coarse, const float* weights, const float* dist_coarse,
                       int64_t n_rays, int32_t n_bins, int32_t n_samples, int32_t mode,

@@ -6,6 +6,8 @@
 //   _get_intervals                barf/model_interpolation.py:114-132
 //   _sample_t_pdf_weighted        barf/model_interpolation.py:193-277 (mode 0)
 //   _sample_t_fine                naive-to-vanilla/model_interpolation.py:128-169 (mode 1)
+//   _sample_t_fine(linspace=False) nerf-siren/model.py:106-112 (mode 2; the multinomial branch
+//                                  SURVEY §8(a) a5 names at 3d-ingp/model.py:306-312)
 //
 // Resample design: one wavefront per ray, lane i = coarse bin i (n_bins <= 64).
 // The integer allocation (floor / largest remainder / +1) is done in registers,
@@ -140,6 +142,75 @@ __global__ __launch_bounds__(256) void resample_kernel(ResampleArgs a) {
     }
 }
 
+// Mode 2, torch.multinomial(weights, n_fine, replacement=True) -> t_coarse.gather + U * dist.gather
+// -> cat with t_coarse -> sort (nerf-siren/model.py:106-112): one wave per ray.  Bin of fine
+// sample j: the inverse of the fp64 cumulative weights at u_j * total (u_j = Philox(seed, counter,
+// ray * n_fine + j)); offset U = Philox(seed, counter ^ 2^62, same index).  The K coarse and
+// n_fine fine values are sorted in LDS by rank counting (ascending, ties by index: a stable
+// sort, deterministic).  A row torch.multinomial rejects (a negative or non-finite weight, or a
+// zero sum) draws its bins uniformly and sets bit 1 (value 2) of the status word.
+constexpr int kMnMax = 512;              // K + n_fine per ray
+__device__ __forceinline__ double bcast_d(double v, int lane) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, lane);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), lane);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+__global__ __launch_bounds__(256) void resample_multinomial_kernel(ResampleArgs a, uint64_t seed, uint64_t counter) {
+#pragma clang fp contract(off)
+    __shared__ float sv[4][kMnMax];      // the ray's K coarse then n_fine fine values
+    __shared__ float stc[4][64], sdi[4][64];
+    const int lane = lane_id();
+    const int wid = threadIdx.x >> 6;
+    const int64_t ray = (int64_t)blockIdx.x * 4 + wid;
+    if (ray >= a.n_rays) return;        // wave-uniform: only wave-local synchronisation below
+    const int K = a.K, N = a.N, nfine = N - K;
+    const bool active = lane < K;
+    const int64_t rb = ray * K;
+    const float wi = active ? a.w[rb + lane] : 0.0f;
+    const float tci = active ? a.t_coarse[rb + lane] : 0.0f;
+    const float di = active ? a.dist[rb + lane] : 0.0f;
+    const bool wok = !active || (isfinite(wi) && wi >= 0.0f);
+    const double incl = wave_inclusive_scan((double)wi);
+    const double total = __shfl(incl, NERF_WAVE - 1, NERF_WAVE);
+    const bool valid = __all(wok) && isfinite(total) && total > 0.0;
+    if (!valid && lane == 0) atomicOr(a.status, 2);
+    const double cum = valid ? incl : (double)(lane + 1);
+    const double tot = valid ? total : (double)K;
+    if (active) {
+        sv[wid][lane] = tci;
+        stc[wid][lane] = tci;
+        sdi[wid][lane] = di;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int j = lane; j < nfine; j += NERF_WAVE) {
+        const uint64_t id = (uint64_t)ray * (uint64_t)nfine + (uint64_t)j;
+        const double target = (double)philox_uniform(seed, counter, id) * tot;
+        int bin = 0;
+        for (int i = 0; i < 64; ++i) {
+            if (i >= K) break;
+            bin += bcast_d(cum, i) <= target ? 1 : 0;
+        }
+        bin = bin < K ? bin : K - 1;
+        const float u2 = philox_uniform(seed, counter ^ 0x4000000000000000ull, id);
+        sv[wid][K + j] = stc[wid][bin] + u2 * sdi[wid][bin];
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int64_t ob = ray * N;
+    for (int e = lane; e < N; e += NERF_WAVE) {
+        const float ve = sv[wid][e];
+        int rank = 0;
+        for (int f = 0; f < N; ++f) {
+            const float vf = sv[wid][f];
+            rank += (vf < ve || (vf == ve && f < e)) ? 1 : 0;
+        }
+        a.t_start[ob + rank] = ve;
+    }
+}
+
 // t_end = next t_start, far for the last sample; the batch fallback overwrites
 // everything when the status word is set.
 __global__ __launch_bounds__(256) void resample_finish_kernel(int64_t n_rays, int N, float near_, float far_,
@@ -191,12 +262,15 @@ extern "C" int nerf_resample_pdf(const float* t_coarse, const float* weights, co
     NERF_REQUIRE(n_rays >= 0);
     if (n_rays == 0) return NERF_OK;
     NERF_REQUIRE(t_coarse && weights && dist_coarse && t_start && t_end && status);
-    NERF_REQUIRE(n_bins >= 1 && n_samples >= n_bins && (mode == 0 || mode == 1));
-    if (n_bins > 64) return NERF_ERR_UNSUPPORTED;
+    NERF_REQUIRE(n_bins >= 1 && n_samples >= n_bins && (mode == 0 || mode == 1 || mode == 2));
+    if (n_bins > 64 || (mode == 2 && n_samples > kMnMax)) return NERF_ERR_UNSUPPORTED;
     ResampleArgs a{t_coarse, weights, dist_coarse, n_rays, n_bins, n_samples, mode, t_start, t_end, status};
     hipStream_t st = as_stream(stream);
     dim3 grid((unsigned)((n_rays + 3) / 4)), block(256);
-    hipLaunchKernelGGL(resample_kernel, grid, block, 0, st, a);
+    if (mode == 2)
+        hipLaunchKernelGGL(resample_multinomial_kernel, grid, block, 0, st, a, seed, counter);
+    else
+        hipLaunchKernelGGL(resample_kernel, grid, block, 0, st, a);
     NERF_CHECK_LAUNCH();
     const int64_t total = n_rays * n_samples;
     dim3 grid2((unsigned)((total + 255) / 256));
