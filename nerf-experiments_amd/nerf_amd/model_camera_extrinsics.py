@@ -41,8 +41,10 @@ class CameraExtrinsics(NerfBaseModel):
             *img_idx.shape, 3, 3)
 
     def forward_origins(self, i: th.Tensor, o: th.Tensor) -> tuple[th.Tensor, th.Tensor]:
-        new_o, _, _, t = K.pose_rays(self.rotation, self.translation, i, o, o, MAGIC_NUMBER_THE_SECOND)
-        return new_o, t
+        # translation only (model_camera_extrinsics.py:61-74): rotation takes no part and gets no
+        # gradient, as in the reference (the validation alignment calls this under no_grad)
+        t = self.translation.index_select(0, i.reshape(-1)).view(*i.shape, 3) / MAGIC_NUMBER_THE_SECOND
+        return o + t, t
 
     def forward(self, i: th.Tensor, o: th.Tensor, d: th.Tensor):
         """(new_o, new_d, R, t) as model_camera_extrinsics.py:77-85 returns them ([B, 3], [B, 3],

@@ -124,3 +124,15 @@ def test_pose_rays_partial_gradients_deterministic_and_bad_index():
     new_o, new_d, R, t = K.pose_rays(rot.to(DEV), trans.to(DEV), bad.to(DEV), o.to(DEV), d.to(DEV))
     assert torch.isnan(new_o[5]).all() and torch.isnan(R[5]).all()
     assert torch.isfinite(new_o[torch.arange(4096) != 5]).all()
+
+
+def test_forward_origins_leaves_rotation_without_gradient():
+    """forward_origins (model_camera_extrinsics.py:61-74) involves only the translation."""
+    from nerf_amd.model_camera_extrinsics import CameraExtrinsics
+    m = CameraExtrinsics(5, 1e-3, 1e-5, 100).to(DEV)
+    idx = torch.tensor([0, 3, 3, 1], device=DEV)
+    o = torch.randn(4, 3, device=DEV)
+    new_o, t = m.forward_origins(idx, o)
+    new_o.sum().backward()
+    assert m.rotation.grad is None
+    assert torch.equal(m.translation.grad[3].cpu(), torch.full((3,), 2.0))
