@@ -3,8 +3,12 @@
 Restates `INGPTable` / `INGPEncoding` of the reference's 3d-ingp/model.py:14-121 (hash 44-56,
 trilinear interpolation 58-90, levels and the x/8 + 0.5 normalisation 92-121) from SURVEY.md
 §8(a) row a9; the builder's read of that file was refused in round 1, so this
-restatement follows the survey's description and is **parity unpinned**: no golden vector of the
-reference pins it.  numpy int64 for the integer index arithmetic (the reference hashes in int64
+restatement follows the survey's description.  The arithmetic the reference's 2-D copy of the
+same module shares with it (2d-ingp/model.py:13-115: the fp32 resolution schedule, bijective
+indexing, the int64 product-xor hash with primes 1 and 2654435761 and torch.remainder, multilinear
+weights on the unclipped corners) is pinned by tests/golden/hashgrid2d.npz, generated from that
+file; the 3-D specifics (third prime 805459861, x/8 + 0.5, the clip of bijective corners) remain
+as the survey states them, unpinned.  numpy int64 for the integer index arithmetic (the reference hashes in int64
 with Python-style `remainder`), fp32 for the interpolation, corners summed in a fixed order
 (k = dx + 2 dy + 4 dz) with separate multiplies and adds.
 
@@ -37,6 +41,45 @@ def corner_index(c: np.ndarray, r: int, table_size: int) -> np.ndarray:
         return cc[..., 0] + (r + 1) * cc[..., 1] + (r + 1) * (r + 1) * cc[..., 2]
     h = (c[..., 0] * PRIMES[0]) ^ (c[..., 1] * PRIMES[1]) ^ (c[..., 2] * PRIMES[2])
     return np.mod(h, table_size)
+
+
+def corner_index_2d(c: np.ndarray, r: int, table_size: int) -> np.ndarray:
+    """The reference's 2-D statement of the same indexing (2d-ingp/model.py:22,33-50): bijective
+    when (r + 1)^2 <= T, x + (r+1) y (no clip there: the 2-D inputs stay in [0, r]); otherwise
+    (x * 1) ^ (y * 2654435761) in int64 with torch.remainder (non-negative)."""
+    c = c.astype(np.int64)
+    if (r + 1) ** 2 <= table_size:
+        return c[..., 0] + (r + 1) * c[..., 1]
+    return np.mod((c[..., 0] * PRIMES[0]) ^ (c[..., 1] * PRIMES[1]), table_size)
+
+
+def level_corners_2d(u: np.ndarray, r: int, table_size: int):
+    """(indices [N, 4], weights [N, 4]) of 2d-ingp/model.py:52-81 for points u [N, 2] in [0, 1):
+    x_hat = u * r, corners (x_i, y_j) in the order (0,0), (0,1), (1,0), (1,1), weights
+    prod_d (1 - |x_hat_d - corner_d|)."""
+    xh = u.astype(np.float32) * np.float32(r)
+    base = np.floor(xh).astype(np.int64)
+    idx = np.empty((u.shape[0], 4), dtype=np.int64)
+    w = np.empty((u.shape[0], 4), dtype=np.float32)
+    for k, (i, j) in enumerate(((0, 0), (0, 1), (1, 0), (1, 1))):
+        c = base + np.array([i, j], dtype=np.int64)
+        idx[:, k] = corner_index_2d(c, r, table_size)
+        d = np.float32(1.0) - np.abs(xh - c.astype(np.float32))
+        w[:, k] = d[:, 0] * d[:, 1]
+    return idx, w
+
+
+def encode_2d(u: np.ndarray, tables: list[np.ndarray], res: list[int], table_size: int) -> np.ndarray:
+    """2d-ingp INGPEncoding.forward (model.py:109-115): per level sum_k w_k * table[idx_k] in the
+    corner order above, levels concatenated."""
+    outs = []
+    for t, r in zip(tables, res):
+        idx, w = level_corners_2d(u, r, table_size)
+        acc = np.zeros((u.shape[0], t.shape[1]), dtype=np.float32)
+        for k in range(4):
+            acc = acc + t[idx[:, k]] * w[:, k:k + 1]
+        outs.append(acc)
+    return np.concatenate(outs, axis=1)
 
 
 def scaled(x: np.ndarray, r: int) -> np.ndarray:

@@ -24,6 +24,7 @@ Fixtures:
   mipnerf.npz    mip_NeRF API: IntegratedFourierFeatures (both variance modes), MipNerfModel forward /
                  gradients, MipNerf coarse+fine forward with injected coarse t
   nerf2d.npz     2d-reconstruction Nerf2d (C1): init, Fourier features, forward, loss, gradients, 3 Adam steps
+  hashgrid2d.npz 2d-ingp INGPTable / INGPEncoding (the readable copy of the hash grid): tables, indices, weights, output
   kabsch.npz     CameraCalibrationModel.kabsch_algorithm (outlier removal on / off) and compute_pose_error
   feed.npz       ImagePoseDataset rays + __getitem__ (DataLoader collation) + get_blurred_pixel_colors
                  on a small in-memory image set; the notebook's 4x2 meshgrid known answer
@@ -580,7 +581,36 @@ def gen_kabsch():
     np.savez_compressed(os.path.join(OUT, "kabsch.npz"), **out)
 
 
-GENERATORS = {"kabsch": gen_kabsch, "nerf2d": gen_nerf2d, "pe": gen_pe, "composite": gen_composite, "resample": gen_resample, "model": gen_model,
+def gen_hashgrid2d():
+    """2d-ingp/model.py:13-115 INGPTable / INGPEncoding: the reference's readable copy of the
+    multiresolution hash grid (the 3d-ingp file itself was not read).  8 levels between 16 and
+    4096, T = 2^14, 2 features, the reference's own table init under th.manual_seed(0); inputs on a
+    1/1024 grid (so that u = x/8 + 0.5 exactly for the 3-D kernel's x = 8u - 4).  Stored: the
+    resolutions, bijective flags, per-level tables, corner indices (compute_idx on the corners
+    (x_i, y_j) in the forward's order), bilinear weights and the encoding output."""
+    (m,) = _import_from("2d-ingp", ["model"])
+    th.manual_seed(0)
+    enc = m.INGPEncoding(4096, 16, 2 ** 14, 2, 8)
+    g = th.Generator().manual_seed(3)
+    k = th.randint(0, 1024, (509, 2), generator=g)
+    k = th.cat((k, th.tensor([[0, 0], [1023, 1023], [0, 1023]])), dim=0)
+    u = k.float() / 1024
+    out = {"u": f32(u), "res": np.array([t.resolution for t in enc.encodings], np.int64),
+           "bijective": np.array([int(t.bijective) for t in enc.encodings], np.int64),
+           "features": f32(enc(u))}
+    for l, t in enumerate(enc.encodings):
+        xs = u * t.resolution
+        fl = th.floor(xs)
+        lim = th.stack((fl, fl + 1), dim=1)
+        corners = th.stack([lim[:, [i, j], th.arange(2)] for i, j in [(0, 0), (0, 1), (1, 0), (1, 1)]],
+                           dim=1).to(th.int64)
+        out[f"table{l}"] = f32(t.table)
+        out[f"idx{l}"] = t.compute_idx(corners).numpy().astype(np.int64)
+        out[f"w{l}"] = f32(th.prod(1 - th.abs(xs.unsqueeze(1) - corners), dim=-1))
+    np.savez_compressed(os.path.join(OUT, "hashgrid2d.npz"), **out)
+
+
+GENERATORS = {"hashgrid2d": gen_hashgrid2d, "kabsch": gen_kabsch, "nerf2d": gen_nerf2d, "pe": gen_pe, "composite": gen_composite, "resample": gen_resample, "model": gen_model,
               "color": gen_color, "cos_kat": gen_cos_kat, "ipe_grad": gen_ipe_grad, "garf": gen_garf,
               "pose": gen_pose, "pose_render": gen_pose_render, "mipnerf": gen_mipnerf, "feed": gen_feed}
 

@@ -1,5 +1,6 @@
-"""Hash-grid encoding (a9, config C5; 3d-ingp/model.py:14-121 as SURVEY.md §8(a) describes it —
-parity unpinned, see oracle/hashgrid_oracle.py).  CPU: the oracle's own invariants and the survey's
+"""Hash-grid encoding (a9, config C5; 3d-ingp/model.py:14-121 as SURVEY.md §8(a) describes it;
+the arithmetic it shares with the reference's readable 2-D copy, 2d-ingp/model.py:13-115, is pinned
+by tests/golden/hashgrid2d.npz — see oracle/hashgrid_oracle.py).  CPU: the oracle's own invariants and the survey's
 stated facts.  GPU: nerf_hashgrid_fwd bit-exact against the oracle (indices are integer arithmetic,
 the interpolation the same fp32 operations in the same order), the deterministic fixed-point table
 gradient against the oracle's fp64 scatter, and NerfModelINGP on the fused MLP against a
@@ -191,3 +192,66 @@ def test_nerf_model_ingp_forward_backward_vs_oracle_features():
     # the split-precision backward through 10 ReLU layers: within 1e-2 of the gradient's scale, the
     # bound of the fused input-gradient chain's own tests (tests/test_gpu_fused.py)
     assert np.abs(got - ref_gt).max() <= 1e-2 * scale, (np.abs(got - ref_gt).max(), scale)
+
+
+# ------------------------------------------------------- pinned by the reference's 2-D hash grid
+def test_oracle_matches_reference_2d_hash_grid(golden):
+    """2d-ingp/model.py:13-115 (tests/golden/hashgrid2d.npz): resolution schedule, bijective flags,
+    corner indices (int64, exact), bilinear weights (exact) and features."""
+    g = golden("hashgrid2d")
+    T = 2 ** 14
+    res = H.resolutions(8, 16, 4096)
+    assert res == g["res"].tolist()
+    assert [int((r + 1) ** 2 <= T) for r in res] == g["bijective"].tolist()
+    u = g["u"]
+    for l, r in enumerate(res):
+        idx, w = H.level_corners_2d(u, r, T)
+        assert np.array_equal(idx, g[f"idx{l}"]), l
+        assert np.array_equal(w, g[f"w{l}"]), l
+    feat = H.encode_2d(u, [g[f"table{l}"] for l in range(8)], res, T)
+    np.testing.assert_allclose(feat, g["features"], rtol=1e-6, atol=1e-12)
+
+
+def test_3d_oracle_reduces_to_the_reference_2d_grid(golden):
+    """The 3-D restatement at z = -4 (x_hat_z = 0: the z = 1 corners weigh 0, the z = 0 corners
+    hash as 2-D) on x = 8u - 4 (x/8 + 0.5 = u exactly) gives the 2-D reference's features on every
+    level where both are hashed or both bijective."""
+    g = golden("hashgrid2d")
+    T, F = 2 ** 14, 2
+    res = g["res"].tolist()
+    lv = [l for l, r in enumerate(res) if ((r + 1) ** 3 <= T) == ((r + 1) ** 2 <= T)]
+    assert lv == [0, 3, 4, 5, 6, 7]
+    u = g["u"]
+    x = np.concatenate([8 * u - 4, np.full((u.shape[0], 1), -4.0, np.float32)], axis=1).astype(np.float32)
+    table = np.zeros((len(lv), T, F), np.float32)
+    for i, l in enumerate(lv):
+        t = g[f"table{l}"]
+        table[i, :t.shape[0]] = t
+    out = H.encode(x, table, [res[l] for l in lv])
+    want = np.concatenate([g["features"][:, l * F:(l + 1) * F] for l in lv], axis=1)
+    # corners summed in another order than the reference's: fp32 rounding of a 4-term sum
+    np.testing.assert_allclose(out, want, rtol=0, atol=2e-7 * np.abs(want).max())
+
+
+@gpu
+def test_hashgrid_kernel_vs_reference_2d_grid(golden):
+    """nerf_hashgrid_fwd on the same reduction: the kernel reproduces the reference's 2-D
+    features (2d-ingp/model.py) on the shared levels."""
+    import torch
+    from nerf_amd import kernels as K
+    g = golden("hashgrid2d")
+    T, F = 2 ** 14, 2
+    res = g["res"].tolist()
+    lv = [0, 3, 4, 5, 6, 7]
+    u = g["u"]
+    x = np.concatenate([8 * u - 4, np.full((u.shape[0], 1), -4.0, np.float32)], axis=1).astype(np.float32)
+    table = np.zeros((len(lv), T, F), np.float32)
+    for i, l in enumerate(lv):
+        t = g[f"table{l}"]
+        table[i, :t.shape[0]] = t
+    dev = torch.device("cuda", 0)
+    out = torch.zeros(x.shape[0], 32, device=dev)
+    K.hashgrid_fwd(K.make_hashgrid_params(len(lv), T, F, [res[l] for l in lv]), torch.from_numpy(table).to(dev),
+                   out, x=torch.from_numpy(x).to(dev), n_samples=x.shape[0])
+    want = np.concatenate([g["features"][:, l * F:(l + 1) * F] for l in lv], axis=1)
+    np.testing.assert_allclose(out[:, :len(lv) * F].cpu().numpy(), want, rtol=0, atol=2e-7 * np.abs(want).max())
