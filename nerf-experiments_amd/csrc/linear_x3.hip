@@ -116,13 +116,13 @@ __device__ __forceinline__ f4 gauss_v4(const float* s, int n) {
 
 __device__ __forceinline__ void gauss_fwd_store(float* o, float* yo, f4 z, f4 v) {
 #pragma clang fp contract(off)
-    *reinterpret_cast<f4*>(o) = z;
+    __builtin_nontemporal_store(z, reinterpret_cast<f4*>(o));
     f4 y;
     y.x = expf((-(z.x * z.x)) * v.x);
     y.y = expf((-(z.y * z.y)) * v.y);
     y.z = expf((-(z.z * z.z)) * v.z);
     y.w = expf((-(z.w * z.w)) * v.w);
-    *reinterpret_cast<f4*>(yo) = y;
+    __builtin_nontemporal_store(y, reinterpret_cast<f4*>(yo));
 }
 
 __device__ __forceinline__ float gauss_bwd1(float g, float zz, float v, double& acc) {
@@ -139,7 +139,7 @@ __device__ __forceinline__ void gauss_bwd_store(float* o, f4 g, f4 z, f4 v, doub
     dz.y = gauss_bwd1(g.y, z.y, v.y, acc[1]);
     dz.z = gauss_bwd1(g.z, z.z, v.z, acc[2]);
     dz.w = gauss_bwd1(g.w, z.w, v.w, acc[3]);
-    *reinterpret_cast<f4*>(o) = dz;
+    __builtin_nontemporal_store(dz, reinterpret_cast<f4*>(o));
 }
 
 // ------------------------------------------------------------------------- NT
@@ -637,7 +637,7 @@ __global__ __launch_bounds__(512, 1) void linear_nt_x3_glds_kernel(NTArgs a, int
                         }
                         if (MSK) v = mbits ? apply_bits(v, xb[u]) : apply_sign(v, xa[u]);
                         if (EPI & NERF_EPI_ACCUM) v = xo[u] + v;
-                        *reinterpret_cast<f4*>(o) = v;
+                        __builtin_nontemporal_store(v, reinterpret_cast<f4*>(o));
                         nib = quad_bits(v);
                     } else if (ok) {
                         nib = epi_quad_lane(E, m, en, v);      // partial / unaligned quads (bias from memory)
