@@ -908,7 +908,7 @@ constexpr int WS_T = 16;                        // samples per step
 constexpr int WS_RAW = 2 * WS_T * 1024;         // ring stage: dY rows then X rows, 1 KB each
 constexpr int WS_IMG = 2 * 256 * 64;            // image stage: Y rows then X rows, 64 B each
 template <int NRAW, int NIMG>
-__global__ __launch_bounds__(512, 1) void linear_wgrad_x3_stream_kernel(TNArgs a, int npad, int kpad) {
+__global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void linear_wgrad_x3_stream_kernel(TNArgs a, int npad, int kpad) {
     static_assert(NRAW * WS_RAW + NIMG * WS_IMG <= 160 * 1024, "LDS");
     __shared__ __attribute__((aligned(16))) char smem[NRAW * WS_RAW + NIMG * WS_IMG];
     char* const ring = smem;
@@ -982,12 +982,18 @@ __global__ __launch_bounds__(512, 1) void linear_wgrad_x3_stream_kernel(TNArgs a
     auto conv_store = [&](int step, float (&v)[WS_T]) __attribute__((always_inline)) {
         __bf16* dst = reinterpret_cast<__bf16*>(img + (step % NIMG) * WS_IMG + op * 256 * 64);
         const int valid = mend - (mbeg + step * WS_T);      // rows of this step inside the split
-        const unsigned cm = c_ok ? ~0u : 0u;
+        // masking only where a row or the column is invalid (the split's last step, padded
+        // columns: a branch around it that full steps skip)
+        if (!(c_ok && valid >= WS_T)) {
+            const unsigned cm = c_ok ? ~0u : 0u;
 #pragma unroll
-        for (int r = 0; r < WS_T; ++r)
-            v[r] = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, v[r]) & (r < valid ? cm : 0u));
+            for (int r = 0; r < WS_T; ++r)
+                v[r] = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, v[r]) & (r < valid ? cm : 0u));
+        }
+        if (op == 0) {                                      // wave-uniform: the dY threads
 #pragma unroll
-        for (int r = 0; r < WS_T; ++r) db += v[r];
+            for (int r = 0; r < WS_T; ++r) db += v[r];
+        }
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
             bf16x8 h, l;
@@ -1039,14 +1045,20 @@ __global__ __launch_bounds__(512, 1) void linear_wgrad_x3_stream_kernel(TNArgs a
             xh[j] = *reinterpret_cast<const bf16x8*>(Xb + swz(row, lh));
             xl[j] = *reinterpret_cast<const bf16x8*>(Xb + swz(row, 2 + lh));
         }
+        // every fragment read issued before the first MFMA (one LDS latency per step, not one per
+        // reuse of a fragment register)
+        bf16x8 yh[4], yl[4];
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii) {
             const int row = wr * 128 + ii * 32 + li;
-            const bf16x8 yh = *reinterpret_cast<const bf16x8*>(Yb + swz(row, lh));
-            const bf16x8 yl = *reinterpret_cast<const bf16x8*>(Yb + swz(row, 2 + lh));
-#pragma unroll
-            for (int j = 0; j < 2; ++j) acc[ii][j] = mfma_x3(yh, yl, xh[j], xl[j], acc[ii][j]);
+            yh[ii] = *reinterpret_cast<const bf16x8*>(Yb + swz(row, lh));
+            yl[ii] = *reinterpret_cast<const bf16x8*>(Yb + swz(row, 2 + lh));
         }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[ii][j] = mfma_x3(yh[ii], yl[ii], xh[j], xl[j], acc[ii][j]);
     };
     if (steps > 0) {
         // prologue: steps 0 .. NRAW-1 issued, step 0 converted, step 1 landed
@@ -1058,12 +1070,17 @@ __global__ __launch_bounds__(512, 1) void linear_wgrad_x3_stream_kernel(TNArgs a
         wait_dma(min(steps, NRAW) - 2);
         barrier();
         for (int i = 0; i < steps; ++i) {
+            // the stage step i held was converted before the previous barrier: refill it now, so
+            // that two steps (i + 2, i + 3) stream in while step i multiplies and i + 1 converts
+            if (i + NRAW < steps) issue(i + NRAW);
             // NIMG = 2: step i + 1's conversion overlaps step i's MFMAs (other image stage)
             if (NIMG == 2) {
                 if (active) {
                     float v[WS_T];
                     conv_load(i + 1, v);
+                    __builtin_amdgcn_sched_barrier(0);      // the ring reads fly while the MFMAs run
                     mfma_step(i);
+                    __builtin_amdgcn_sched_barrier(0);
                     conv_store(i + 1, v);
                 } else {
                     convert(i + 1);
@@ -1073,8 +1090,6 @@ __global__ __launch_bounds__(512, 1) void linear_wgrad_x3_stream_kernel(TNArgs a
                 barrier();                                  // the single image stage is free
                 convert(i + 1);
             }
-            // the stage step i held was converted before the previous barrier
-            if (i + NRAW < steps) issue(i + NRAW);
             // step i + 2 landed (it is converted in the next iteration)
             wait_dma(min(steps - 1, i + NRAW) - (i + 2));
             barrier();
