@@ -789,15 +789,27 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
 
     f4 rv[8];
     unsigned mmask = 0;
+    // waves whose lanes all read one source row per sample take the pointer walk below (decided
+    // per wave: a wave mixing the two forms would run both)
+    const bool wave_rd1 = __ballot(grd != 1u) == 0;
     auto gload = [&](int mc) __attribute__((always_inline)) {
-        mmask = 0;
+        const int m0 = mc + rg * 8;
+        if (wave_rd1 && m0 + 8 <= mend) {
+            // all 8 rows inside the split, one source row per sample: a pointer walk
+            const float* p = gptr + (int64_t)m0 * gld + gcol;
+            mmask = 0xffu;
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const int m = mc + rg * 8 + r;
-            const bool mok = m < mend;
-            mmask |= (mok ? 1u : 0u) << r;
-            const unsigned mm = (unsigned)(mok ? m : mbeg);
-            rv[r] = *reinterpret_cast<const f4*>(gptr + (int64_t)(grd == 1u ? mm : mm / grd) * gld + gcol);
+            for (int r = 0; r < 8; ++r, p += gld) rv[r] = *reinterpret_cast<const f4*>(p);
+        } else {
+            mmask = 0;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int m = m0 + r;
+                const bool mok = m < mend;
+                mmask |= (mok ? 1u : 0u) << r;
+                const unsigned mm = (unsigned)(mok ? m : mbeg);
+                rv[r] = *reinterpret_cast<const f4*>(gptr + (int64_t)(grd == 1u ? mm : mm / grd) * gld + gcol);
+            }
         }
     };
     auto sstore = [&](int buf) __attribute__((always_inline)) {
@@ -805,7 +817,11 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
         __bf16* Pl = Ph + PL;
         f4 v[8];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] = (col_ok && ((mmask >> r) & 1u)) ? rv[r] : f4{0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < 8; ++r) v[r] = rv[r];
+        if (!(col_ok && mmask == 0xffu)) {                 // padded column or the split's last rows
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = (col_ok && ((mmask >> r) & 1u)) ? rv[r] : f4{0.f, 0.f, 0.f, 0.f};
+        }
         if (!isx) {
 #pragma unroll
             for (int r = 0; r < 8; ++r) dbacc += v[r];
