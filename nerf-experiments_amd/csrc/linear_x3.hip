@@ -83,6 +83,26 @@ __device__ __forceinline__ void split4(f4 v, bf16x4& hi, bf16x4& lo) {
     lo = __builtin_convertvector(v - __builtin_convertvector(hi, f4), bf16x4);
 }
 
+// 8 values -> their bf16 hi and lo halves (hi = bf16(x), lo = bf16(x - hi), both RNE), one packed
+// conversion per PAIR: hi of (x, y) in one v_cvt_pk_bf16_f32, its halves read back as fp32 by a
+// shift / a mask, x - hi and y - hi in one v_pk_add_f32, lo in one more conversion (5 VALU per pair)
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void split8_pairs(const float (&x)[8], bf16x8& hi, bf16x8& lo) {
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    u32x4 h, l;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const f2 v = {x[2 * p], x[2 * p + 1]};
+        const unsigned hp = __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
+        const f2 hv = {__builtin_bit_cast(float, hp << 16), __builtin_bit_cast(float, hp & 0xffff0000u)};
+        h[p] = hp;
+        l[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(v - hv, bf16x2));
+    }
+    hi = __builtin_bit_cast(bf16x8, h);
+    lo = __builtin_bit_cast(bf16x8, l);
+}
+
 __device__ __forceinline__ bool tile_coords(int tile, int ntm, int ntn, int& tm, int& tn) {
     const int grp = 8 * ntn;
     const int g = tile / grp, r = tile - g * grp;
@@ -830,13 +850,10 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             bf16x8 h, l;
+            float x[8];
 #pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                const float x = e == 0 ? v[r].x : (e == 1 ? v[r].y : (e == 2 ? v[r].z : v[r].w));
-                const __bf16 hb = (__bf16)x;
-                h[r] = hb;
-                l[r] = (__bf16)(x - (float)hb);
-            }
+            for (int r = 0; r < 8; ++r) x[r] = e == 0 ? v[r].x : (e == 1 ? v[r].y : (e == 2 ? v[r].z : v[r].w));
+            split8_pairs(x, h, l);
             const int o = swz(cg * 4 + e, rg);
             *reinterpret_cast<bf16x8*>(Ph + o) = h;
             *reinterpret_cast<bf16x8*>(Pl + o) = l;
@@ -1013,13 +1030,10 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
             bf16x8 h, l;
+            float x[8];
 #pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                const float x = v[8 * hh + r];
-                const __bf16 hb = (__bf16)x;
-                h[r] = hb;
-                l[r] = (__bf16)(x - (float)hb);
-            }
+            for (int r = 0; r < 8; ++r) x[r] = v[8 * hh + r];
+            split8_pairs(x, h, l);
             *reinterpret_cast<bf16x8*>(dst + swz(c, hh)) = h;
             *reinterpret_cast<bf16x8*>(dst + swz(c, 2 + hh)) = l;
         }
