@@ -19,8 +19,10 @@ Other BASELINE.json configs as extra workloads (same JSON line, their own `confi
 
   --workload garf  garf GarfModel (SURVEY §8 a8 + f3): proposal estimator on 64 samples (interlevel loss) ->
                    inverse-cdf 192 samples -> radiance network, 4096 rays per GPU
-  --workload ingp  configs[4]: 3d-ingp hash-grid NeRF (16-level hash encoding + NerfModelINGP on the fused
-                   MLP), coarse 64 + fine 192 (round/argmax resample), 5120 rays per GPU
+  --workload ingp  configs[4]: 3d-ingp NaiveINGP (3d-ingp/model.py:195-519): INGPEncoding(1600, 16, 2^16, 2, 16)
+                   + FourierFeatures(4) shared by separate coarse / fine NerfModelINGP (8 x 256) fields,
+                   64 coarse samples, fine pass of 64 + 192 (round/argmax), positions at the sample t,
+                   Adam(0.9, 0.99, 1e-15); 5120 rays per GPU -> 64 + 256 ray-samples per ray
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload mip|n2v|barf|ingp]
     (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
@@ -63,9 +65,11 @@ WORKLOADS = {
                        "2/7 (garf/main.py:168-171, model_garf.py:194-260), 4096 rays per GPU (the reference trains "
                        "at 1024)",
              "rays": 4096, "coarse": 64, "fine": 192},
-    "ingp": {"config": "3d-ingp hash-grid NeRF: 16-level hash encoding (16 x 2^16 x 2 fp32 table), NerfModelINGP "
-                       "(8 x 256 MLP, softplus(z - 1)), coarse 64 + fine 192 samples (round/argmax resample), "
-                       "5120 rays per GPU (BASELINE.json configs[4])", "rays": 5120, "coarse": 64, "fine": 192},
+    "ingp": {"config": "3d-ingp NaiveINGP step: INGPEncoding(1600, 16, 2^16, 2, 16) + FourierFeatures(4) shared by "
+                       "separate coarse and fine NerfModelINGP fields (8 x 256, softplus(z - 1)); 64 coarse samples, "
+                       "fine pass of 64 + 192 (round/argmax resample) at the sample t; MSE(coarse) + MSE(fine), "
+                       "Adam(0.9, 0.99, 1e-15); near/far 2/7 (3d-ingp/main.py:40-118), 5120 rays per GPU "
+                       "(BASELINE.json configs[4])", "rays": 5120, "coarse": 64, "fine": 256},
     "barf": {"config": "BARF camera-pose refinement: masked Fourier PE L10/L4 + identity, 128 equidistant "
                        "samples, per-image so3 CameraExtrinsics (100 views), 4096 rays per GPU "
                        "(BASELINE.json configs[3])", "rays": 4096, "coarse": 0, "fine": 128},
@@ -252,29 +256,29 @@ def build_workload(name: str, device, rank: int, feed: bool = False):
             return ren(o2, d2, pw)
         return ren, [ren, extr], opt, loss_fn, render_fn
     if name == "ingp":
-        from nerf_amd import NerfModelINGP
+        from nerf_amd.model_ingp import FourierFeatures as IngpFourier
+        from nerf_amd.model_ingp import INGPEncoding, NaiveINGP
         torch.manual_seed(0)
-        model = NerfModelINGP()
-        # 3d-ingp: near/far 2/7, no MAGIC factor in the compositor, round/argmax fine sampling
-        ren = NerfInterpolation(2.0, 7.0, model, w["fine"], "stratified_uniform", 0.0, "middle", model, w["coarse"],
-                                density_factor=(1.0, 1.0), resample_mode=1).to(device)
+        # 3d-ingp/main.py:94-118 with the hash-grid position encoder of its commented config (:98-104)
+        ren = NaiveINGP(2, 7, 64, 192, INGPEncoding(1600, 16, 2 ** 16, 2, 16), IngpFourier(4), 8, 256,
+                        learning_rate=1e-5, learning_rate_decay=1, weight_decay=0).to(device)
         o, d, pw, target, _ = synthetic_batch_lego(w["rays"], 1000 + rank, device, 400)
         opt = ren.configure_optimizers()["optimizer"]
         if feed:
             nxt = _feed_stream(device_feed(name, device, rank, w["rays"]))
 
             def loss_fn():
-                o_, _, d_, _, c_, _, pw_ = next(nxt)
-                return ren.training_loss(o_, d_, pw_, c_[:, -1])[0]
+                o_, _, d_, _, c_, _, _ = next(nxt)
+                return ren.training_loss(o_, d_, c_[:, -1])[0]
 
             def render_fn():
-                o_, _, d_, _, _, _, pw_ = next(nxt)
-                return ren(o_, d_, pw_)
+                o_, _, d_, _, _, _, _ = next(nxt)
+                return ren(o_, d_)
             return ren, [ren], opt, loss_fn, render_fn
 
         def loss_fn():
-            return ren.training_loss(o, d, pw, target)[0]
-        return ren, [ren], opt, loss_fn, lambda: ren(o, d, pw)
+            return ren.training_loss(o, d, target)[0]
+        return ren, [ren], opt, loss_fn, lambda: ren(o, d)
     if name == "garf":
         import types
         from nerf_amd import ProposalNetwork, RadianceNetwork
@@ -336,8 +340,8 @@ def build_workload(name: str, device, rank: int, feed: bool = False):
 
 def flops_per_sample(ren) -> float:
     """Algorithmic MLP FLOPs per sample for fwd + bwd (dX and dW): 2*MACs * 3."""
-    macs = sum(m.in_features * m.out_features for m in ren.model_radiance.modules()
-               if isinstance(m, torch.nn.Linear))
+    model = ren.model_fine if hasattr(ren, "model_fine") else ren.model_radiance
+    macs = sum(m.in_features * m.out_features for m in model.modules() if isinstance(m, torch.nn.Linear))
     return 2.0 * macs * 3.0
 
 

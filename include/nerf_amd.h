@@ -429,14 +429,19 @@ int nerf_ray_batch(const int64_t* indices, int64_t B, int32_t H, int32_t W, floa
                    float* colors_raw, float* colors_pair, int64_t* img_idx, int32_t* status, void* stream);
 
 /* ---------------------------------------------------------------------------
- * Multiresolution hash-grid encoding (a9, config C5): INGPTable / INGPEncoding,
- * 3d-ingp/model.py:14-121 (restated from SURVEY.md §8(a) a9; parity unpinned).
- * Per level l with resolution res[l]: x_hat = (x / 8 + 0.5) * res[l]; corners floor(x_hat) +
- * {0,1}^3; table row = x + (r+1) y + (r+1)^2 z of the corner clipped to [0, r] while (r+1)^3 <=
- * table_size, else ((x * 1) ^ (y * 2654435761) ^ (z * 805459861)) mod table_size in 64-bit
- * integers (non-negative remainder); weight prod_d (1 - |x_hat_d - corner_d|) on the unclipped
- * corner; out[n, l * F + f] = sum over corners k = dx + 2 dy + 4 dz (in that order) of
- * w_k * table[l][row_k][f].  table: [levels][table_size][features] fp32.
+ * Multiresolution hash-grid encoding (a9, config C5): INGPTable.forward / INGPEncoding.forward,
+ * 3d-ingp/model.py:14-121 (interface per VERDICT r2; arithmetic per SURVEY.md §8(a) a9, its 2-D
+ * statement 2d-ingp/model.py:13-115 pinned by tests/golden/hashgrid2d.npz).
+ * Level l has resolution res[l] and its own table of rows_l = (r+1)^3 rows when bijective
+ * ((r+1)^3 <= table_size) and table_size rows otherwise; the levels' tables are packed back to
+ * back, table = [sum_l rows_l][features] fp32 (nerf_hashgrid_table_rows).
+ * Per level: x_hat = (x / 8 + 0.5) * r (normalize = 1, INGPEncoding) or x * r (normalize = 0,
+ * INGPTable on normalised points); corners floor(x_hat) + {0,1}^3 in the reference's stacking order
+ * (0,0,0), (0,0,1), (0,1,0), ..., (1,1,1) (z fastest); row = x + (r+1) y + (r+1)^2 z of the corner
+ * clipped to [0, r] when bijective, else ((x*pi1) ^ (y*pi2) ^ (z*pi3)) mod table_size in 64-bit
+ * integers (wrapping products, non-negative remainder); weight prod_d (1 - |x_hat_d - corner_d|)
+ * on the unclipped corner; out[n, l*F + f] = sum over the corners in that order of
+ * w * table[level l][row][f] (products rounded, then added).
  * Positions: x [n][3], or (x == NULL) o[ray] + tq * d[ray] with ray = n / samples_per_ray and
  * tq = t_start[n] (query 0) or (t_start[n] + t_end[n]) / 2 (query 1).
  * ------------------------------------------------------------------------- */
@@ -447,19 +452,25 @@ typedef struct nerf_hashgrid_params {
     int32_t table_size;
     int32_t features;
     int32_t query;
+    int32_t normalize;          /* 1: x / 8 + 0.5 first (INGPEncoding); 0: points already in [0, 1) */
+    int32_t reserved;
+    int64_t primes[3];          /* pi1, pi2, pi3 (the reference's defaults 1, 2654435761, 805459861) */
     int32_t res[NERF_HASHGRID_MAX_LEVELS];
 } nerf_hashgrid_params;
+
+/* Rows of level `level`'s table, or of the whole packed table when level < 0 (-1 on bad params). */
+int64_t nerf_hashgrid_table_rows(const nerf_hashgrid_params* params, int32_t level);
 
 int nerf_hashgrid_fwd(const nerf_hashgrid_params* params, const float* x, const float* ray_o,
                       const float* ray_d, const float* t_start, const float* t_end, int64_t n_samples,
                       int32_t samples_per_ray, const float* table, float* out, int64_t out_ld, void* stream);
 
-/* Gradient of sum(out * grad_out) w.r.t. the table (positions get none): every contribution
- * w * g rounded to a 64-bit fixed-point grid 2^-s chosen from the batch's max |g| (no entry can
- * overflow) and added with integer atomics, so the result does not depend on their order
+/* Gradient of sum(out * grad_out) w.r.t. the packed table (positions get none): every
+ * contribution w * g rounded to a 64-bit fixed-point grid 2^-s chosen from the batch's max |g| (no
+ * entry can overflow) and added with integer atomics, so the result does not depend on their order
  * (deterministic); then grad_table = acc * 2^-s (+= if accumulate).  A non-finite grad_out gives
- * NaN.  workspace: nerf_hashgrid_workspace(params) bytes, 256-byte aligned, ZERO on the first call
- * (every call leaves it zero). */
+ * NaN.  workspace: nerf_hashgrid_workspace(params) bytes, 256-byte aligned; zeroed by the call
+ * itself (no state is carried between calls). */
 size_t nerf_hashgrid_workspace(const nerf_hashgrid_params* params);
 int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float* x, const float* ray_o,
                       const float* ray_d, const float* t_start, const float* t_end, int64_t n_samples,

@@ -1,7 +1,7 @@
 // Library-level C-ABI helpers (version, status strings).
 #include "common.h"
 
-extern "C" int nerf_abi_version(void) { return 3; }
+extern "C" int nerf_abi_version(void) { return 4; }
 
 extern "C" const char* nerf_status_string(int status) {
     switch (status) {

@@ -1,14 +1,22 @@
 // Multiresolution hash-grid encoding (a9, config C5): INGPTable / INGPEncoding of the
-// reference's 3d-ingp/model.py:14-121, restated from SURVEY.md §8(a) a9 (parity unpinned, see
+// reference's 3d-ingp/model.py:14-121 (the interface VERDICT r2 states; the arithmetic restated
+// from SURVEY.md §8(a) a9 and pinned on its 2-D copy, 2d-ingp/model.py:13-115 — see
 // oracle/hashgrid_oracle.py).  Contract in include/nerf_amd.h.
+//
+// Table layout = the reference's parameters: one [rows_l][F] table per level, rows_l = (r+1)^3 for
+// a bijective level ((r+1)^3 <= T), T otherwise, the levels packed back to back (row offsets
+// computed on the host from (res, T)), so INGPEncoding's per-level Parameters are views of one
+// buffer.
 //
 // Forward: one thread per (sample, level), consecutive threads = consecutive levels of one sample,
 // so a sample's L*F features are written by L adjacent threads as one contiguous row.  Per level:
-// x_hat = (x / 8 + 0.5) * r, the 8 corners floor(x_hat) + {0,1}^3, their table rows (bijective
-// while (r+1)^3 <= T, else the product-xor hash modulo T computed in 64-bit integers exactly as the
+// x_hat = (x / 8 + 0.5) * r (INGPEncoding; x * r for INGPTable on normalised points), the 8
+// corners floor(x_hat) + {0,1}^3, their table rows (bijective: x + (r+1) y + (r+1)^2 z of the corner
+// clipped to [0, r]; else the product-xor hash with primes (pi1, pi2, pi3) modulo T computed as the
 // reference's int64 tensor arithmetic with a non-negative remainder), weights prod_d (1 - |x_hat_d -
-// corner_d|) on the unclipped corner, features summed over the corners in the fixed order
-// k = dx + 2 dy + 4 dz with separate multiplies and adds (no contraction): bit-exact with the oracle.
+// corner_d|) on the unclipped corner, features summed over the corners in the reference's stacking
+// order (i, j, k) = (0,0,0), (0,0,1), (0,1,0), ... — z fastest, corner c = 4 dx + 2 dy + dz — with
+// separate multiplies and adds (no contraction), as th.sum over the stacked corners adds them.
 //
 // Backward (the table gradient; positions receive none): every contribution w * g is rounded to a
 // 64-bit fixed-point integer at a scale 2^s chosen from the batch's max |g| so that no table entry
@@ -20,6 +28,7 @@ namespace {
 
 struct HashArgs {
     nerf_hashgrid_params p;
+    int64_t off[NERF_HASHGRID_MAX_LEVELS];          // first row of each level in the packed table
     const float* x;
     const float* o;
     const float* d;
@@ -48,14 +57,30 @@ struct Corners {
     float w[8];
 };
 
-__device__ __forceinline__ Corners level_corners(const float* p, int r, int T) {
+// the hash of one corner: int64 (x*pi1) ^ (y*pi2) ^ (z*pi3) with wrap-around products and the
+// non-negative remainder modulo T (torch.remainder); modulo a power of two that is the low bits,
+// which only the low 32 bits of corners and primes determine (two's complement): 32-bit arithmetic
+__device__ __forceinline__ int hash_row(const long long* cc, const nerf_hashgrid_params& p, int T, bool pow2) {
+    if (pow2) {
+        const unsigned h = ((unsigned)cc[0] * (unsigned)p.primes[0]) ^ ((unsigned)cc[1] * (unsigned)p.primes[1]) ^
+                           ((unsigned)cc[2] * (unsigned)p.primes[2]);
+        return (int)(h & (unsigned)(T - 1));
+    }
+    const unsigned long long h = ((unsigned long long)cc[0] * (unsigned long long)p.primes[0]) ^
+                                 ((unsigned long long)cc[1] * (unsigned long long)p.primes[1]) ^
+                                 ((unsigned long long)cc[2] * (unsigned long long)p.primes[2]);
+    const long long m = (long long)h % (long long)T;
+    return (int)(m < 0 ? m + T : m);
+}
+
+__device__ __forceinline__ Corners level_corners(const float* p, const nerf_hashgrid_params& prm, int r, int T) {
 #pragma clang fp contract(off)
     Corners c;
     float xh[3];
     long long base[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        xh[j] = (p[j] / 8.0f + 0.5f) * (float)r;
+        xh[j] = (prm.normalize ? (p[j] / 8.0f + 0.5f) : p[j]) * (float)r;
         base[j] = (long long)floorf(xh[j]);
     }
     const bool bij = (long long)(r + 1) * (r + 1) * (r + 1) <= (long long)T;
@@ -66,7 +91,7 @@ __device__ __forceinline__ Corners level_corners(const float* p, int r, int T) {
         float dw[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            cc[j] = base[j] + ((k >> j) & 1);
+            cc[j] = base[j] + ((k >> (2 - j)) & 1);         // z fastest: the reference's stacking order
             dw[j] = 1.0f - fabsf(xh[j] - (float)cc[j]);
         }
         c.w[k] = (dw[0] * dw[1]) * dw[2];
@@ -76,15 +101,8 @@ __device__ __forceinline__ Corners level_corners(const float* p, int r, int T) {
 #pragma unroll
             for (int j = 0; j < 3; ++j) q[j] = cc[j] < 0 ? 0 : (cc[j] > r ? r : (int)cc[j]);
             c.idx[k] = q[0] + r1 * q[1] + r1 * r1 * q[2];
-        } else if (pow2) {
-            // the int64 product-xor modulo a power of two is its low bits, which only the low 32
-            // bits of the corners and primes determine (two's complement): 32-bit arithmetic
-            const unsigned h = (unsigned)cc[0] ^ ((unsigned)cc[1] * 2654435761u) ^ ((unsigned)cc[2] * 805459861u);
-            c.idx[k] = (int)(h & (unsigned)(T - 1));
         } else {
-            const long long h = (cc[0] * 1LL) ^ (cc[1] * 2654435761LL) ^ (cc[2] * 805459861LL);
-            const long long m = h % (long long)T;
-            c.idx[k] = (int)(m < 0 ? m + T : m);
+            c.idx[k] = hash_row(cc, prm, T, pow2);
         }
     }
     return c;
@@ -100,8 +118,8 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(HashArgs a, const flo
     if (n >= a.n) return;
     float p[3];
     sample_position(a, n, p);
-    const Corners c = level_corners(p, a.p.res[l], T);
-    const float* tab = table + (int64_t)l * T * F;
+    const Corners c = level_corners(p, a.p, a.p.res[l], T);
+    const float* tab = table + a.off[l] * F;
     float acc[NERF_HASHGRID_MAX_FEATURES];
 #pragma unroll
     for (int f = 0; f < NERF_HASHGRID_MAX_FEATURES; ++f) acc[f] = 0.0f;
@@ -263,7 +281,7 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_kernel(HashArgs a, B
 #pragma unroll
         for (int u = 0; u < BWD_UNROLL; ++u) {
             if (nb + u * BWD_THREADS >= n1) continue;
-            const Corners c = level_corners(p[u], res, T);
+            const Corners c = level_corners(p[u], a.p, res, T);
             // An LDS atomic costs the same per wave-instruction however few lanes are active, and a
             // part holds only ~1/parts of a sample's corners: so each lane queues its in-range
             // corners and the wave issues one add per queued-corner round (its longest queue)
@@ -297,7 +315,7 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_kernel(HashArgs a, B
         }
     }
     __syncthreads();
-    unsigned long long* dst = acc + ((int64_t)l * T + row0) * F;
+    unsigned long long* dst = acc + (a.off[l] + row0) * F;
     for (int e = threadIdx.x; e < prow * F; e += BWD_THREADS) {
         const unsigned long long v = part[e];
         if (v != 0ull) atomicAdd(dst + e, v);
@@ -310,8 +328,7 @@ void launch_bwd(int64_t blocks, hipStream_t s, const HashArgs& a, const BwdPlan&
     hipLaunchKernelGGL(hashgrid_bwd_kernel<F>, dim3((unsigned)blocks), dim3(BWD_THREADS), 0, s, a, pl, g, ld, gmax, acc);
 }
 
-// table gradient = accumulator * 2^-s (or NaN after a non-finite gradient); the accumulators are
-// zeroed for the next call
+// table gradient = accumulator * 2^-s (or NaN after a non-finite gradient)
 __global__ __launch_bounds__(256) void hashgrid_finish_kernel(unsigned long long* __restrict__ acc, int64_t count,
                                                               const unsigned* __restrict__ gmax, int64_t n,
                                                               float* __restrict__ grad, int accumulate) {
@@ -321,7 +338,6 @@ __global__ __launch_bounds__(256) void hashgrid_finish_kernel(unsigned long long
         const long long q = (long long)acc[i];
         const float v = s == -1000 ? NAN : (float)((double)q * inv);
         grad[i] = accumulate ? grad[i] + v : v;
-        acc[i] = 0ull;
     }
 }
 
@@ -331,7 +347,27 @@ bool valid_params(const nerf_hashgrid_params* p) {
     if ((int64_t)p->levels * p->table_size * p->features >= ((int64_t)1 << 31)) return false;
     for (int l = 0; l < p->levels; ++l)
         if (p->res[l] < 1 || p->res[l] > (1 << 20)) return false;
+    if (p->normalize != 0 && p->normalize != 1) return false;
     return p->query == 0 || p->query == 1;
+}
+
+int64_t total_rows(const nerf_hashgrid_params* p) {
+    int64_t rows = 0;
+    for (int l = 0; l < p->levels; ++l) rows += level_rows(p->res[l], p->table_size);
+    return rows;
+}
+
+HashArgs make_args(const nerf_hashgrid_params* p, const float* x, const float* o, const float* d, const float* t0,
+                   const float* t1, int64_t n, int spr) {
+    HashArgs a{};
+    a.p = *p;
+    int64_t r = 0;
+    for (int l = 0; l < p->levels; ++l) {
+        a.off[l] = r;
+        r += level_rows(p->res[l], p->table_size);
+    }
+    a.x = x, a.o = o, a.d = d, a.t0 = t0, a.t1 = t1, a.n = n, a.spr = spr;
+    return a;
 }
 
 }  // namespace
@@ -345,7 +381,7 @@ extern "C" int nerf_hashgrid_fwd(const nerf_hashgrid_params* params, const float
     NERF_REQUIRE(x != nullptr || (ray_o && ray_d && t_start && samples_per_ray >= 1 &&
                                   (params->query == 0 || t_end)));
     if (n_samples == 0) return NERF_OK;
-    HashArgs a{*params, x, ray_o, ray_d, t_start, t_end, n_samples, samples_per_ray};
+    const HashArgs a = make_args(params, x, ray_o, ray_d, t_start, t_end, n_samples, samples_per_ray);
     const int64_t threads = n_samples * params->levels;
     hipLaunchKernelGGL(hashgrid_fwd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
                        as_stream(stream), a, table, out, out_ld);
@@ -353,9 +389,14 @@ extern "C" int nerf_hashgrid_fwd(const nerf_hashgrid_params* params, const float
     return NERF_OK;
 }
 
+extern "C" int64_t nerf_hashgrid_table_rows(const nerf_hashgrid_params* params, int32_t level) {
+    if (!valid_params(params) || level >= params->levels) return -1;
+    return level < 0 ? total_rows(params) : level_rows(params->res[level], params->table_size);
+}
+
 extern "C" size_t nerf_hashgrid_workspace(const nerf_hashgrid_params* params) {
     if (!valid_params(params)) return 0;
-    return 256 + (size_t)params->levels * params->table_size * params->features * sizeof(unsigned long long);
+    return 256 + (size_t)total_rows(params) * params->features * sizeof(unsigned long long);
 }
 
 extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float* x, const float* ray_o,
@@ -370,10 +411,12 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
     NERF_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 255) == 0);
     unsigned* gmax = static_cast<unsigned*>(workspace);
     unsigned long long* acc = reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) + 256);
-    const int64_t count = (int64_t)params->levels * params->table_size * params->features;
+    const int64_t count = total_rows(params) * params->features;
     hipStream_t s = as_stream(stream);
-    if (hipMemsetAsync(gmax, 0, sizeof(unsigned), s) != hipSuccess) return NERF_ERR_LAUNCH;
-    HashArgs a{*params, x, ray_o, ray_d, t_start, t_end, n_samples, samples_per_ray};
+    // header and accumulators zeroed by every call (no state carried between calls)
+    if (hipMemsetAsync(workspace, 0, 256 + (size_t)count * sizeof(unsigned long long), s) != hipSuccess)
+        return NERF_ERR_LAUNCH;
+    const HashArgs a = make_args(params, x, ray_o, ray_d, t_start, t_end, n_samples, samples_per_ray);
     if (n_samples > 0) {
         const int cols = params->levels * params->features;
         const bool vec = cols % 4 == 0 && g_ld % 4 == 0 && (reinterpret_cast<uintptr_t>(grad_out) & 15) == 0;

@@ -7,7 +7,7 @@ from .positional_encodings import (BarfPositionalEncoding, FourierFeatures, Iden
 from .model_interpolation_architecture import NerfBaseModel, NerfModel  # noqa: F401
 from .model_interpolation import MAGIC_NUMBER, NerfInterpolation, SchedulerLeNice  # noqa: F401
 from .model_garf import GaussAct, ProposalNetwork, RadianceNetwork  # noqa: F401
-from .model_ingp import INGPEncoding, INGPTable, NerfModelINGP  # noqa: F401
+from .model_ingp import INGPEncoding, INGPTable, NaiveINGP, NerfModelINGP  # noqa: F401
 from .model_2d import FourierFeatures2d, Nerf2d  # noqa: F401
 from .optim import FusedAdam  # noqa: F401
 from .pose import compute_pose_error, kabsch_algorithm, validation_transform_rays  # noqa: F401

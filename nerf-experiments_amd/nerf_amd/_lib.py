@@ -125,6 +125,9 @@ class NerfHashgridParams(ctypes.Structure):
         ("table_size", c_i32),
         ("features", c_i32),
         ("query", c_i32),
+        ("normalize", c_i32),
+        ("reserved", c_i32),
+        ("primes", c_i64 * 3),
         ("res", c_i32 * NERF_HASHGRID_MAX_LEVELS),
     ]
 
@@ -180,6 +183,7 @@ _SIGNATURES = {
     "nerf_prop_loss": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f, c_vp, c_f, c_vp,
                                c_i64, c_vp]),
     "nerf_hashgrid_workspace": (c_sz, [ctypes.POINTER(NerfHashgridParams)]),
+    "nerf_hashgrid_table_rows": (c_i64, [ctypes.POINTER(NerfHashgridParams), c_i32]),
     "nerf_hashgrid_bwd": (c_i32, [ctypes.POINTER(NerfHashgridParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
                                   c_vp, c_i64, c_vp, c_i32, c_vp, c_sz, c_vp]),
 }
@@ -204,7 +208,7 @@ def load(path: str | None = None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.nerf_abi_version() != 3:
+    if lib.nerf_abi_version() != 4:
         raise RuntimeError("nerf_amd: ABI version mismatch between Python binding and libnerf_amd.so")
     if path is None:
         _lib = lib

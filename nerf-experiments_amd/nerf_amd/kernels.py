@@ -491,31 +491,81 @@ def pack_weight(W: torch.Tensor, col_map: torch.Tensor, Kp: int, Wp: torch.Tenso
 
 
 # ----------------------------------------------------------------------------- hash grid (a9)
-def make_hashgrid_params(levels: int, table_size: int, features: int, res, query: int = 1) -> _lib.NerfHashgridParams:
+INGP_PRIMES = (1, 2654435761, 805459861)
+
+
+def make_hashgrid_params(levels: int, table_size: int, features: int, res, query: int = 1, *,
+                         primes=INGP_PRIMES, normalize: bool = True) -> _lib.NerfHashgridParams:
     if not 1 <= levels <= _lib.NERF_HASHGRID_MAX_LEVELS:
         raise ValueError(f"levels must be in [1, {_lib.NERF_HASHGRID_MAX_LEVELS}] (got {levels})")
     if not 1 <= features <= _lib.NERF_HASHGRID_MAX_FEATURES:
-        raise ValueError(f"feature_dim must be in [1, {_lib.NERF_HASHGRID_MAX_FEATURES}] (got {features})")
+        raise ValueError(f"n_features must be in [1, {_lib.NERF_HASHGRID_MAX_FEATURES}] (got {features})")
+    if len(res) != levels or any(not 1 <= int(r) <= (1 << 20) for r in res):
+        raise ValueError(f"need {levels} resolutions in [1, 2^20] (got {list(res)})")
+    if not 1 <= table_size or levels * table_size * features >= 2 ** 31:
+        raise ValueError(f"table_size {table_size} out of range")
+    if len(primes) != 3 or any(not -2 ** 63 <= int(q) < 2 ** 63 for q in primes):
+        raise ValueError("primes must be three int64 values")
     p = _lib.NerfHashgridParams()
     p.levels, p.table_size, p.features, p.query = levels, table_size, features, query
+    p.normalize = int(bool(normalize))
+    for i, q in enumerate(primes):
+        p.primes[i] = int(q)
     for i, r in enumerate(res):
         p.res[i] = int(r)
     return p
 
 
-def hashgrid_fwd(params, table: torch.Tensor, out: torch.Tensor, *, x=None, ray_o=None, ray_d=None, t_start=None,
-                 t_end=None, n_samples: int, samples_per_ray: int = 1) -> None:
-    _require_cuda_f32("table", table)
-    _require_cuda_f32("out", out)
-    if not table.is_contiguous() or table.shape != (params.levels, params.table_size, params.features):
-        raise ValueError(f"table must be a contiguous [{params.levels}, {params.table_size}, {params.features}] tensor")
-    if out.stride(1) != 1 or out.shape[0] < n_samples or out.shape[1] < params.levels * params.features:
-        raise ValueError("out must be a row-major [n, >= levels * features] tensor")
+def hashgrid_level_rows(resolution: int, table_size: int) -> int:
+    """Rows of one level's table: (r + 1)^3 when bijective, else table_size (nerf_hashgrid_table_rows)."""
+    n = (int(resolution) + 1) ** 3
+    return n if n <= table_size else table_size
+
+
+def hashgrid_table_rows(params) -> int:
+    return sum(hashgrid_level_rows(params.res[l], params.table_size) for l in range(params.levels))
+
+
+def _hashgrid_inputs(params, n_samples, x, ray_o, ray_d, t_start, t_end, samples_per_ray):
+    """Validate the position inputs of nerf_hashgrid_fwd / _bwd: explicit [n, 3] points, or rays
+    ([B, 3] origins / directions, [B * samples_per_ray] intervals) covering n_samples."""
     for name, t in (("x", x), ("ray_o", ray_o), ("ray_d", ray_d), ("t_start", t_start), ("t_end", t_end)):
         if t is not None:
             _require_cuda_f32(name, t)
             if not t.is_contiguous():
                 raise ValueError(f"{name} must be contiguous")
+    if x is not None:
+        if x.dim() != 2 or x.shape[1] != 3 or x.shape[0] < n_samples:
+            raise ValueError(f"x must be [>= {n_samples}, 3] (got {tuple(x.shape)})")
+        return
+    if ray_o is None or ray_d is None or t_start is None or (params.query != 0 and t_end is None):
+        raise ValueError("ray mode needs ray_o, ray_d, t_start (and t_end for midpoint queries)")
+    if samples_per_ray < 1:
+        raise ValueError("samples_per_ray must be >= 1")
+    rays = (n_samples + samples_per_ray - 1) // samples_per_ray
+    for name, t in (("ray_o", ray_o), ("ray_d", ray_d)):
+        if t.numel() < 3 * rays:
+            raise ValueError(f"{name} must hold {rays} rays")
+    for name, t in (("t_start", t_start), ("t_end", t_end)):
+        if t is not None and t.numel() < n_samples:
+            raise ValueError(f"{name} must hold {n_samples} samples")
+
+
+def _hashgrid_table_check(name: str, params, table: torch.Tensor) -> None:
+    _require_cuda_f32(name, table)
+    rows = hashgrid_table_rows(params)
+    if not table.is_contiguous() or table.numel() != rows * params.features:
+        raise ValueError(f"{name} must be a contiguous packed table of {rows} x {params.features} floats "
+                         f"(got {tuple(table.shape)})")
+
+
+def hashgrid_fwd(params, table: torch.Tensor, out: torch.Tensor, *, x=None, ray_o=None, ray_d=None, t_start=None,
+                 t_end=None, n_samples: int, samples_per_ray: int = 1) -> None:
+    _hashgrid_table_check("table", params, table)
+    _require_cuda_f32("out", out)
+    if out.dim() != 2 or out.stride(1) != 1 or out.shape[0] < n_samples or out.shape[1] < params.levels * params.features:
+        raise ValueError("out must be a row-major [n, >= levels * features] tensor")
+    _hashgrid_inputs(params, n_samples, x, ray_o, ray_d, t_start, t_end, samples_per_ray)
     end = TIMER.bracket("hashgrid_fwd", 0.0, 8.0 * n_samples * params.levels * params.features * 8
                         + 4.0 * n_samples * params.levels * params.features, fn="hashgrid_fwd_kernel") \
         if TIMER is not None else None
@@ -528,16 +578,23 @@ def hashgrid_fwd(params, table: torch.Tensor, out: torch.Tensor, *, x=None, ray_
 
 
 def hashgrid_workspace_bytes(params) -> int:
-    return int(_lib.load().nerf_hashgrid_workspace(ctypes.byref(params)))
+    return 256 + hashgrid_table_rows(params) * params.features * 8
 
 
 def hashgrid_bwd(params, grad_out: torch.Tensor, grad_table: torch.Tensor, workspace: torch.Tensor, *, x=None,
                  ray_o=None, ray_d=None, t_start=None, t_end=None, n_samples: int, samples_per_ray: int = 1,
                  accumulate: bool = False) -> None:
     _require_cuda_f32("grad_out", grad_out)
-    _require_cuda_f32("grad_table", grad_table)
-    if not grad_table.is_contiguous() or grad_out.stride(1) != 1:
-        raise ValueError("grad_table must be contiguous and grad_out row-major")
+    _hashgrid_table_check("grad_table", params, grad_table)
+    if grad_out.dim() != 2 or grad_out.stride(1) != 1 or grad_out.shape[0] < n_samples \
+            or grad_out.shape[1] < params.levels * params.features:
+        raise ValueError(f"grad_out must be a row-major [>= {n_samples}, >= {params.levels * params.features}] "
+                         f"tensor (got {tuple(grad_out.shape)})")
+    _hashgrid_inputs(params, n_samples, x, ray_o, ray_d, t_start, t_end, samples_per_ray)
+    need = hashgrid_workspace_bytes(params)
+    if workspace.device != grad_out.device or not workspace.is_contiguous() \
+            or workspace.numel() * workspace.element_size() < need or workspace.data_ptr() % 256:
+        raise ValueError(f"workspace must be a contiguous, 256-byte aligned device buffer of >= {need} bytes")
     end = TIMER.bracket("hashgrid_bwd", 0.0, 8.0 * n_samples * params.levels * params.features * 8
                         + 4.0 * n_samples * params.levels * params.features, fn="hashgrid_bwd_kernel") \
         if TIMER is not None else None

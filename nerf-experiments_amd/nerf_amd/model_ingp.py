@@ -1,19 +1,38 @@
-"""Hash-grid NeRF (config C5) on gfx950 kernels: INGPTable, INGPEncoding, NerfModelINGP.
+"""Hash-grid NeRF (config C5) on gfx950 kernels, with the reference's 3d-ingp module API.
 
-The reference's 3d-ingp/model.py:14-193 as SURVEY.md §8(a) describes it (rows a7, a9): the
-builder's read of that file was refused in round 1, so constructor arguments,
-parameter names and initialisation here are this package's own and the numerics are **parity
-unpinned** (checked against oracle/hashgrid_oracle.py, a restatement of the same description).
+Mirrors 3d-ingp/model.py as VERDICT r2 states its interface (the builder's round-1 read of that
+file was refused; the file is not read again in any form) together with SURVEY.md §8(a) rows a7 /
+a9 and the readable sibling statements of the same lineage (2d-ingp/model.py:13-115 for the tables,
+naive-to-vanilla/relics/model_original.py:32-120 for the field MLP, nerf-siren/model.py:9-281 for
+the renderer):
 
-* ``INGPEncoding``: ``levels`` resolutions r_l = floor(16 b^l), b = exp((ln 1600 - ln 16) / 15),
-  one ``[levels, table_size, feature_dim]`` table (bijective rows while (r+1)^3 <= table_size, the
-  product-xor hash otherwise), positions normalised as x / 8 + 0.5; output [N, levels * feature_dim]
-  (level-major).  Forward and the (deterministic, fixed-point) table gradient are nerf_hashgrid_fwd /
-  nerf_hashgrid_bwd; positions receive no gradient.
-* ``NerfModelINGP``: the NerfModel lowering with one segment of 9 Linear layers
-  (enc -> 256, 7 x 256 -> 256, 256 -> 257), the colour head [z | dir PE] -> 128 -> 3, direction
-  encoding FourierFeatures(4, 1.0) (3d-ingp/model.py:137-148, scale 1), density softplus(z - 1).
-  The whole field MLP runs on the fused kernel (the hash features are its HBM-fed input).
+* ``INGPTable(resolution, table_size, n_features, pi1, pi2, pi3)`` — one level; its ``table``
+  Parameter has (r+1)^3 rows when bijective ((r+1)^3 <= table_size) and table_size rows
+  otherwise, initialised ``(th.rand(rows, n_features) * 2 - 1) * 10**-4`` (model.py:14-33).
+  ``forward(x)`` on points already normalised to [0, 1): nerf_hashgrid_fwd with one level.
+* ``INGPEncoding(resolution_max, resolution_min, table_size, n_features, n_levels, pi1=1,
+  pi2=2654435761, pi3=805459861)`` — ``encodings`` ModuleList of INGPTables (state_dict keys
+  ``encodings.{l}.table``), resolutions ``th.floor(resolution_min * b ** th.arange(n_levels))``;
+  ``forward(x)`` = the levels' features of x / 8 + 0.5, concatenated (model.py:92-121).  The level
+  Parameters are views of one packed buffer (re-established after ``.to()`` / ``load_state_dict``
+  or any reassignment), so one kernel launch reads every level; the table gradient is the
+  deterministic fixed-point nerf_hashgrid_bwd.  Positions receive no gradient (the renderer's
+  rays are data).
+* ``FourierFeatures(levels)`` — 3d-ingp's own encoding: [cos(x 2^k) | sin(x 2^k)], scale 1
+  (model.py:124-148; nerf_encode_fwd kind 0).
+* ``NerfModelINGP(n_hidden, hidden_dim, position_encoder, direction_encoder)`` — ``model_density``
+  (Linear(enc -> h), (n_hidden - 1) x [ReLU, Linear(h -> h)], ReLU, Linear(h -> h + 1); layer1 and
+  layer2 created first), ``model_color`` (Linear(h + dir -> h/2), ReLU, Linear(h/2 -> 3));
+  ``forward(pos, dir) -> (density, rgb)`` with density = Softplus(threshold=8)(z[:, h] - 1) and
+  rgb = sigmoid(model_color([z[:, :h] | dir])) (model.py:151-193).  The whole network runs on the
+  fused MLP kernel (the hash features are its HBM-fed input).
+* ``NaiveINGP(near_sphere_normalized, far_sphere_normalized, samples_per_ray_coarse,
+  samples_per_ray_fine, position_encoder, direction_encoder, n_hidden, hidden_dim, learning_rate,
+  learning_rate_decay, weight_decay)`` — separate ``model_coarse`` / ``model_fine`` sharing the
+  encoders; stratified coarse t; positions at the sample t; distances = t differences plus
+  far - t_last; compositing without a density factor; fine pass of samples_per_ray_coarse +
+  samples_per_ray_fine samples from the round/argmax allocation (or multinomial); Adam with betas
+  (0.9, 0.99) and eps 1e-15 + ExponentialLR (model.py:195-519).
 """
 from __future__ import annotations
 
@@ -24,126 +43,219 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import kernels as K
-from .model_interpolation_architecture import NerfModel, RawHeads
-from .positional_encodings import FourierFeatures
+from . import positional_encodings as _pe
+from .mlp import nerf_model_plan
+from .model_interpolation import _RenderRaysFn, _rng_seed, composite_raw
+from .model_interpolation_architecture import NerfBaseModel, NerfModel, RawHeads
+from .optim import FusedAdam
 
 
-def ingp_resolutions(levels: int = 16, resolution_min: int = 16, resolution_max: int = 1600) -> list[int]:
-    if levels == 1:
-        return [resolution_min]
-    b = math.exp((math.log(resolution_max) - math.log(resolution_min)) / (levels - 1))
-    return [int(math.floor(resolution_min * b ** l)) for l in range(levels)]
+def ingp_resolutions(n_levels: int = 16, resolution_min: int = 16, resolution_max: int = 1600) -> list[int]:
+    """floor(resolution_min * b^l) in the reference's fp32 tensor arithmetic (2d-ingp/model.py:101-103)."""
+    b = 1 if n_levels == 1 else math.exp((math.log(resolution_max) - math.log(resolution_min)) / (n_levels - 1))
+    return [int(r) for r in th.floor(resolution_min * b ** th.arange(n_levels))]
 
 
 class _HashGridFn(th.autograd.Function):
+    """Features of every level in one launch; the gradient of each level's table is a view of one
+    packed fixed-point gradient (nerf_hashgrid_bwd)."""
+
     @staticmethod
-    def forward(ctx, enc, x, ray_o, ray_d, t_start, t_end, samples_per_ray, query, n, table):
-        params = enc._params(query)
-        out = th.empty(n, K.pad32(enc.output_dim), device=table.device, dtype=th.float32)
-        if out.shape[1] > enc.output_dim:
-            out[:, enc.output_dim:].zero_()
-        K.hashgrid_fwd(params, table, out, x=x, ray_o=ray_o, ray_d=ray_d, t_start=t_start, t_end=t_end,
+    def forward(ctx, params, packed, rows, out_cols, x, ray_o, ray_d, t_start, t_end, samples_per_ray, n, *tables):
+        out = th.empty(n, out_cols, device=packed.device, dtype=th.float32)
+        used = params.levels * params.features
+        if out_cols > used:
+            out[:, used:].zero_()
+        K.hashgrid_fwd(params, packed, out, x=x, ray_o=ray_o, ray_d=ray_d, t_start=t_start, t_end=t_end,
                        n_samples=n, samples_per_ray=samples_per_ray)
-        ctx.enc = enc
-        ctx.meta = (samples_per_ray, query, n)
+        ctx.params = params
+        ctx.rows = rows
+        ctx.meta = (samples_per_ray, n, packed.shape)
         ctx.save_for_backward(*(t if t is not None else th.empty(0) for t in (x, ray_o, ray_d, t_start, t_end)))
         return out
 
     @staticmethod
     def backward(ctx, g):
-        enc = ctx.enc
-        spr, query, n = ctx.meta
+        spr, n, shape = ctx.meta
         x, o, d, t0, t1 = (t if t.numel() else None for t in ctx.saved_tensors)
-        grad_table = None
-        if ctx.needs_input_grad[9] and g is not None:
-            grad_table = th.empty_like(enc.table)
-            K.hashgrid_bwd(enc._params(query), g.contiguous(), grad_table, enc._workspace(g.device), x=x,
-                           ray_o=o, ray_d=d, t_start=t0, t_end=t1, n_samples=n, samples_per_ray=spr)
-        return None, None, None, None, None, None, None, None, None, grad_table
+        grads = [None] * len(ctx.rows)
+        if g is not None and any(ctx.needs_input_grad[11:]):
+            gp = th.empty(shape, device=g.device, dtype=th.float32)
+            ws = th.empty((K.hashgrid_workspace_bytes(ctx.params) + 7) // 8, dtype=th.int64, device=g.device)
+            K.hashgrid_bwd(ctx.params, g.contiguous(), gp, ws, x=x, ray_o=o, ray_d=d, t_start=t0, t_end=t1,
+                           n_samples=n, samples_per_ray=spr)
+            off = 0
+            for l, r in enumerate(ctx.rows):
+                grads[l] = gp[off:off + r]
+                off += r
+        return (None,) * 11 + tuple(grads)
+
+
+class INGPTable(nn.Module):
+    def __init__(self, resolution, table_size, n_features, pi1, pi2, pi3):
+        super().__init__()
+        self.resolution = int(resolution)
+        self.table_size = table_size
+        self.n_features = n_features
+        self.pi1 = pi1
+        self.pi2 = pi2
+        self.pi3 = pi3
+        self.bijective = table_size >= (self.resolution + 1) ** 3
+        rows = (self.resolution + 1) ** 3 if self.bijective else table_size
+        self.table = nn.Parameter((th.rand((rows, n_features)) * 2 - 1) * 10 ** (-4))
+
+    def _params(self, query: int = 1, normalize: bool = False):
+        return K.make_hashgrid_params(1, self.table_size, self.n_features, [self.resolution], query,
+                                      primes=(self.pi1, self.pi2, self.pi3), normalize=normalize)
+
+    def forward(self, x: th.Tensor) -> th.Tensor:
+        """Features [N, n_features] of points x [N, 3] already normalised to [0, 1)."""
+        if x.dim() != 2 or x.shape[1] != 3:
+            raise ValueError(f"x must be [N, 3] (got {tuple(x.shape)})")
+        x = x.contiguous()
+        table = self.table
+        if not table.is_contiguous():
+            raise ValueError("INGPTable.table must be contiguous")
+        return _HashGridFn.apply(self._params(), table, [table.shape[0]], self.n_features, x, None, None, None, None,
+                                 1, x.shape[0], table)
 
 
 class INGPEncoding(nn.Module):
-    """Multiresolution hash encoding with the PositionalEncoding interface of the renderer
-    (``forward(x, dir, pixel_width, t_start, t_end)``, ``output_dim``)."""
-
-    def __init__(self, levels: int = 16, resolution_min: int = 16, resolution_max: int = 1600,
-                 table_size: int = 2 ** 16, feature_dim: int = 2, init_scale: float = 1e-4):
+    def __init__(self, resolution_max, resolution_min, table_size, n_features, n_levels, pi1=1, pi2=2654435761,
+                 pi3=805459861):
         super().__init__()
-        self.levels = levels
+        self.output_dim = n_features * n_levels
+        self.resolution_max = resolution_max
+        self.resolution_min = resolution_min
         self.table_size = table_size
-        self.feature_dim = feature_dim
-        self.resolutions = ingp_resolutions(levels, resolution_min, resolution_max)
-        self.output_dim = levels * feature_dim
+        self.n_features = n_features
+        self.n_levels = n_levels
+        self.pi1, self.pi2, self.pi3 = pi1, pi2, pi3
         self.space_dimensions = 3
-        self.table = nn.Parameter(th.empty(levels, table_size, feature_dim).uniform_(-init_scale, init_scale))
-        self._ws = {}
+        self.b = 1 if n_levels == 1 else math.exp((math.log(resolution_max) - math.log(resolution_min)) / (n_levels - 1))
+        self.resolution = th.floor(resolution_min * self.b ** th.arange(n_levels))
+        self.encodings = nn.ModuleList(
+            [INGPTable(int(r), table_size, n_features, pi1, pi2, pi3) for r in self.resolution])
+        self.resolutions = [e.resolution for e in self.encodings]
+        self._rows = [e.table.shape[0] for e in self.encodings]
+        self._packed_table = None
+        self._pack()
+
+    @property
+    def padded_dim(self) -> int:
+        return K.pad32(self.output_dim)
 
     def _params(self, query: int = 1):
-        return K.make_hashgrid_params(self.levels, self.table_size, self.feature_dim, self.resolutions, query)
+        return K.make_hashgrid_params(self.n_levels, self.table_size, self.n_features, self.resolutions, query,
+                                      primes=(self.pi1, self.pi2, self.pi3), normalize=True)
 
-    def _workspace(self, device) -> th.Tensor:
-        # the fixed-point accumulators: zero on the first call, left zero by every call
-        ws = self._ws.get(device)
-        if ws is None:
-            nbytes = K.hashgrid_workspace_bytes(self._params())
-            ws = self._ws[device] = th.zeros((nbytes + 7) // 8, dtype=th.int64, device=device)
-        return ws
+    # -- the level Parameters as views of one buffer -------------------------------------------
+    def _aliased(self) -> bool:
+        buf = self._packed_table
+        if buf is None:
+            return False
+        F_ = self.n_features
+        off = 0
+        for e, rows in zip(self.encodings, self._rows):
+            t = e.table
+            if (t.device != buf.device or t.dtype != th.float32 or t.shape != (rows, F_) or not t.is_contiguous()
+                    or t.data_ptr() != buf.data_ptr() + off * F_ * 4):
+                return False
+            off += rows
+        return True
 
-    def bijective(self, level: int) -> bool:
-        r = self.resolutions[level]
-        return (r + 1) ** 3 <= self.table_size
+    def _pack(self) -> th.Tensor:
+        """The packed [sum rows, F] table the kernels read; re-points the level Parameters at it
+        when a conversion, load or reassignment has separated them (a device copy, no sync)."""
+        if self._aliased():
+            return self._packed_table
+        t0 = self.encodings[0].table
+        buf = th.empty(sum(self._rows), self.n_features, device=t0.device, dtype=th.float32)
+        off = 0
+        with th.no_grad():
+            for e, rows in zip(self.encodings, self._rows):
+                view = buf[off:off + rows]
+                view.copy_(e.table)
+                e.table.data = view
+                off += rows
+        self._packed_table = buf
+        return buf
 
+    def _apply(self, fn, recurse=True):
+        out = super()._apply(fn, recurse)
+        self._pack()
+        return out
+
+    def packed_table(self) -> th.Tensor:
+        return self._pack()
+
+    def _run(self, x, ray_o, ray_d, t_start, t_end, samples_per_ray, query, n):
+        packed = self._pack()
+        tables = [e.table for e in self.encodings]
+        return _HashGridFn.apply(self._params(query), packed, self._rows, K.pad32(self.output_dim), x, ray_o, ray_d,
+                                 t_start, t_end, samples_per_ray, n, *tables)
+
+    # -- kernel-facing API (the NerfModel lowering's encoder interface) -------------------------
     def encode_padded(self, x: th.Tensor, dir=None, pixel_width=None, t_start=None, t_end=None) -> th.Tensor:
         """[N, pad32(output_dim)] features of explicit positions x [N, 3]."""
-        x = x.contiguous()
-        return _HashGridFn.apply(self, x, None, None, None, None, 1, 1, x.shape[0], self.table)
+        if x.dim() != 2 or x.shape[1] != 3:
+            raise ValueError(f"x must be [N, 3] (got {tuple(x.shape)})")
+        x = x.detach().contiguous()
+        return self._run(x, None, None, None, None, 1, 1, x.shape[0])
 
     def encode_rays(self, ray_origs, ray_dirs, t_start, t_end, pixel_width, samples_per_ray: int, query: int,
                     pw_mode: int = 0) -> th.Tensor:
         """Features of the samples o + t_q d generated in-kernel (no gradient to the rays)."""
         n = t_start.numel()
-        return _HashGridFn.apply(self, None, ray_origs.detach().contiguous(), ray_dirs.detach().contiguous(),
-                                 t_start.contiguous(), t_end.contiguous(), samples_per_ray, query, n, self.table)
+        return self._run(None, ray_origs.detach().contiguous(), ray_dirs.detach().contiguous(),
+                         t_start.detach().contiguous(), t_end.detach().contiguous(), samples_per_ray, query, n)
 
+    # -- reference API ----------------------------------------------------------------------------
     def forward(self, x: th.Tensor, dir=None, pixel_width=None, t_start=None, t_end=None) -> th.Tensor:
         return self.encode_padded(x)[:, :self.output_dim]
 
 
-class INGPTable(nn.Module):
-    """One level of an INGPEncoding (its resolution, table rows and features): a view onto the
-    encoding's shared table, so the kernels read every level from one contiguous tensor."""
+class FourierFeatures(_pe.FourierFeatures):
+    """3d-ingp's FourierFeatures(levels): [cos(x 2^k) | sin(x 2^k)] (d-major), scale 1, no pi."""
 
-    def __init__(self, encoding: INGPEncoding, level: int):
-        super().__init__()
-        self._encoding = [encoding]          # not a submodule: the parameter belongs to the encoding
-        self.level = level
-        self.resolution = encoding.resolutions[level]
-        self.table_size = encoding.table_size
-        self.feature_dim = encoding.feature_dim
-
-    @property
-    def table(self) -> th.Tensor:
-        return self._encoding[0].table[self.level]
-
-    def forward(self, x: th.Tensor) -> th.Tensor:
-        enc = self._encoding[0]
-        f = enc(x)
-        return f[:, self.level * self.feature_dim:(self.level + 1) * self.feature_dim]
+    def __init__(self, levels: int):
+        super().__init__(levels, 1.0)
 
 
 class NerfModelINGP(NerfModel):
-    """Hash-grid field (config C5): NerfModel lowering with one 9-layer segment and density
-    softplus(z - 1)."""
-
     DENSITY_SHIFT = 1.0
 
-    def __init__(self, position_encoder: INGPEncoding | None = None, direction_encoder=None, n_hidden: int = 8,
-                 hidden_dim: int = 256, learning_rate_start: float = 5e-4, learning_rate_stop: float = 5e-5,
-                 learning_rate_decay_end: float = 0):
-        super().__init__(n_hidden, hidden_dim, True, False, 1,
-                         position_encoder if position_encoder is not None else INGPEncoding(),
-                         direction_encoder if direction_encoder is not None else FourierFeatures(4, 1.0),
-                         learning_rate_start, learning_rate_stop, learning_rate_decay_end)
+    def __init__(self, n_hidden: int, hidden_dim: int, position_encoder, direction_encoder):
+        NerfBaseModel.__init__(self)
+        self.n_hidden = n_hidden
+        self.hidden_dim = hidden_dim
+        self.position_encoder = position_encoder
+        self.direction_encoder = direction_encoder
+        self.model_density = self.contruct_model_density(position_encoder.output_dim, hidden_dim, hidden_dim + 1)
+        self.model_color = nn.Sequential(
+            nn.Linear(hidden_dim + direction_encoder.output_dim, hidden_dim // 2),
+            nn.ReLU(inplace=True),
+            nn.Linear(hidden_dim // 2, 3),
+        )
+        self.relu = nn.ReLU(inplace=True)
+        self.softplus = nn.Softplus(threshold=8)
+        self.sigmoid = nn.Sigmoid()
+        # the NerfModel lowering: one segment, direction at the colour head, density = trunk column h
+        self.delayed_direction = True
+        self.delayed_density = False
+        self.n_segments = 1
+        self._plan = None
+
+    def _get_plan(self):
+        if self._plan is None:
+            self._plan, self._z_last, self._head_out = nerf_model_plan(
+                1, [self.model_density], self.model_color, self.hidden_dim, self.position_encoder.output_dim,
+                self.direction_encoder.output_dim, True, False)
+        return self._plan
+
+    def list_segments(self):
+        print(f"Density: {self.model_density}")
+        print(f"Final layer: {self.model_color}")
 
     def _heads(self, z_last, head, dens) -> RawHeads:
         return RawHeads(head, dens.view(-1, 1), 0, self.DENSITY_SHIFT)
@@ -155,3 +267,111 @@ class NerfModelINGP(NerfModel):
         density = F.softplus(dens - self.DENSITY_SHIFT, beta=1, threshold=8)
         rgb = th.sigmoid(head[:, :3])
         return density, rgb
+
+
+class NaiveINGP(nn.Module):
+    def __init__(self, near_sphere_normalized: float, far_sphere_normalized: float, samples_per_ray_coarse: int,
+                 samples_per_ray_fine: int, position_encoder, direction_encoder, n_hidden: int, hidden_dim: int,
+                 learning_rate: float = 1e-4, learning_rate_decay: float = 0.5, weight_decay: float = 0.0):
+        super().__init__()
+        self.near_sphere_normalized = near_sphere_normalized
+        self.far_sphere_normalized = far_sphere_normalized
+        self.samples_per_ray_coarse = samples_per_ray_coarse
+        self.samples_per_ray_fine = samples_per_ray_fine
+        self.learning_rate = learning_rate
+        self.learning_rate_decay = learning_rate_decay
+        self.weight_decay = weight_decay
+        self.model_coarse = NerfModelINGP(n_hidden, hidden_dim, position_encoder, direction_encoder)
+        self.model_fine = NerfModelINGP(n_hidden, hidden_dim, position_encoder, direction_encoder)
+        # bit 0: the fine allocation fell back to equidistant samples; bit 1: a multinomial row was
+        # not a distribution (nerf_resample_pdf; device int32, read only if the caller wants it)
+        self.last_resample_status: th.Tensor | None = None
+
+    @property
+    def device(self) -> th.device:
+        return next(self.parameters()).device
+
+    # ---------------------------------------------------------------- sampling
+    def _sample_t_coarse(self, batch_size: int) -> th.Tensor:
+        """linspace(near, far - D, S) + U[0, 1) * D, D = (far - near) / S (Philox draws)."""
+        t, _ = K.sample_uniform(batch_size, self.samples_per_ray_coarse, self.near_sphere_normalized,
+                                self.far_sphere_normalized, True, 0.0, _rng_seed(), 0, self.device)
+        return t
+
+    def _sample_t_fine(self, t_coarse: th.Tensor, weights: th.Tensor, distances_coarse: th.Tensor,
+                       linspace: bool = True) -> th.Tensor:
+        """[batch, coarse + fine] sample t: round(w * fine) per bin with the remainder on the first
+        argmax bin, +1 (the coarse point), spread evenly over each bin (linspace=True); or fine
+        multinomial draws jittered within their bins, joined with t_coarse and sorted."""
+        if weights.dim() == 3:
+            weights = weights.squeeze(2)
+        t0, _, status = K.resample_pdf(t_coarse.detach(), weights.detach(), distances_coarse.detach(),
+                                       self.samples_per_ray_coarse + self.samples_per_ray_fine, 1 if linspace else 2,
+                                       self.near_sphere_normalized, self.far_sphere_normalized, _rng_seed(), 0)
+        self.last_resample_status = status
+        return t0
+
+    def _intervals(self, t: th.Tensor) -> th.Tensor:
+        t_end = th.empty_like(t)
+        t_end[:, :-1] = t[:, 1:]
+        t_end[:, -1] = self.far_sphere_normalized
+        return t_end
+
+    def _compute_positions(self, origins: th.Tensor, directions: th.Tensor, t: th.Tensor):
+        """(positions o + t d [B, S, 3], directions [B, S, 3], distances [B, S]: t differences and
+        far - t_last)."""
+        positions = origins.unsqueeze(1) + t.unsqueeze(2) * directions.unsqueeze(1)
+        distances = self._intervals(t) - t
+        directions = directions.unsqueeze(1).repeat(1, positions.shape[1], 1)
+        return positions, directions, distances
+
+    # ---------------------------------------------------------------- rendering
+    def _render_rays(self, densities: th.Tensor, colors: th.Tensor, distances: th.Tensor):
+        """(rgb [B, 3], weights [B, S, 1]); no density factor in 3d-ingp's compositor."""
+        rgb, w = _RenderRaysFn.apply(densities, colors, distances, 1.0, 1.0)
+        return rgb, w.unsqueeze(-1)
+
+    def _compute_color(self, model, t: th.Tensor, ray_origs: th.Tensor, ray_dirs: th.Tensor, batch_size: int,
+                       samples_per_ray: int):
+        t = t.contiguous()
+        t_end = self._intervals(t)
+        sample_dist = t_end - t
+        if isinstance(model, NerfModel):
+            # fused: positions o + t d generated in the encoding kernel, direction encoding once per
+            # ray, softplus(z - 1) / sigmoid applied in the compositor
+            heads = model.render_raw(ray_origs, ray_dirs, None, t, t_end, samples_per_ray, 0, 1)
+            rgb, weights = composite_raw(heads, sample_dist, batch_size, samples_per_ray, 1.0, 1.0)
+            return rgb, weights.unsqueeze(-1), sample_dist
+        sample_pos, sample_dir, _ = self._compute_positions(ray_origs, ray_dirs, t)
+        density, color = model(sample_pos.view(batch_size * samples_per_ray, 3),
+                               sample_dir.reshape(batch_size * samples_per_ray, 3))
+        rgb, weights = self._render_rays(density.view(batch_size, samples_per_ray),
+                                         color.view(batch_size, samples_per_ray, 3), sample_dist)
+        return rgb, weights, sample_dist
+
+    def forward(self, ray_origs: th.Tensor, ray_dirs: th.Tensor):
+        """(rgb_fine, rgb_coarse) [B, 3] each."""
+        batch_size = ray_origs.shape[0]
+        t_coarse = self._sample_t_coarse(batch_size)
+        rgb_coarse, weights, sample_dist_coarse = self._compute_color(
+            self.model_coarse, t_coarse, ray_origs, ray_dirs, batch_size, self.samples_per_ray_coarse)
+        t_fine = self._sample_t_fine(t_coarse, weights, sample_dist_coarse)
+        rgb_fine, _, _ = self._compute_color(self.model_fine, t_fine, ray_origs, ray_dirs, batch_size,
+                                             self.samples_per_ray_coarse + self.samples_per_ray_fine)
+        return rgb_fine, rgb_coarse
+
+    # ---------------------------------------------------------------- training helpers
+    def training_loss(self, ray_origs: th.Tensor, ray_dirs: th.Tensor, ray_colors: th.Tensor):
+        """MSE(coarse) + MSE(fine) of the step helper, without Lightning logging or syncs."""
+        fine, coarse = self(ray_origs, ray_dirs)
+        loss_coarse = nn.functional.mse_loss(coarse, ray_colors)
+        loss_fine = nn.functional.mse_loss(fine, ray_colors)
+        return loss_coarse + loss_fine, {"loss_coarse": loss_coarse.detach(), "loss_fine": loss_fine.detach()}
+
+    def configure_optimizers(self):
+        params = list(self.parameters())
+        opt_cls = FusedAdam if all(p.is_cuda for p in params) else th.optim.Adam
+        optimizer = opt_cls(params, lr=self.learning_rate, betas=(0.9, 0.99), eps=1e-15,
+                            weight_decay=self.weight_decay)
+        scheduler = th.optim.lr_scheduler.ExponentialLR(optimizer, gamma=self.learning_rate_decay)
+        return {"optimizer": optimizer, "lr_scheduler": scheduler}

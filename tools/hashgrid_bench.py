@@ -47,11 +47,11 @@ def main():
     def run(res):
         L = len(res)
         p = kernels.make_hashgrid_params(L, T, F, res, query=1)
-        table = (torch.rand(L, T, F, generator=g) * 2e-4 - 1e-4).to(dev)
+        table = (torch.rand(kernels.hashgrid_table_rows(p), F, generator=g) * 2e-4 - 1e-4).to(dev)
         out = torch.empty(n, L * F, device=dev)
         gout = torch.randn(n, L * F, generator=g).to(dev)
         gt = torch.empty_like(table)
-        ws = torch.zeros(kernels.hashgrid_workspace_bytes(p) // 8 + 1, dtype=torch.int64, device=dev)
+        ws = torch.empty(kernels.hashgrid_workspace_bytes(p) // 8 + 1, dtype=torch.int64, device=dev)
         kw = dict(ray_o=o, ray_d=d, t_start=t0, t_end=t1, n_samples=n, samples_per_ray=S)
         f = timed(lambda: kernels.hashgrid_fwd(p, table, out, **kw))
         b = timed(lambda: kernels.hashgrid_bwd(p, gout, gt, ws, **kw))
