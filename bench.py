@@ -638,8 +638,10 @@ def main():
 
     wl = WORKLOADS[args.workload]
     ren, modules, opt, loss_fn, render_fn = build_workload(args.workload, device, rank, args.feed == "device")
-    # gradient buckets all-reduced asynchronously from post-accumulate-grad hooks (no-op at N=1)
-    allreduce = BucketedGradAllReduce([p for m in modules for p in m.parameters()])
+    # gradient buckets all-reduced asynchronously while backward runs; direct=True: the field MLPs'
+    # weight gradients land in their buckets (N=1: in .grad) from the slab reduce itself, layer by
+    # layer, and a field used twice per step accumulates there without an extra add per parameter
+    allreduce = BucketedGradAllReduce([p for m in modules for p in m.parameters()], direct=True)
     torch.manual_seed(1234 + rank)
     render = args.mode == "render"
 

@@ -240,7 +240,8 @@ int nerf_linear_fwd(const nerf_seg* segs, int32_t n_segs, int64_t M,
  * nerf_linear_wgrad_reduce (same M, N, K) sums the slices in a fixed order
  * (deterministic) and scatters rows n < n_valid into dW[n, col_map[k]]
  * (row stride ld_dw; col_map[k] < 0 skips; col_map NULL = identity) and db[n]
- * (db may be NULL).  dY needs N % 4 == 0 and ld_dy % 4 == 0: pass N rounded up
+ * (db may be NULL); accumulate != 0 adds the rounded sums onto dW / db instead (the second
+ * pass of a field used twice per step lands in the same gradient).  dY needs N % 4 == 0 and ld_dy % 4 == 0: pass N rounded up
  * to 4 over a zero-padded dY and the true row count as n_valid. */
 size_t nerf_linear_wgrad_workspace(int64_t M, int32_t N, int32_t K);
 int nerf_linear_wgrad(const float* dY, int64_t ld_dy, int32_t N,
@@ -248,7 +249,7 @@ int nerf_linear_wgrad(const float* dY, int64_t ld_dy, int32_t N,
                       void* workspace, size_t workspace_bytes, void* stream);
 int nerf_linear_wgrad_reduce(int64_t M, int32_t N, int32_t K, int32_t n_valid,
                              const void* workspace, const int32_t* col_map,
-                             float* dW, int64_t ld_dw, float* db, void* stream);
+                             float* dW, int64_t ld_dw, float* db, int32_t accumulate, void* stream);
 
 /* Pack an nn.Linear weight W[N][K_orig] into the kernel layouts:
  *   Wp [ceil(N/128)*128][Kp]         Wp[n][k] = W[n][col_map[k]] (0 if map < 0 or n >= N)
@@ -535,14 +536,18 @@ int nerf_kabsch(const float* from, const float* to, int32_t n, int32_t remove_ou
  * nerf_pose_rays_bwd: gradients of the per-ray outputs (g_new_o, g_new_d, g_R, g_t; any may be
  *   NULL = zero) to g_rotation, g_translation [n_images][3] (overwritten; zero for images without
  *   rays).  One workgroup per image, fixed-order fp64 sums, the analytic derivative of Rodrigues'
- *   formula: deterministic.
+ *   formula: deterministic.  ray_order / image_start (both NULL, or both set): the rays bucketed by
+ *   image — ray_order [n_rays] the ray indices stably sorted by img_idx, image_start [n_images + 1]
+ *   the first position of each image in it — so each workgroup reads only its own rays (O(n_rays)
+ *   work instead of O(n_images * n_rays)); without them every workgroup tests every ray's index.
  * ------------------------------------------------------------------------- */
 int nerf_pose_rays_fwd(const float* rotation, const float* translation, int32_t n_images, const int64_t* img_idx,
                        const float* o, const float* d, int64_t n_rays, float magic, float* new_o, float* new_d,
                        float* R, float* t, void* stream);
 int nerf_pose_rays_bwd(const float* rotation, int32_t n_images, const int64_t* img_idx, const float* d,
                        int64_t n_rays, float magic, const float* g_new_o, const float* g_new_d, const float* g_R,
-                       const float* g_t, float* g_rotation, float* g_translation, void* stream);
+                       const float* g_t, const int64_t* ray_order, const int64_t* image_start, float* g_rotation,
+                       float* g_translation, void* stream);
 
 #ifdef __cplusplus
 }

@@ -101,6 +101,8 @@ __global__ __launch_bounds__(PT) void pose_rays_fwd_kernel(const float* __restri
 
 __global__ __launch_bounds__(PT) void pose_rays_bwd_kernel(const float* __restrict__ rotation, int n_images,
                                                            const int64_t* __restrict__ img_idx,
+                                                           const int64_t* __restrict__ ray_order,
+                                                           const int64_t* __restrict__ image_start,
                                                            const float* __restrict__ d, int64_t n_rays, float magic,
                                                            const float* __restrict__ g_o,
                                                            const float* __restrict__ g_d,
@@ -114,8 +116,12 @@ __global__ __launch_bounds__(PT) void pose_rays_bwd_kernel(const float* __restri
     double s[12];                                   // dL/dt (3), G = dL/dR row-major (9)
 #pragma unroll
     for (int k = 0; k < 12; ++k) s[k] = 0.0;
-    for (int64_t j = tid; j < n_rays; j += PT) {
-        if (img_idx[j] != img) continue;
+    // bucketed (ray_order != NULL): this image's rays are ray_order[image_start[img] ..
+    // image_start[img + 1]) in increasing index order; otherwise every ray's index is tested
+    const int64_t lo = ray_order ? image_start[img] : 0, hi = ray_order ? image_start[img + 1] : n_rays;
+    for (int64_t p = lo + tid; p < hi; p += PT) {
+        const int64_t j = ray_order ? ray_order[p] : p;
+        if (!ray_order && img_idx[j] != img) continue;
         const double gd[3] = {g_d ? g_d[3 * j] : 0.f, g_d ? g_d[3 * j + 1] : 0.f, g_d ? g_d[3 * j + 2] : 0.f};
         const double dd[3] = {d[3 * j], d[3 * j + 1], d[3 * j + 2]};
 #pragma unroll
@@ -178,13 +184,15 @@ extern "C" int nerf_pose_rays_fwd(const float* rotation, const float* translatio
 
 extern "C" int nerf_pose_rays_bwd(const float* rotation, int32_t n_images, const int64_t* img_idx, const float* d,
                                   int64_t n_rays, float magic, const float* g_new_o, const float* g_new_d,
-                                  const float* g_R, const float* g_t, float* g_rotation, float* g_translation,
-                                  void* stream) {
+                                  const float* g_R, const float* g_t, const int64_t* ray_order,
+                                  const int64_t* image_start, float* g_rotation, float* g_translation, void* stream) {
     NERF_REQUIRE(n_rays >= 0 && n_images >= 1 && magic != 0.0f);
     NERF_REQUIRE(rotation && g_rotation && g_translation);
     NERF_REQUIRE(n_rays == 0 || (img_idx && d));
+    NERF_REQUIRE((ray_order == nullptr) == (image_start == nullptr));
     hipLaunchKernelGGL(pose_rays_bwd_kernel, dim3(n_images), dim3(PT), 0, as_stream(stream), rotation, n_images,
-                       img_idx, d, n_rays, magic, g_new_o, g_new_d, g_R, g_t, g_rotation, g_translation);
+                       img_idx, ray_order, image_start, d, n_rays, magic, g_new_o, g_new_d, g_R, g_t, g_rotation,
+                       g_translation);
     NERF_CHECK_LAUNCH();
     return NERF_OK;
 }

@@ -430,7 +430,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(int splits, int n_val
                                                            const float* __restrict__ db_slab,
                                                            const int32_t* __restrict__ col_map,
                                                            float* __restrict__ dW, int64_t ld_dw,
-                                                           float* __restrict__ db) {
+                                                           float* __restrict__ db, int accumulate) {
     __shared__ double part[4][64];
     const int t = threadIdx.x;
     const int o = t & 63, g = t >> 6;
@@ -462,12 +462,16 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(int splits, int n_val
     __syncthreads();
     if (g == 0 && idx < lim) {
         const double s = ((part[0][o] + part[1][o]) + part[2][o]) + part[3][o];
+        // accumulate: += the rounded sum (an fp32 add, as autograd's accumulation of two passes)
         if (is_db) {
-            db[idx] = (float)s;
+            db[idx] = accumulate ? db[idx] + (float)s : (float)s;
         } else {
             const int n = (int)(idx / K), k = (int)(idx - (idx / K) * K);
             const int dst = col_map ? col_map[k] : k;
-            if (dst >= 0) dW[(int64_t)n * ld_dw + dst] = (float)s;
+            if (dst >= 0) {
+                float* p = dW + (int64_t)n * ld_dw + dst;
+                *p = accumulate ? *p + (float)s : (float)s;
+            }
         }
     }
 }
@@ -611,7 +615,8 @@ extern "C" int nerf_linear_wgrad(const float* dY, int64_t ld_dy, int32_t N, cons
 }
 
 extern "C" int nerf_linear_wgrad_reduce(int64_t M, int32_t N, int32_t K, int32_t n_valid, const void* workspace,
-                                        const int32_t* col_map, float* dW, int64_t ld_dw, float* db, void* stream) {
+                                        const int32_t* col_map, float* dW, int64_t ld_dw, float* db,
+                                        int32_t accumulate, void* stream) {
     NERF_REQUIRE(workspace && dW && N >= 1 && K >= 1 && n_valid >= 1 && n_valid <= N);
     const int ntn = (N + TB - 1) / TB, ntk = (K + TB - 1) / TB;
     const int splits = choose_splits(M, ntn * ntk);
@@ -620,7 +625,7 @@ extern "C" int nerf_linear_wgrad_reduce(int64_t M, int32_t N, int32_t K, int32_t
     const int64_t total = (int64_t)n_valid * K;
     const int64_t blocks = (total + 63) / 64 + (db ? (n_valid + 63) / 64 : 0);
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), splits, n_valid, K,
-                       ntn * TB, ntk * TB, slab, db_slab, col_map, dW, ld_dw, db);
+                       ntn * TB, ntk * TB, slab, db_slab, col_map, dW, ld_dw, db, accumulate != 0 ? 1 : 0);
     NERF_CHECK_LAUNCH();
     return NERF_OK;
 }

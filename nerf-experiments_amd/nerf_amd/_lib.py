@@ -161,7 +161,7 @@ _SIGNATURES = {
                                 c_i32, c_vp, c_i64, c_vp]),
     "nerf_linear_wgrad_workspace": (c_sz, [c_i64, c_i32, c_i32]),
     "nerf_linear_wgrad": (c_i32, [c_vp, c_i64, c_i32, ctypes.POINTER(NerfSeg), c_i32, c_i64, c_vp, c_sz, c_vp]),
-    "nerf_linear_wgrad_reduce": (c_i32, [c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "nerf_linear_wgrad_reduce": (c_i32, [c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp]),
     "nerf_pack_weight": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
     "nerf_linear_fwd_x3": (c_i32, [ctypes.POINTER(NerfSeg), c_i32, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp,
                                    c_i64, c_i32, c_vp, c_i64, c_vp]),
@@ -176,7 +176,8 @@ _SIGNATURES = {
                                   c_vp, c_vp, c_i64, c_vp]),
     "nerf_kabsch": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "nerf_pose_rays_fwd": (c_i32, [c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_i64, c_f, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    "nerf_pose_rays_bwd": (c_i32, [c_vp, c_i32, c_vp, c_vp, c_i64, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "nerf_pose_rays_bwd": (c_i32, [c_vp, c_i32, c_vp, c_vp, c_i64, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                   c_vp, c_vp]),
     "nerf_prop_cdf": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp]),
     "nerf_prop_sample": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i32, c_u64, c_u64, c_i32, c_f,
                                  c_f, c_vp, c_vp, c_i64, c_vp]),

@@ -8,7 +8,10 @@ itself is single-device (run_barf.py:103-148).
 
 ``BucketedGradAllReduce`` (what bench.py uses) launches one asynchronous all-reduce
 per gradient bucket from post-accumulate-grad hooks while the backward pass is still
-running; ``GradAllReduce`` is the one-collective-after-backward form.
+running; with ``direct=True`` it is also the field MLPs' gradient sink (nerf_amd.mlp.GRAD_SINK):
+each layer's weight gradient is reduced straight into its bucket view inside the MLP's backward,
+so buckets launch layer by layer while the remaining weight-gradient kernels run.
+``GradAllReduce`` is the one-collective-after-backward form.
 """
 from __future__ import annotations
 
@@ -93,9 +96,19 @@ class BucketedGradAllReduce:
     a parameter that NO rank produced a gradient for ends with ``.grad = None`` on every rank, as
     with one process (the reduced flags are read on the host only by a rank that itself lacked a
     gradient).  Gradients are pre-scaled by 1/world and summed.  One backward per ``finish()``.
-    With world size 1 (or no process group) every method is a no-op and ``.grad`` is untouched."""
+    With world size 1 (or no process group) every method is a no-op and ``.grad`` is untouched.
 
-    def __init__(self, params, bucket_bytes: int = 1 << 20, group=None):
+    ``direct=True`` also installs this object as the field MLPs' gradient sink
+    (``nerf_amd.mlp.GRAD_SINK``): every MLP forward recorded for autograd ``claim``s its layers'
+    weights and biases (one expected contribution each per use), and the MLP backward writes each
+    layer's gradient straight into ``target(p)`` — the bucket view, or ``.grad`` at world size 1 —
+    accumulating in the slab reduce when an earlier pass of the step already landed, then calls
+    ``landed(p)``; the last expected landing marks the parameter ready, so its bucket can start its
+    all-reduce while the MLP's remaining weight-gradient kernels run.  Those parameters never pass
+    through autograd's accumulation (the backward returns None for them), and a field used twice
+    per step costs no extra add."""
+
+    def __init__(self, params, bucket_bytes: int = 1 << 20, group=None, direct: bool = False):
         seen, plist = set(), []
         for p in params:
             if p.requires_grad and id(p) not in seen:
@@ -109,6 +122,15 @@ class BucketedGradAllReduce:
         self._where = {}
         self._next = 0
         self._hooks = []
+        self.direct = direct
+        self._owned = {id(p) for p in plist}
+        self._expected: dict[int, int] = {}
+        self._arrived: dict[int, int] = {}
+        if direct:
+            from . import mlp
+            if mlp.GRAD_SINK is not None and mlp.GRAD_SINK is not self:
+                raise RuntimeError("another direct gradient sink is installed; remove() it first")
+            mlp.GRAD_SINK = self
         if not self.active:
             return
         cur, cur_bytes = [], 0
@@ -126,7 +148,54 @@ class BucketedGradAllReduce:
                 self._where[id(p)] = (bi, j)
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._hook))
 
+    # -- direct gradient sink (nerf_amd.mlp.GRAD_SINK) --------------------------------------------
+    def claim(self, params) -> bool:
+        """One more expected contribution for each of ``params`` this step (all must be ours)."""
+        if not all(id(p) in self._owned for p in params):
+            return False
+        for p in params:
+            self._expected[id(p)] = self._expected.get(id(p), 0) + 1
+        return True
+
+    def target(self, p):
+        """(tensor the next contribution of p is written into, accumulate onto it?)."""
+        first = self._arrived.get(id(p), 0) == 0
+        if self.active:
+            bi, j = self._where[id(p)]
+            b = self.buckets[bi]
+            if b.launched or b.ready[j]:
+                raise RuntimeError("BucketedGradAllReduce: a gradient arrived after its bucket was launched; "
+                                   "call finish() after every backward()")
+            v = b.view(j)
+            if first:
+                g = p.grad
+                if g is None:
+                    return v, False
+                if g.data_ptr() != v.data_ptr():
+                    v.copy_(g)
+            return v, True
+        if first and p.grad is None:
+            p.grad = torch.empty_like(p)
+            return p.grad, False
+        return p.grad, True
+
+    def landed(self, p) -> None:
+        k = id(p)
+        n = self._arrived.get(k, 0) + 1
+        self._arrived[k] = n
+        if n == self._expected.get(k, 0) and self.active:
+            bi, j = self._where[k]
+            b = self.buckets[bi]
+            p.grad = b.view(j)
+            b.ready[j] = True
+            b.pending -= 1
+            self._launch_ready()
+
     def _hook(self, p) -> None:
+        # the hook also fires when a backward returned no gradient for p (.grad untouched): the
+        # direct sink's parameters (their gradients land through target / landed) and unused ones
+        if id(p) in self._expected or p.grad is None:
+            return
         bi, j = self._where[id(p)]
         b = self.buckets[bi]
         if b.launched or b.ready[j]:
@@ -156,12 +225,19 @@ class BucketedGradAllReduce:
             self._next += 1
 
     def finish(self) -> None:
+        arrived = self._arrived
+        self._expected, self._arrived = {}, {}
         if not self.active:
             return
         missing = []
         for b in self.buckets[self._next:]:
             for j, p in enumerate(b.params):
                 if not b.ready[j]:
+                    if arrived.get(id(p), 0) > 0:
+                        # direct contributions landed, fewer than claimed (a claimed forward whose
+                        # backward never ran): what landed is the gradient
+                        b.ready[j] = True
+                        continue
                     b.view(j).zero_()
                     missing.append((b, j))
             self._launch(b)
@@ -190,6 +266,10 @@ class BucketedGradAllReduce:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        if self.direct:
+            from . import mlp
+            if mlp.GRAD_SINK is self:
+                mlp.GRAD_SINK = None
 
 
 def shard_rays(n_global: int, rank: int, world: int) -> slice:

@@ -394,9 +394,9 @@ def linear_wgrad_workspace_bytes(M: int, N4: int, K: int) -> int:
 
 
 def linear_wgrad_reduce(M: int, N4: int, K: int, n_valid: int, workspace: torch.Tensor, col_map: torch.Tensor,
-                        dW: torch.Tensor, db: torch.Tensor | None) -> None:
+                        dW: torch.Tensor, db: torch.Tensor | None, accumulate: bool = False) -> None:
     st = _lib.load().nerf_linear_wgrad_reduce(M, N4, K, n_valid, _ptr(workspace), _ptr(col_map), _ptr(dW),
-                                              dW.stride(0), _ptr(db), _stream(dW.device))
+                                              dW.stride(0), _ptr(db), int(accumulate), _stream(dW.device))
     _lib.check(st, "nerf_linear_wgrad_reduce")
 
 
@@ -640,6 +640,19 @@ def _check_pose_inputs(rotation, translation, img_idx, o, d):
         raise ValueError(f"o / d must be [{B}, 3] (one row per image index)")
 
 
+# above this many (image, ray) pairs the pose backward buckets the rays by image first (a stable
+# device argsort + searchsorted, no host sync): each workgroup then reads only its own rays
+POSE_BUCKET_MIN_WORK = 1 << 22
+
+
+def pose_ray_buckets(idx: torch.Tensor, n_images: int):
+    """(ray_order, image_start): ray indices stably sorted by image, and each image's first position."""
+    order = torch.argsort(idx, stable=True)
+    start = torch.searchsorted(idx[order].contiguous(),
+                               torch.arange(n_images + 1, device=idx.device, dtype=torch.int64))
+    return order.contiguous(), start.contiguous()
+
+
 class _PoseRays(torch.autograd.Function):
     """CameraExtrinsics.forward on nerf_pose_rays_fwd / _bwd (csrc/camera.hip)."""
 
@@ -670,9 +683,13 @@ class _PoseRays(torch.autograd.Function):
             gr = [None if g is None else g.contiguous() for g in (g_o, g_d, g_R, g_t)]
             g_rot = torch.empty_like(rotation)
             g_trans = torch.empty_like(rotation)
+            order = start = None
+            if rotation.shape[0] * B > POSE_BUCKET_MIN_WORK:
+                order, start = pose_ray_buckets(idx, rotation.shape[0])
             _lib.check(_lib.load().nerf_pose_rays_bwd(rotation.data_ptr(), rotation.shape[0], idx.data_ptr(),
                                                       d.data_ptr(), B, float(ctx.magic), *[_ptr(g) for g in gr],
-                                                      g_rot.data_ptr(), g_trans.data_ptr(), _stream(d.device)),
+                                                      _ptr(order), _ptr(start), g_rot.data_ptr(), g_trans.data_ptr(),
+                                                      _stream(d.device)),
                        "nerf_pose_rays_bwd")
             grads[0], grads[1] = g_rot, g_trans
         if ctx.needs_input_grad[3]:
@@ -724,8 +741,20 @@ def prop_sample(vals: torch.Tensor, cdf: torch.Tensor, n: int, stratified: bool,
 def prop_loss(q_vals, q_cdf, k_vals, k_cdf, eps: float, grad_scale: float = 0.0, want_loss: bool = True,
               want_grad: bool = False):
     """Interlevel loss of query vs key intervals: (per-ray loss sums [R] or None, d/d key weights [R, K] or None)."""
+    for name, t in (("q_vals", q_vals), ("q_cdf", q_cdf), ("k_vals", k_vals), ("k_cdf", k_cdf)):
+        _require_cuda_f32(name, t)
+        if t.dim() != 2 or t.stride(1) != 1:
+            raise ValueError(f"{name} must be a row-major [R, edges] tensor")
+    if q_cdf.shape != q_vals.shape or k_cdf.shape != k_vals.shape:
+        raise ValueError("each cdf must have its edges' shape [R, edges]")
+    if q_cdf.stride(0) != q_vals.stride(0) or k_cdf.stride(0) != k_vals.stride(0):
+        raise ValueError("each cdf must share its edges' row stride")
+    if q_vals.shape[0] != k_vals.shape[0]:
+        raise ValueError("query and key intervals must cover the same rays")
     R, E = q_vals.shape
     Kb = k_vals.shape[1] - 1
+    if E < 2 or Kb < 1 or E > _lib.NERF_PROP_MAX_EDGES or Kb + 1 > _lib.NERF_PROP_MAX_EDGES:
+        raise ValueError(f"edge counts must lie in [2, {_lib.NERF_PROP_MAX_EDGES}]")
     lr = torch.empty(R, device=q_vals.device, dtype=torch.float32) if want_loss else None
     gw = torch.empty(R, Kb, device=q_vals.device, dtype=torch.float32) if want_grad else None
     _lib.check(_lib.load().nerf_prop_loss(q_vals.data_ptr(), q_cdf.data_ptr(), q_vals.stride(0), k_vals.data_ptr(),

@@ -52,6 +52,16 @@ GAUSS_EPILOGUE = True
 # test hook: when a list, every MLPFunction.forward appends (layer outputs, ReLU mask bits)
 CAPTURE: list | None = None
 
+# Direct weight-gradient sink (nerf_amd.ddp.BucketedGradAllReduce(direct=True) installs itself):
+# a forward recorded for autograd claims its layers' weight and bias parameters (one expected
+# contribution each), and the backward writes each layer's gradient straight into the sink's
+# target — the parameter's gradient-bucket view, or .grad — accumulating in the slab reduce's
+# epilogue when an earlier pass of the same step already landed there, instead of returning it
+# to autograd (no separate add per parameter for a field used twice per step).  The sink learns
+# of every landing at once, so a complete gradient bucket can start its all-reduce while the
+# remaining layers' weight gradients are still being computed.
+GRAD_SINK = None
+
 
 @dataclass
 class Source:
@@ -203,6 +213,10 @@ class MLPPlan:
                 lp.finalize(device)
             self.device = device
 
+    def linear_params(self):
+        """The layers' weight and bias parameters (what a direct gradient sink takes over)."""
+        return [t for lp in self.layers for t in (lp.module.weight, lp.module.bias)]
+
     def params(self):
         """Autograd inputs in a fixed order: per layer weight, bias (+ Gaussian inverse std)."""
         ps = []
@@ -304,6 +318,8 @@ class MLPFunction(torch.autograd.Function):
         ctx.masks = masks
         ctx.prec = prec
         ctx.plan = plan
+        sink = GRAD_SINK
+        ctx.sink = sink if (sink is not None and not plan.infer and sink.claim(plan.linear_params())) else None
         ctx.M = M
         ctx.dir_rd = dir_rd
         ctx.has_dirs = dirs is not None
@@ -406,8 +422,17 @@ class MLPFunction(torch.autograd.Function):
                     dY[li][:, c] += g
             dZ = dY[li]
             w = lp.module.weight
+            sink = ctx.sink
             if dZ is None:
-                layer_grads[li] = [torch.zeros_like(w), torch.zeros_like(lp.module.bias)]
+                if sink is not None:
+                    for t in (w, lp.module.bias):
+                        g, acc = sink.target(t)
+                        if not acc:
+                            g.zero_()
+                        sink.landed(t)
+                    layer_grads[li] = [None, None]
+                else:
+                    layer_grads[li] = [torch.zeros_like(w), torch.zeros_like(lp.module.bias)]
                 if lp.gauss is not None:
                     layer_grads[li].append(torch.zeros_like(lp.gauss))
                 continue
@@ -431,13 +456,22 @@ class MLPFunction(torch.autograd.Function):
                 segs.append((t, s.k_seg, rd))
             # ---- weight and bias gradients
             N4 = (lp.N + 3) // 4 * 4
-            gW = torch.empty_like(w)
-            gb = torch.empty_like(lp.module.bias)
+            if sink is not None:
+                gW, acc = sink.target(w)
+                gb, acc_b = sink.target(lp.module.bias)
+                if acc != acc_b:
+                    raise RuntimeError("direct gradient sink: weight and bias of one layer out of step")
+            else:
+                gW, gb, acc = torch.empty_like(w), torch.empty_like(lp.module.bias), False
             if ctx.prec == "x3":
                 K.linear_wgrad_x3(dZ, N4, segs, M, workspace)
             else:
                 K.linear_wgrad(dZ, N4, segs, M, workspace)
-            K.linear_wgrad_reduce(M, N4, lp.Kp, lp.N, workspace, lp.col_map, gW, gb)
+            K.linear_wgrad_reduce(M, N4, lp.Kp, lp.N, workspace, lp.col_map, gW, gb, accumulate=acc)
+            if sink is not None:
+                sink.landed(w)
+                sink.landed(lp.module.bias)
+                gW = gb = None
             layer_grads[li] = [gW, gb] + ([gs] if gs is not None else [])
             # ---- input gradients
             if chain:

@@ -207,7 +207,7 @@ class BarfPositionalEncoding(PositionalEncoding):
         self.space_dimensions = space_dimensions
         self.register_buffer("alpha", th.tensor(float(alpha_start)))
         self._alpha_host = float(th.tensor(float(alpha_start), dtype=th.float32))
-        self._alpha_seen = (id(self.alpha), self.alpha._version)
+        self._alpha_seen = (self.alpha, self.alpha._version)
 
     def update_alpha(self, epoch: float) -> None:
         if epoch < self.alpha_increase_start_epoch:
@@ -220,24 +220,26 @@ class BarfPositionalEncoding(PositionalEncoding):
         # device-side buffer kept for state_dict compatibility; fill_ enqueues, never syncs
         self.alpha.fill_(float(alpha))
         self._alpha_host = float(th.tensor(float(alpha), dtype=th.float32))
-        self._alpha_seen = (id(self.alpha), self.alpha._version)
+        self._alpha_seen = (self.alpha, self.alpha._version)
 
     def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
         super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
         key = prefix + "alpha"
         if key in state_dict:
             self._alpha_host = float(state_dict[key].float().cpu())
-            self._alpha_seen = (id(self.alpha), self.alpha._version)
+            self._alpha_seen = (self.alpha, self.alpha._version)
 
     def _sync_alpha_host(self) -> None:
         """Refresh the host mirror of alpha after a write that bypassed update_alpha: assigning a new
         tensor (``enc.alpha = th.tensor(a)``, what the reference's own update_alpha does) or an
         in-place write (``enc.alpha.fill_(a)``, ``.to()``/``_apply`` moves).  Detected by the buffer's
-        identity and version counter (a host-side check; the device read happens only then)."""
-        cur = (id(self.alpha), self.alpha._version)
-        if cur != self._alpha_seen:
+        identity and version counter (a host-side check; the device read happens only then).  The
+        last-seen tensor is held by reference and compared with ``is``: a freed tensor's id() can be
+        reused by the next one, a live one's cannot."""
+        seen, version = self._alpha_seen
+        if self.alpha is not seen or self.alpha._version != version:
             self._alpha_host = float(self.alpha.detach().float().cpu())
-            self._alpha_seen = (id(self.alpha), self.alpha._version)
+            self._alpha_seen = (self.alpha, self.alpha._version)
 
     def compute_mask(self, alpha: th.Tensor) -> th.Tensor:
         vals = barf_mask_values(float(alpha), self.levels)

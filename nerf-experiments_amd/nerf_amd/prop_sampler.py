@@ -96,7 +96,11 @@ class PropNetEstimator:
     def compute_loss(self, trans: th.Tensor, loss_scaler: float = 1.0) -> th.Tensor:
         if len(self.prop_cache) == 0:
             return th.zeros((), device=trans.device)
-        q_vals, _, _ = self.prop_cache.pop()
+        q_vals, _, _ = self.prop_cache[-1]
+        if trans.dim() != 2 or tuple(trans.shape) != (q_vals.shape[0], q_vals.shape[1] - 1):
+            raise ValueError(f"trans must be [{q_vals.shape[0]}, {q_vals.shape[1] - 1}] (the last sampling's "
+                             f"intervals), got {tuple(trans.shape)}")
+        self.prop_cache.pop()
         q_cdf = (1.0 - th.cat([trans, th.zeros_like(trans[:, :1])], dim=-1)).detach().contiguous()
         loss = th.zeros((), device=trans.device)
         while self.prop_cache:

@@ -136,3 +136,31 @@ def test_forward_origins_leaves_rotation_without_gradient():
     new_o.sum().backward()
     assert m.rotation.grad is None
     assert torch.equal(m.translation.grad[3].cpu(), torch.full((3,), 2.0))
+
+
+def test_pose_rays_bucketed_backward_matches_scan():
+    """Above POSE_BUCKET_MIN_WORK (image, ray) pairs the backward buckets rays by image (stable
+    device argsort + searchsorted) so each workgroup reads only its own rays: same gradients as the
+    all-rays scan (fp64 sums in another grouping, rounded to fp32: 1e-6 of scale), deterministic,
+    rays with an out-of-range index contribute to no image."""
+    from nerf_amd import kernels as K
+    rot, trans, idx, o, d = _pose_case(300, 20000, 0.2, 11)
+    idx[7] = -1
+    idx[8] = 300
+    g = torch.Generator().manual_seed(2)
+    go, gd = torch.randn(20000, 3, generator=g).to(DEV), torch.randn(20000, 3, generator=g).to(DEV)
+    outs = []
+    old = K.POSE_BUCKET_MIN_WORK
+    try:
+        for thr in (1 << 62, 0, 0):
+            K.POSE_BUCKET_MIN_WORK = thr
+            rd, td = rot.to(DEV).requires_grad_(), trans.to(DEV).requires_grad_()
+            new_o, new_d, _, _ = K.pose_rays(rd, td, idx.to(DEV), o.to(DEV), d.to(DEV))
+            ((torch.nan_to_num(new_o) * go).sum() + (torch.nan_to_num(new_d) * gd).sum()).backward()
+            outs.append((rd.grad.clone(), td.grad.clone()))
+    finally:
+        K.POSE_BUCKET_MIN_WORK = old
+    for a, b in zip(outs[0], outs[1]):
+        assert (a - b).abs().max().item() <= 1e-6 * a.abs().max().item()
+    assert torch.equal(outs[1][0], outs[2][0]) and torch.equal(outs[1][1], outs[2][1])
+    assert torch.equal(outs[1][0][-1].cpu(), torch.zeros(3))      # the last image has no rays

@@ -33,6 +33,51 @@ def test_prop_cdf_vs_oracle(K):
     torch.testing.assert_close(cdf, NO.prop_cdf(w), atol=1e-6, rtol=0)
 
 
+@pytest.mark.parametrize("S", [1, 64, 192])
+def test_prop_cdf_of_composite_weights_is_one_minus_trans(S):
+    """nerfacc forms the proposal cdf as 1 - [trans, 0] from the renderer's exclusive transmittance
+    (garf/model_garf.py:210-230,257 call sites); here it is built from the compositing kernel's
+    weights.  The two agree within 1e-6: trans from the same sigma, delta in fp64 (the compositing
+    kernel's own fp64 scan), weights from nerf_composite_fwd, cdf from nerf_prop_cdf."""
+    from nerf_amd import kernels as Kn
+    R = 53
+    g = torch.Generator().manual_seed(S)
+    sigma = torch.nn.functional.softplus(torch.randn(R, S, generator=g) * 2)
+    sigma[3] = 0.0                                   # an empty ray: trans 1 everywhere
+    sigma[4, S // 2:] = 1e4                          # an opaque one: trans 0 past the wall
+    t = torch.sort(torch.rand(R, S + 1, generator=g), dim=1).values * 5 + 2
+    delta = (t[:, 1:] - t[:, :-1]).contiguous()
+    col = torch.rand(R * S, 4, generator=g)
+    _, w = Kn.composite_fwd(sigma.reshape(-1).to(DEV), 1, col.to(DEV), 4, delta.to(DEV), R, S, 1.0, 1.0, False)
+    cdf = Kn.prop_cdf(w.view(R, S)).cpu().double()
+    trans = torch.exp(-torch.cumsum(torch.cat([torch.zeros(R, 1, dtype=torch.float64),
+                                               (sigma.double() * delta.double())[:, :-1]], 1), dim=1))
+    want = 1.0 - torch.cat([trans, torch.zeros(R, 1, dtype=torch.float64)], dim=1)
+    assert (cdf - want).abs().max().item() <= 1e-6
+
+
+def test_prop_loss_and_compute_loss_validate_inputs():
+    from nerf_amd import kernels as Kn
+    from nerf_amd.prop_sampler import PropNetEstimator
+    R, n, Kb = 8, 16, 12
+    q_vals = torch.linspace(0, 1, n + 1).expand(R, n + 1).contiguous().to(DEV)
+    k_vals = torch.linspace(0, 1, Kb + 1).expand(R, Kb + 1).contiguous().to(DEV)
+    q_cdf, k_cdf = q_vals.clone(), k_vals.clone()
+    Kn.prop_loss(q_vals, q_cdf, k_vals, k_cdf, 1e-7)                       # well-formed: fine
+    with pytest.raises(ValueError):
+        Kn.prop_loss(q_vals, q_cdf[:, :-1], k_vals, k_cdf, 1e-7)           # cdf / edges mismatch
+    with pytest.raises(ValueError):
+        Kn.prop_loss(q_vals, q_cdf, k_vals[:4], k_cdf[:4], 1e-7)           # different ray counts
+    with pytest.raises(ValueError):
+        Kn.prop_loss(q_vals.t().contiguous().t(), q_cdf, k_vals, k_cdf, 1e-7)   # column-major edges
+    with pytest.raises(ValueError):
+        Kn.prop_loss(q_vals.cpu(), q_cdf, k_vals, k_cdf, 1e-7)             # host tensor
+    est = PropNetEstimator()
+    est.prop_cache = [(k_vals, torch.rand(R, Kb, device=DEV), k_cdf), (q_vals, None, None)]
+    with pytest.raises(ValueError):
+        est.compute_loss(torch.rand(R, n + 3, device=DEV))                 # trans of another sample count
+
+
 @pytest.mark.parametrize("transform", ["uniform", "lindisp"])
 @pytest.mark.parametrize("K,n", [(1, 64), (64, 192), (300, 100)])
 def test_prop_sample_deterministic_vs_oracle(transform, K, n):

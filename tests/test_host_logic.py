@@ -153,6 +153,22 @@ def test_barf_alpha_direct_writes_refresh_the_mask():
     assert enc.mask_values() == O.barf_mask(10.0, 10).tolist()
 
 
+def test_barf_alpha_reassigned_twice_without_forward():
+    """Two assignments with no mask read between them: the second tensor may reuse the first's
+    freed id() at version 0, which an (id, version) check would take for the seen tensor."""
+    import gc
+
+    import torch as th
+    from nerf_amd import BarfPositionalEncoding
+    enc = BarfPositionalEncoding(10, 0.0, 2.0, 6.0, True, 1.0)
+    assert enc.mask_values() == O.barf_mask(0.0, 10).tolist()
+    for a in (2.5, 6.75, 1.25, 9.5):
+        enc.alpha = th.tensor(a)
+        enc.alpha = th.tensor(a + 0.125)
+        gc.collect()
+        assert enc.mask_values() == O.barf_mask(a + 0.125, 10).tolist()
+
+
 def test_encoder_dims_and_errors():
     from nerf_amd import (FourierFeatures, IdentityPositionalEncoding, IntegratedBarfFourierFeatures,
                           IntegratedFourierFeatures)
