@@ -197,12 +197,16 @@ __device__ __forceinline__ void dma_seek(Ctx& c, int l) {
 constexpr int DMA_PER_WAVE = 2 * KBMAX / NWAVE;
 __device__ __forceinline__ void issue_dma(Ctx& c, int slot) {
     char* dst = c.smem + slot * SLOT_BYTES;
+#ifndef NERF_FUSED_NODMA          // diagnostic builds only: time the kernel without its weight stream
 #pragma unroll
     for (int i = 0; i < DMA_PER_WAVE; ++i) {
         const int u = (c.wave + NWAVE * i) & (c.d_units - 1);   // d_units: 8 or 16
         __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rimg, (lds_void_t*)(dst + u * 1024), 16, c.lane * 16,
                                                  c.d_off + u * 1024, 0, 0);
     }
+#else
+    (void)dst;
+#endif
     if (c.d_remaining > 1) {
         c.d_off += c.d_units * 1024;
         if (--c.d_left == 0) dma_seek(c, __builtin_amdgcn_readlane(c.t_next, c.d_layer));
@@ -241,6 +245,9 @@ __device__ __forceinline__ void split2(float x, float y, unsigned& hi, unsigned&
 // bits (FWD); 3 = the hi/lo split into the LDS image of the next layer's operand.
 template <int MODE>
 __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, f4 (&a)[SB], f4 b) {
+#ifdef NERF_FUSED_NOEPI           // diagnostic builds only (timing without the chunk epilogues)
+    return;
+#endif
     const int g = c.lane >> 4;
     const int q = ch >> 1, bb = ch & 1;
     if (p < 2) {
@@ -450,7 +457,9 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
             // chunk and followed by >= AFTER_DMA_VM vector-memory ops), then everyone else's; the
             // other slot is free
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AFTER_DMA_VM) : "memory");
+#ifndef NERF_FUSED_NOBARRIER      // diagnostic builds only (timing without the per-chunk barrier)
             barrier();
+#endif
             lds_frag<0>(fr[0][0], sa);
             lds_frag<1024>(fr[0][1], sa);
             if (KBR > 1) {
