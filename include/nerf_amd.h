@@ -48,6 +48,10 @@ extern "C" {
 /* Library / ABI version (bumped on any signature change). */
 int nerf_abi_version(void);
 const char* nerf_status_string(int status);
+/* sizeof of the argument structs, for bindings to check their layouts against:
+ * 0 nerf_pe_params, 1 nerf_fused_layer, 2 nerf_fused_encoding, 3 nerf_hashgrid_params,
+ * 4 nerf_adam_batch, 5 nerf_seg; -1 for an unknown index. */
+int64_t nerf_struct_size(int32_t which);
 
 /* ---------------------------------------------------------------------------
  * Alpha compositing (a4).  One wavefront per ray, exclusive prefix sum of
@@ -290,16 +294,19 @@ int nerf_pack_weight_x3(const float* W, int32_t N, int32_t K_orig, const int32_t
  * Fused field-MLP forward (a7: NerfModel.forward, barf/model_interpolation_architecture.py:96-141,
  * every Linear + bias + ReLU of the network in ONE launch, split precision as above).
  *
- * Each wave owns 32 samples and keeps their activations in registers from layer to layer
- * (as the B operand of v_mfma_f32_32x32x16_bf16, bf16 hi/lo): only the HBM-fed inputs
- * (position / direction encodings) are read and only the outputs the backward needs are
- * written.  Weights stream through LDS by LDS-DMA in "chunks" (32 output rows of one layer:
- * its 32-deep k-blocks as ready-to-use MFMA fragments, 4 KB each), all packed into one image by
- * nerf_fused_pack together with the biases ([nb][32] fp32 per layer at bias_off).  Layer l's
- * input is [previous layer's output (kbr 32-wide blocks, none for the first layer) | up to 2 HBM
- * segments (kbh blocks in all)]; type = 3*(kbr/4) + kbh with kbr in {0, 4, 8}, kbh in {0, 1, 2}.  out[m, n] for n < ldo
- * (columns >= N are written as 0), ReLU mask bits as NERF_EPI_MASKOUT (N <= 256), column
- * col_idx (a multiple of 32) additionally into col_out[m].  Buffers: byte extents < 2^31.
+ * A workgroup of 8 waves owns 128 samples, a wave 16 of them, whose activations stay in
+ * registers from layer to layer (the B operand of v_mfma_f32_16x16x32_bf16, bf16 hi/lo): only
+ * the HBM-fed inputs are read and only the outputs the backward needs are written.  Weights
+ * stream through LDS by LDS-DMA in "chunks" (16 output rows of one layer: its 32-deep k-blocks as
+ * ready-to-use MFMA fragments, 2 KB each), all packed into one image by nerf_fused_pack together
+ * with the biases.  Layer l's input is [previous layer's output (kbr 32-wide blocks, none for the
+ * first layer) | up to 2 HBM-fed segments (kbh blocks in all)]; type = 3*(kbr/4) + kbh with kbr in
+ * {0, 4, 8}, kbh in {0, 1, 2}.  A segment is read from seg_ptr, or GENERATED in-kernel
+ * (seg_gen): the position encoding of the samples o + tq d of rays, or the encoding of the
+ * rays' directions, exactly as nerf_encode_fwd computes them (the first layer reading it also
+ * stores the rows for the weight gradients).  out[m, n] for n < ldo (columns >= N are written as
+ * 0), ReLU mask bits as NERF_EPI_MASKOUT (N <= 256), column col_idx (a multiple of 32)
+ * additionally into col_out[m].  Buffers: byte extents < 2^31.
  * The same launch runs the input-gradient chain of the backward (layers in reverse, images of
  * W^T, no bias, mask_in instead of ReLU): each step's output is the previous layer's
  * pre-activation gradient, kept in registers for the next step and stored for the weight gradients.
@@ -332,10 +339,31 @@ typedef struct nerf_fused_layer {
     int64_t ldo2;
     int32_t n1;            /* chunks written to out (= nb when out2 is unused) */
     int32_t hbm_off;       /* byte offset of the layer's HBM-fed weight fragments in the image */
+    int32_t seg_gen[2];    /* 0: segment s is read from seg_ptr; 1 + e: generated by encodings[e]
+                              (+ 8: this layer also stores the generated rows to encodings[e].out) */
 } nerf_fused_layer;
 
+/* An encoding generated inside the fused kernel (a segment with seg_gen = 1 + e). */
+typedef struct nerf_fused_encoding {
+    nerf_pe_params params;     /* as nerf_encode_fwd takes it (ray mode: query, pw_mode) */
+    const float* ray_o;        /* [n_rays][3] */
+    const float* ray_d;        /* [n_rays][3] */
+    const float* t_start;      /* [M] (position encodings) */
+    const float* t_end;        /* [M] (midpoint queries, IPE) */
+    const float* pixel_width;  /* IPE, addressed by params.pw_mode */
+    float* out;                /* rows stored by the layer with seg_gen & 8: [M][ld], or [n_rays][ld]
+                                  when per_ray; NULL: not stored */
+    int64_t ld;
+    int64_t n_rays;
+    int32_t samples_per_ray;   /* sample m belongs to ray m / samples_per_ray */
+    int32_t per_ray;           /* 0: position encoding of o + tq d; 1: encoding of the ray direction */
+    int32_t out_dim;           /* encoding columns (the rest of a 32-column block reads 0) */
+    int32_t reserved;
+} nerf_fused_encoding;
+
+/* encodings: NULL, or 2 entries (generated segments index them) */
 int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_layers, const void* image, int64_t M,
-                       void* stream);
+                       const nerf_fused_encoding* encodings, void* stream);
 
 /* Gather + split packer for the fused image: for i < n, v = srcs[map_src[i] >> 24][map_src[i] & 0xffffff]
  * (0 if map_src[i] < 0); map_dst[i] >= 0: bf16 element index of hi = bf16(v) (lo = bf16(v - hi)

@@ -1,7 +1,19 @@
 // Library-level C-ABI helpers (version, status strings).
 #include "common.h"
 
-extern "C" int nerf_abi_version(void) { return 4; }
+extern "C" int nerf_abi_version(void) { return 5; }
+
+extern "C" int64_t nerf_struct_size(int32_t which) {
+    switch (which) {
+        case 0: return (int64_t)sizeof(nerf_pe_params);
+        case 1: return (int64_t)sizeof(nerf_fused_layer);
+        case 2: return (int64_t)sizeof(nerf_fused_encoding);
+        case 3: return (int64_t)sizeof(nerf_hashgrid_params);
+        case 4: return (int64_t)sizeof(nerf_adam_batch);
+        case 5: return (int64_t)sizeof(nerf_seg);
+        default: return -1;
+    }
+}
 
 extern "C" const char* nerf_status_string(int status) {
     switch (status) {

@@ -755,7 +755,14 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
     const int ntn = (a.N + TB - 1) / TB;
     const int ntk = (a.X.ktot + TB - 1) / TB;
     const int tiles = ntn * ntk;
-    const int bid = blockIdx.x;
+    // XCD-aware block order (speed only): the tiles of one M split read the same dY / X rows, so
+    // they are given consecutive logical ids on blocks that share an XCD (blockIdx % 8, dealt
+    // round-robin) and meet in that XCD's L2 instead of each fetching the rows from HBM (bijective
+    // for any grid size: MI355X guide, XCD swizzle)
+    const int bid = [] {
+        const int nwg = (int)gridDim.x, orig = (int)blockIdx.x, xcd = orig % 8, q = nwg / 8, r = nwg % 8;
+        return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+    }();
     const int split = bid / tiles;
     const int tile = bid - split * tiles;
     const int tn = tile / ntk, tk = tile - (tile / ntk) * ntk;

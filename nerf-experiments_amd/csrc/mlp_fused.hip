@@ -32,8 +32,10 @@
 // is stored; waits are counted (asm fragment reads, a per-layer DMA table in VGPRs) so the
 // prefetch is never drained.
 #include <stddef.h>
+#include <string.h>
 
 #include "common.h"
+#include "encode_common.h"
 
 using namespace nerf;
 
@@ -74,9 +76,18 @@ constexpr int ST_AUX = NERF_FUSED_STORE_AUX;
 // starts: the predecessor's 4 epilogue stores (absent outputs included, as dropped stores) and the
 // bias load at the start of the chunk itself
 constexpr int AFTER_DMA_VM = 1 + 2 * SB;
+// Layer-output stores in chunk pairs (NERF_FUSED_PAIR, default 1): a 16-row chunk is 64 B of each
+// sample row, half a 128-B line.  The even chunk's values wait in registers for the odd one's, and
+// the pair leaves as two stores each covering whole lines of 8 samples (lanes s and s ^ 8 trade
+// halves by a DPP row rotate), not two half-line stores per sample a chunk apart.  Every chunk
+// still issues 2 stores per column block (counted waits assume at least that many).
+#ifndef NERF_FUSED_PAIR
+#define NERF_FUSED_PAIR 1
+#endif
 
 struct FusedArgs {
     nerf_fused_layer L[NERF_FUSED_MAX_LAYERS];
+    nerf_fused_encoding enc[2];
     const char* img;
     int img_bytes;
     int n_layers;
@@ -99,6 +110,12 @@ typedef const uint8_t* cu8ptr_t;
     (*(const __attribute__((address_space(4))) T*)(c.kargs + offsetof(FusedArgs, L) +                        \
                                                    (size_t)(l) * sizeof(nerf_fused_layer) +                  \
                                                    offsetof(nerf_fused_layer, f) + (size_t)(i) * sizeof(T)))
+
+// fields of encoding e (the generated HBM-fed segments), from the kernel-argument segment
+#define EF(T, f, e)                                                                                          \
+    (*(const __attribute__((address_space(4))) T*)(c.kargs + offsetof(FusedArgs, enc) +                      \
+                                                   (size_t)(e) * sizeof(nerf_fused_encoding) +               \
+                                                   offsetof(nerf_fused_encoding, f)))
 
 __device__ __forceinline__ f4 mfma16(bf16x8 a, bf16x8 b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -171,6 +188,7 @@ struct Ctx {
     int t_off, t_units, t_n16, t_next;
     // the current layer's register-fed input (B operand): [32-deep k-block][16-sample column block]
     bf16x8 xh[KBMAX][SB], xl[KBMAX][SB];
+    float dsink;          // diagnostic builds only
 };
 
 __device__ __forceinline__ int dma_units(Ctx& c, int l) { return LF(int, chunk_units, l); }
@@ -214,6 +232,56 @@ __device__ __forceinline__ void issue_dma(Ctx& c, int slot) {
     }
 }
 
+// Arguments of the shared encoding math (encode_common.h) for a generated segment: the encoding's
+// parameters stay in the kernel-argument segment (uniform fields are scalar loads; the per-level
+// mask is indexed per lane and read from there too, never copied to private memory)
+struct GenArgs {
+    const __attribute__((address_space(4))) nerf_pe_params& p;
+    const float *x, *xdir, *o, *d, *t0, *t1, *pw;
+    int S;
+    int64_t n_rays;
+};
+
+// Columns col .. col + 7 of encoding e for sample m (zeros past out_dim and for rows past M), as
+// nerf_encode_fwd computes them (bitwise: the same functions, fp contraction off), split into the
+// bf16 hi/lo operand halves; `store`: also written to the encoding's output rows for the weight
+// gradients (a per-ray encoding by the ray's first sample).
+__device__ __forceinline__ void gen_block(const Ctx& c, int e, bool store, int m, bool ok, int col, bf16x8& h,
+                                          bf16x8& lo) {
+#pragma clang fp contract(off)
+    const int per_ray = EF(int, per_ray, e);
+    const int S = EF(int, samples_per_ray, e);
+    const float* ray_d = EF(cfptr_t, ray_d, e);
+    const GenArgs a{EF(nerf_pe_params, params, e), per_ray ? ray_d : nullptr, nullptr, EF(cfptr_t, ray_o, e), ray_d,
+                    EF(cfptr_t, t_start, e), EF(cfptr_t, t_end, e), EF(cfptr_t, pixel_width, e), S,
+                    EF(int64_t, n_rays, e)};
+    const int out_dim = EF(int, out_dim, e);
+    const int L = a.p.levels, id = a.p.include_identity ? 3 : 0;
+    f8 v = {};
+    if (ok) {
+        const int64_t n = per_ray ? (int64_t)((unsigned)m / (unsigned)S) : (int64_t)m;
+        float p[3], dv[3], pm[3];
+        load_pos_dir(a, n, p, dv);
+        IpeSample q;
+        if (a.p.kind == 1) {
+            q = ipe_sample(a.p, p, dv, a.t0[n], a.t1[n], a.pw ? pixel_width_at(a, n) : 0.f);
+            pm[0] = q.pm[0]; pm[1] = q.pm[1]; pm[2] = q.pm[2];
+        } else {
+            pm[0] = p[0]; pm[1] = p[1]; pm[2] = p[2];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = col + j < out_dim ? enc_column(a.p, L, id, col + j, pm, q) : 0.f;
+        float* out = EF(fptr_t, out, e);
+        if (store && out != nullptr && (!per_ray || (unsigned)m % (unsigned)S == 0u)) {
+            const int64_t ld = EF(int64_t, ld, e);
+            float* r = out + n * ld + col;
+            if (col < ld) *reinterpret_cast<f4*>(r) = v.lo;
+            if (col + 4 < ld) *reinterpret_cast<f4*>(r + 4) = v.hi;
+        }
+    }
+    split8(v, h, lo);
+}
+
 struct LayerState {
     int floor_i;          // ReLU as an integer max on the fp32 bits: 0, or INT_MIN for no ReLU
     int col_chunk;        // 16-row chunk holding the column output (-1: none)
@@ -226,6 +294,12 @@ struct LayerState {
     unsigned mrow_off[SB];    // this lane's 8 bytes of the sample's mask row (OOB past M)
     __amdgpu_buffer_rsrc_t ro, rm, rc, ro2;
     unsigned mw[SB][2];   // ReLU mask words 2g, 2g + 1 of this lane's sample rows
+#if NERF_FUSED_PAIR
+    f4 stash[SB];             // the even chunk's values, stored with the odd chunk's
+    unsigned pa[SB], pb[SB];  // row offsets (+16 g) of the samples this lane writes in the pair's
+    unsigned pa2[SB], pb2[SB];  // stores A (samples 0-7 of the block) and B (8-15), in out / out2
+    int last_even;            // NC - 1 for an odd chunk count (stored alone), else -1
+#endif
     unsigned mi[SB][8];   // mask_in: the sample rows of those bits
 };
 
@@ -239,6 +313,39 @@ __device__ __forceinline__ void split2(float x, float y, unsigned& hi, unsigned&
     lo = __builtin_bit_cast(unsigned, __builtin_convertvector((f4{x - hx, y - hy, 0.f, 0.f}).xy, bf16x2));
 }
 
+#if NERF_FUSED_PAIR
+__device__ __forceinline__ bool pair_odd(int ch) { return ch >= 0 && (ch & 1) != 0; }
+
+__device__ __forceinline__ float ror8(float x) {      // lane (s ^ 8) of this lane's 16-lane row
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x128, 0xf, 0xf, false));
+}
+
+// The two stores of chunk pair (ch - 1, ch), ch odd (chunk indices local to the output): lane (s, g)
+// holds x = columns 4 g .. 4 g + 3 of chunk ch - 1 (stashed) and y = those of chunk ch, for sample
+// s.  Store A writes the whole 128-B line segment of samples 0-7 (lanes s < 8: their own x; lanes
+// s >= 8: y of sample s - 8), store B that of samples 8-15 (lanes s < 8: x of sample s + 8; lanes
+// s >= 8: their own y).
+__device__ __forceinline__ void pair_stores(const Ctx& c, const LayerState& st, int sb, int ch, int colok,
+                                            unsigned pa, unsigned pb, const f4& y, f4& va, f4& vb, unsigned& oa,
+                                            unsigned& ob) {
+    const f4 x = st.stash[sb];
+    const bool lo8 = (c.lane & 8) == 0;
+    f4 rx, ry;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float xr = x[r], yr = y[r];
+        rx[r] = ror8(xr);
+        ry[r] = ror8(yr);
+    }
+    va = lo8 ? x : ry;
+    vb = lo8 ? rx : y;
+    const int cl = lo8 ? ch - 1 : ch;                 // the chunk this lane writes in both stores
+    const bool inr = 16 * cl < colok;
+    oa = inr ? pa + 64u * (unsigned)cl : OOB;
+    ob = inr ? pb + 64u * (unsigned)cl : OOB;
+}
+#endif
+
 // Epilogue of 16-row chunk ch (output rows 16 ch .. 16 ch + 15; ch = -1: none, the stores are
 // dropped), in four parts placed between the next chunk's MFMA stages: 0 / 1 = the values of column
 // block 0 / 1 (FWD: bias + ReLU; DGRAD: times the ReLU bits) and their fp32 stores; 2 = ReLU mask
@@ -247,6 +354,16 @@ template <int MODE>
 __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, f4 (&a)[SB], f4 b) {
 #ifdef NERF_FUSED_NOEPI           // diagnostic builds only (timing without the chunk epilogues)
     return;
+#endif
+#ifdef NERF_FUSED_DIAG_MFMAONLY   // diagnostic: the epilogue reduced to one add (the MFMAs stay live)
+    if (p == 0) c.dsink += a[0][0] + a[0][3];
+    return;
+#endif
+#ifdef NERF_FUSED_DIAG_NOMASK     // diagnostic: no ReLU mask bits
+    if (p == 2) return;
+#endif
+#ifdef NERF_FUSED_DIAG_NOSPLIT    // diagnostic: no next-operand split / image writes
+    if (p == 3) return;
 #endif
     const int g = c.lane >> 4;
     const int q = ch >> 1, bb = ch & 1;
@@ -258,10 +375,33 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 v[r] = __builtin_bit_cast(float, max(__builtin_bit_cast(int, v[r] + b[r]), st.floor_i));
+#if NERF_FUSED_PAIR
+            if (!pair_odd(ch)) {
+                // even chunk: held for the pair (alone if it is the layer's last); the column output
+                // (col_idx is a multiple of 32: always an even chunk)
+                st.stash[sb] = v;
+                const unsigned off =
+                    ch >= 0 && ch == st.last_even && 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
+                __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, off, 0, ST_AUX);
+                const unsigned coff = ch == st.col_chunk ? st.sample_off[sb] : OOB;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), st.rc, coff, 0, 0);
+            } else {
+                f4 va, vb;
+                unsigned oa, ob;
+                pair_stores(c, st, sb, ch, st.colok, st.pa[sb], st.pb[sb], v, va, vb, oa, ob);
+                __builtin_amdgcn_raw_buffer_store_b128(va, st.ro, oa, 0, ST_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(vb, st.ro, ob, 0, ST_AUX);
+            }
+#else
             const unsigned off = ch >= 0 && 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
+#ifndef NERF_FUSED_DIAG_NOSTORE   // diagnostic: no layer-output stores
             __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, off, 0, ST_AUX);
             const unsigned coff = ch == st.col_chunk ? st.sample_off[sb] : OOB;
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), st.rc, coff, 0, 0);
+#else
+            (void)off;
+#endif
+#endif
         } else {
             const bool sec = ch >= st.n1;          // an encoding input's rows (out2): not masked
             // column 16 ch + 4 g + r = 32 q + 16 bb + 4 g + r is bit 8 (q & 3) + 4 bb + g of word
@@ -278,17 +418,44 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
                 const float x = v[r];
                 v[r] = __builtin_bit_cast(float, __builtin_bit_cast(int, x) & keep);
             }
+#if NERF_FUSED_PAIR
+            if (!pair_odd(ch)) {
+                // even chunk: held for the pair (alone if it is the layer's last); n1 is even, so
+                // both chunks of a pair go to the same output
+                st.stash[sb] = v;
+                const bool alone = ch >= 0 && ch == st.last_even;
+                const unsigned off1 = alone && !sec && 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
+                const unsigned off2 =
+                    alone && sec && 16 * (ch - st.n1) < st.colok2 ? st.row_off2[sb] + 64u * (unsigned)(ch - st.n1) : OOB;
+                __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, off1, 0, ST_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(v, st.ro2, off2, 0, ST_AUX);
+            } else if (!sec) {
+                f4 va, vb;
+                unsigned oa, ob;
+                pair_stores(c, st, sb, ch, st.colok, st.pa[sb], st.pb[sb], v, va, vb, oa, ob);
+                __builtin_amdgcn_raw_buffer_store_b128(va, st.ro, oa, 0, ST_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(vb, st.ro, ob, 0, ST_AUX);
+            } else {
+                f4 va, vb;
+                unsigned oa, ob;
+                pair_stores(c, st, sb, ch - st.n1, st.colok2, st.pa2[sb], st.pb2[sb], v, va, vb, oa, ob);
+                __builtin_amdgcn_raw_buffer_store_b128(va, st.ro2, oa, 0, ST_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(vb, st.ro2, ob, 0, ST_AUX);
+            }
+#else
             // one store to each output, the one not addressed dropped (a select of the two resources
             // or offsets here becomes a runtime-indexed private array, i.e. scratch)
             const unsigned off1 = !sec && ch >= 0 && 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
             const unsigned off2 = sec && 16 * (ch - st.n1) < st.colok2 ? st.row_off2[sb] + 64u * (unsigned)(ch - st.n1) : OOB;
             __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, off1, 0, ST_AUX);
             __builtin_amdgcn_raw_buffer_store_b128(v, st.ro2, off2, 0, ST_AUX);
+#endif
         }
     } else if (p == 2) {
         if constexpr (MODE == MODE_FWD) {
             // NERF_EPI_MASKOUT layout; byte r of t collects row r's bits over the lane groups, lane
-            // group g keeps the byte of r = g
+            // group g keeps the byte of r = g (a variant setting each lane's own bits in 8 words and
+            // OR-ing the lanes once per layer measured 0.13 ms slower per mip step)
             const unsigned keep = (ch >= 0 && ch < 2 * KBMAX) ? 0xffu : 0u;
 #pragma unroll
             for (int sb = 0; sb < SB; ++sb) {
@@ -323,16 +490,33 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
     }
 }
 
+// k-steps of weight fragments read ahead of the step being multiplied
+#ifndef NERF_FUSED_FA
+#define NERF_FUSED_FA 2
+#endif
+constexpr int FA = NERF_FUSED_FA;
+
+// the chunk's first min(FA, KBR) steps' fragment reads (compile-time LDS offsets)
+template <int KBR, int I>
+__device__ __forceinline__ void first_reads(bf16x8 (&fr)[FA][2], unsigned sa) {
+    if constexpr (I < FA && I < KBR) {
+        lds_frag<I * 2048>(fr[I][0], sa);
+        lds_frag<I * 2048 + 1024>(fr[I][1], sa);
+        first_reads<KBR, I + 1>(fr, sa);
+    }
+}
+
 // One 16-row chunk's register-fed k-blocks (compile-time KB_I: immediate LDS offsets), fragments
-// read two steps ahead; the previous chunk's epilogue parts 0-2 at stages EPI0 .. EPI0 + 2.
+// read FA steps ahead; the previous chunk's epilogue parts 0-2 at stages EPI0 .. EPI0 + 2.
 template <int MODE, int KBR, int KBH, int KB_I>
-__device__ __forceinline__ void reg_steps(Ctx& c, LayerState& st, unsigned sa, bf16x8 (&fr)[2][2], f4 (&a)[SB],
+__device__ __forceinline__ void reg_steps(Ctx& c, LayerState& st, unsigned sa, bf16x8 (&fr)[FA][2], f4 (&a)[SB],
                                           f4 (&pv)[SB], f4& pb, int ch) {
     constexpr int EPI0 = KBR >= 8 ? 4 : (KBR >= 4 ? 1 : 0);
     if constexpr (KB_I < KBR) {
-        bf16x8(&f)[2] = fr[KB_I & 1];
-        // this step's fragments have landed (the next step's two reads may still be in flight)
-        lds_wait<(KB_I + 1 < KBR ? 2 : 0)>(f[0], f[1]);
+        bf16x8(&f)[2] = fr[KB_I % FA];
+        // this step's fragments have landed (the reads of the steps after it may still be in flight)
+        constexpr int later = (KB_I + FA - 1 < KBR - 1 ? KB_I + FA - 1 : KBR - 1) - KB_I;
+        lds_wait<2 * later>(f[0], f[1]);
         // products lo*hi + hi*lo + hi*hi per accumulator (small terms first, as linear_x3.hip)
 #pragma unroll
         for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(f[1], c.xh[KB_I][sb], a[sb]);
@@ -340,9 +524,9 @@ __device__ __forceinline__ void reg_steps(Ctx& c, LayerState& st, unsigned sa, b
         for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(f[0], c.xl[KB_I][sb], a[sb]);
 #pragma unroll
         for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(f[0], c.xh[KB_I][sb], a[sb]);
-        if constexpr (KB_I + 2 < KBR) {
-            lds_frag<(KB_I + 2) * 2048>(f[0], sa);
-            lds_frag<(KB_I + 2) * 2048 + 1024>(f[1], sa);
+        if constexpr (KB_I + FA < KBR) {
+            lds_frag<(KB_I + FA) * 2048>(f[0], sa);
+            lds_frag<(KB_I + FA) * 2048 + 1024>(f[1], sa);
         }
         if constexpr (KB_I == EPI0) bias_wait<(KBR > 0 ? DMA_PER_WAVE : 0) + 2 * KBH>(pb);
         if constexpr (KB_I >= EPI0 && KB_I < EPI0 + 3) epi_part<MODE>(c, st, KB_I - EPI0, ch - 1, pv, pb);
@@ -363,6 +547,9 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
     const int ldo = (int)LF(int64_t, ldo, l);
     st.floor_i = LF(int, relu, l) != 0 ? 0 : (int)0x80000000;
     st.colok = ldo - 4 * g;
+#if NERF_FUSED_PAIR
+    st.last_even = (NC & 1) ? NC - 1 : -1;
+#endif
     int sample[SB];
     bool row_ok[SB];
 #pragma unroll
@@ -372,6 +559,14 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
         st.row_off[sb] = row_ok[sb] ? (unsigned)sample[sb] * (unsigned)ldo * 4u + 16u * g : OOB;
         st.sample_off[sb] = row_ok[sb] && g == 0 ? (unsigned)sample[sb] * 4u : OOB;
         st.mrow_off[sb] = row_ok[sb] ? (unsigned)sample[sb] * 32u + 8u * g : OOB;
+#if NERF_FUSED_PAIR
+        {
+            const int sa = (c.lane & 8) == 0 ? sample[sb] : sample[sb] - 8;   // store A's sample
+            const int sbb = sa + 8;                                           // store B's
+            st.pa[sb] = sa < c.M ? (unsigned)sa * (unsigned)ldo * 4u + 16u * g : OOB;
+            st.pb[sb] = sbb < c.M ? (unsigned)sbb * (unsigned)ldo * 4u + 16u * g : OOB;
+        }
+#endif
         st.mw[sb][0] = st.mw[sb][1] = 0;
     }
     st.ro = __builtin_amdgcn_make_buffer_rsrc(LF(fptr_t, out, l), 0, c.M * ldo * 4, RSRC_W3);
@@ -392,6 +587,15 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
 #pragma unroll
         for (int sb = 0; sb < SB; ++sb)
             st.row_off2[sb] = row_ok[sb] ? (unsigned)sample[sb] * (unsigned)ldo2 * 4u + 16u * g : OOB;
+#if NERF_FUSED_PAIR
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb) {
+            const int sa = (c.lane & 8) == 0 ? sample[sb] : sample[sb] - 8;
+            const int sbb = sa + 8;
+            st.pa2[sb] = sa < c.M ? (unsigned)sa * (unsigned)ldo2 * 4u + 16u * g : OOB;
+            st.pb2[sb] = sbb < c.M ? (unsigned)sbb * (unsigned)ldo2 * 4u + 16u * g : OOB;
+        }
+#endif
         const uint8_t* mi = LF(cu8ptr_t, mask_in, l);
         const __amdgpu_buffer_rsrc_t rmi =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(mi), 0, mi != nullptr ? c.M * 32 : 0, RSRC_W3);
@@ -419,6 +623,14 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
         for (int kh = 0; kh < KBH; ++kh) {
             const int sg = kh < kb0 ? 0 : 1;            // segment of this block
             const int khl = sg ? kh - kb0 : kh;
+            const int gen = MODE != MODE_FWD ? 0 : sg ? LFI(int, seg_gen, 1, l) : LFI(int, seg_gen, 0, l);
+            if (gen != 0) {                             // generated in-kernel (encodings[gen & 7 - 1])
+#pragma unroll
+                for (int sb = 0; sb < SB; ++sb)
+                    gen_block(c, (gen & 7) - 1, (gen & 8) != 0, sample[sb], row_ok[sb], 32 * khl + 8 * g,
+                              hh[kh][sb], hl[kh][sb]);
+                continue;
+            }
             const float* p = sg ? LFI(cfptr_t, seg_ptr, 1, l) : LFI(cfptr_t, seg_ptr, 0, l);
             const int64_t ld = sg ? LFI(int64_t, seg_ld, 1, l) : LFI(int64_t, seg_ld, 0, l);
             const int k = sg ? LFI(int, seg_k, 1, l) : LFI(int, seg_k, 0, l);
@@ -451,7 +663,7 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
         else
             buf_load16(pb, st.bias_off, c.rimg);     // (zero biases: the load only keeps the count)
         const unsigned sa = lds_addr(c.smem + c.cur * SLOT_BYTES + c.lane * 16);
-        bf16x8 fr[2][2];
+        bf16x8 fr[FA][2];
         if constexpr (KBR > 0) {
             // this chunk's DMA share has landed (issued at the start of the previous register-fed
             // chunk and followed by >= AFTER_DMA_VM vector-memory ops), then everyone else's; the
@@ -460,12 +672,7 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
 #ifndef NERF_FUSED_NOBARRIER      // diagnostic builds only (timing without the per-chunk barrier)
             barrier();
 #endif
-            lds_frag<0>(fr[0][0], sa);
-            lds_frag<1024>(fr[0][1], sa);
-            if (KBR > 1) {
-                lds_frag<2048>(fr[1][0], sa);
-                lds_frag<3072>(fr[1][1], sa);
-            }
+            first_reads<KBR, 0>(fr, sa);
             issue_dma(c, c.cur ^ 1);                 // the next register-fed chunk, a whole chunk ahead
             __builtin_amdgcn_sched_barrier(0);      // keep the DMA ahead of this chunk's vmem ops (vmcnt)
         }
@@ -537,6 +744,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
     c.lane = threadIdx.x & 63;
     c.M = a.M;
     c.n_layers = a.n_layers;
+    c.dsink = 0.f;
     if ((int)blockIdx.x >= a.ntiles) return;
     const int my_tiles = (a.ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
     int per_tile = 0;
@@ -577,9 +785,13 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
             }
         }
     }
+#ifdef NERF_FUSED_DIAG_MFMAONLY
+    if (c.dsink == 1234.5f) LF(fptr_t, out, 0)[threadIdx.x] = c.dsink;   // keeps the MFMAs live
+#endif
 }
 #undef LF
 #undef LFI
+#undef EF
 
 struct PackArgs {
     const float* src[NERF_FUSED_MAX_SRCS];
@@ -623,8 +835,34 @@ int num_cus() {
 
 }  // namespace
 
+namespace {
+int enc_out_dim(const nerf_pe_params& p) { return (2 * p.levels + (p.include_identity ? 1 : 0)) * 3; }
+
+// a generated segment's encoding, checked as nerf_encode_fwd checks its arguments
+bool encoding_ok(const nerf_fused_encoding& e, int64_t M) {
+    const nerf_pe_params& p = e.params;
+    if (!(p.levels >= 0 && p.levels <= 16 && (p.kind == 0 || p.kind == 1))) return false;
+    if (e.out_dim != enc_out_dim(p) || e.out_dim <= 0 || e.samples_per_ray < 1 || e.n_rays < 1) return false;
+    if (e.n_rays * e.samples_per_ray < M || M >= ((int64_t)1 << 31)) return false;
+    if (e.ray_d == nullptr) return false;
+    if (e.per_ray) {
+        if (p.kind != 0) return false;                       // nerf_encode_rays: plain Fourier features
+    } else {
+        if (e.ray_o == nullptr || e.t_start == nullptr || (p.query != 0 && e.t_end == nullptr)) return false;
+        if (p.kind == 1 && (e.t_end == nullptr || e.pixel_width == nullptr || p.pw_mode < 0 || p.pw_mode > 2))
+            return false;
+    }
+    if (e.out != nullptr) {
+        const int64_t rows = e.per_ray ? e.n_rays : M;
+        if (!aligned16(e.out) || e.ld % 4 != 0 || e.ld < e.out_dim || rows * e.ld * 4 >= ((int64_t)1 << 31))
+            return false;
+    }
+    return true;
+}
+}  // namespace
+
 extern "C" int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_layers, const void* image, int64_t M,
-                                  void* stream) {
+                                  const nerf_fused_encoding* encodings, void* stream) {
     NERF_REQUIRE(layers != nullptr && image != nullptr);
     NERF_REQUIRE(n_layers >= 1 && n_layers <= NERF_FUSED_MAX_LAYERS);
     NERF_REQUIRE(M >= 1 && M <= (int64_t)1 << 30);
@@ -666,12 +904,22 @@ extern "C" int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_laye
                                            L.n1 <= L.nb && M * L.ldo2 * 4 < ((int64_t)1 << 31)));
         NERF_REQUIRE(L.nseg >= 0 && L.nseg <= 2);
         int kbs = 0;
+        for (int s = 0; s < 2; ++s) {
+            const int gen = s < L.nseg ? L.seg_gen[s] : 0;
+            NERF_REQUIRE(s < L.nseg || L.seg_gen[s] == 0);
+            if (gen == 0) continue;
+            // generated: encodings[e] (e = (gen & 7) - 1), its columns within the segment's blocks
+            NERF_REQUIRE(!dgrad && encodings != nullptr && (gen & ~15) == 0 && ((gen & 7) == 1 || (gen & 7) == 2));
+            const nerf_fused_encoding& e = encodings[(gen & 7) - 1];
+            NERF_REQUIRE(encoding_ok(e, M) && e.out_dim <= 32 * L.seg_kb[s]);
+        }
         for (int s = 0; s < L.nseg; ++s) {
+            kbs += L.seg_kb[s];
+            if (L.seg_gen[s] != 0) continue;
             NERF_REQUIRE(L.seg_ptr[s] != nullptr && aligned16(L.seg_ptr[s]));
             NERF_REQUIRE(L.seg_k[s] % 4 == 0 && L.seg_k[s] <= 32 * L.seg_kb[s] && L.seg_ld[s] % 4 == 0);
             NERF_REQUIRE(L.seg_ld[s] >= L.seg_k[s] && L.seg_rd[s] >= 1 && L.seg_rows[s] >= (M + L.seg_rd[s] - 1) / L.seg_rd[s]);
             NERF_REQUIRE((int64_t)L.seg_rows[s] * L.seg_ld[s] * 4 < ((int64_t)1 << 31));
-            kbs += L.seg_kb[s];
         }
         NERF_REQUIRE(kbs == kbh);
         if (l > 0) {
@@ -683,9 +931,15 @@ extern "C" int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_laye
         if (L.nseg < 2) {
             a.L[l].seg_kb[1] = 0;
             a.L[l].seg_ptr[1] = L.nseg == 1 ? L.seg_ptr[0] : nullptr;
+            a.L[l].seg_gen[1] = 0;
         }
+        if (L.nseg < 1) a.L[l].seg_gen[0] = 0;
     }
     NERF_REQUIRE(img_end < ((int64_t)1 << 31));
+    for (int e = 0; e < 2; ++e) {
+        if (encodings != nullptr) a.enc[e] = encodings[e];
+        else memset(&a.enc[e], 0, sizeof(a.enc[e]));
+    }
     a.img = static_cast<const char*>(image);
     a.img_bytes = (int)img_end;
     a.n_layers = n_layers;

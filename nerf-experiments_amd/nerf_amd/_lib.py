@@ -112,6 +112,25 @@ class NerfFusedLayer(ctypes.Structure):
         ("ldo2", c_i64),
         ("n1", c_i32),
         ("hbm_off", c_i32),
+        ("seg_gen", c_i32 * 2),
+    ]
+
+
+class NerfFusedEncoding(ctypes.Structure):
+    _fields_ = [
+        ("params", NerfPEParams),
+        ("ray_o", c_vp),
+        ("ray_d", c_vp),
+        ("t_start", c_vp),
+        ("t_end", c_vp),
+        ("pixel_width", c_vp),
+        ("out", c_vp),
+        ("ld", c_i64),
+        ("n_rays", c_i64),
+        ("samples_per_ray", c_i32),
+        ("per_ray", c_i32),
+        ("out_dim", c_i32),
+        ("reserved", c_i32),
     ]
 
 
@@ -170,7 +189,9 @@ _SIGNATURES = {
                                      c_i32, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_sz, c_vp]),
     "nerf_linear_wgrad_x3": (c_i32, [c_vp, c_i64, c_i32, ctypes.POINTER(NerfSeg), c_i32, c_i64, c_vp, c_sz, c_vp]),
     "nerf_pack_weight_x3": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
-    "nerf_mlp_fused_fwd": (c_i32, [ctypes.POINTER(NerfFusedLayer), c_i32, c_vp, c_i64, c_vp]),
+    "nerf_mlp_fused_fwd": (c_i32, [ctypes.POINTER(NerfFusedLayer), c_i32, c_vp, c_i64,
+                                   ctypes.POINTER(NerfFusedEncoding), c_vp]),
+    "nerf_struct_size": (c_i64, [c_i32]),
     "nerf_fused_pack": (c_i32, [ctypes.POINTER(c_vp), c_i32, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "nerf_hashgrid_fwd": (c_i32, [ctypes.POINTER(NerfHashgridParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
                                   c_vp, c_vp, c_i64, c_vp]),
@@ -190,6 +211,8 @@ _SIGNATURES = {
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES.keys())
+# argument structs in nerf_struct_size's order (their sizes are checked against the library at load)
+STRUCTS = (NerfPEParams, NerfFusedLayer, NerfFusedEncoding, NerfHashgridParams, NerfAdamBatch, NerfSeg)
 
 _lib = None
 
@@ -209,8 +232,11 @@ def load(path: str | None = None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.nerf_abi_version() != 4:
+    if lib.nerf_abi_version() != 5:
         raise RuntimeError("nerf_amd: ABI version mismatch between Python binding and libnerf_amd.so")
+    for which, st in enumerate(STRUCTS):
+        if lib.nerf_struct_size(which) != ctypes.sizeof(st):
+            raise RuntimeError(f"nerf_amd: {st.__name__} layout differs from libnerf_amd.so's")
     if path is None:
         _lib = lib
     return lib

@@ -213,7 +213,11 @@ def make_pe_params(kind: int, levels: int, include_identity: bool, scale: float,
 
 def encode_fwd(params: NerfPEParams, out_dim: int, *, x=None, xdir=None, ray_o=None, ray_d=None, t_start=None,
                t_end=None, pixel_width=None, n_samples: int, samples_per_ray: int = 1, n_rays: int = 0,
-               out_ld: int | None = None, device=None) -> torch.Tensor:
+               out_ld: int | None = None, device=None, defer: bool = False) -> torch.Tensor:
+    """[n_samples, out_ld] encoding (nerf_encode_fwd).  defer=True: when the encoding can be generated
+    inside the fused field-MLP kernel (ray-mode positions, or per-ray Fourier features of
+    directions), the rows are left to that kernel: the tensor is returned unfilled, carrying a
+    DeferredEncoding that the consumer either hands to the kernel or fills (see materialize)."""
     ld = out_ld if out_ld is not None else pad32(out_dim)
     for name, t in (("x", x), ("dir", xdir), ("ray_origs", ray_o), ("ray_dirs", ray_d), ("t_start", t_start),
                     ("t_end", t_end), ("pixel_width", pixel_width)):
@@ -222,25 +226,73 @@ def encode_fwd(params: NerfPEParams, out_dim: int, *, x=None, xdir=None, ray_o=N
             if not t.is_contiguous():
                 raise ValueError(f"{name} must be contiguous")
     out = torch.empty(n_samples, ld, device=device, dtype=torch.float32)
-    end = None
-    if TIMER is not None:
-        # algorithmic bytes: the encoding's out_dim columns written, its inputs read once
-        per_sample = 4 * out_dim
-        if x is not None:
-            per_sample += 12 + (12 if params.kind == 1 else 0) + (12 if params.kind == 1 else 0)
-            per_ray = 0
+
+    def fill():
+        end = None
+        if TIMER is not None:
+            # algorithmic bytes: the encoding's out_dim columns written, its inputs read once
+            per_sample = 4 * out_dim
+            if x is not None:
+                per_sample += 12 + (12 if params.kind == 1 else 0) + (12 if params.kind == 1 else 0)
+                per_ray = 0
+            else:
+                per_sample += 4 + (4 if (params.query == 1 or params.kind == 1) else 0)
+                per_ray = 24 + (4 if params.kind == 1 else 0)
+            end = TIMER.bracket("encode_fwd", nbytes=n_samples * per_sample + n_rays * per_ray,
+                                fn="encode_fwd_lds_kernel" if ld <= 128 else "encode_fwd_kernel")
+        st = _lib.load().nerf_encode_fwd(ctypes.byref(params), _ptr(x), _ptr(xdir), _ptr(ray_o), _ptr(ray_d),
+                                         _ptr(t_start), _ptr(t_end), _ptr(pixel_width), n_samples, samples_per_ray,
+                                         n_rays, _ptr(out), ld, _stream(out.device))
+        if end is not None:
+            end.record()
+        _lib.check(st, "nerf_encode_fwd")
+
+    if defer and n_samples > 0 and (x is None or (xdir is None and params.kind == 0)):
+        e = _lib.NerfFusedEncoding()
+        e.params = params
+        if x is None:
+            e.ray_o, e.ray_d, e.t_start, e.t_end = _ptr(ray_o), _ptr(ray_d), _ptr(t_start), _ptr(t_end)
+            e.pixel_width = _ptr(pixel_width)
+            e.samples_per_ray, e.n_rays, e.per_ray = samples_per_ray, n_rays, 0
         else:
-            per_sample += 4 + (4 if (params.query == 1 or params.kind == 1) else 0)
-            per_ray = 24 + (4 if params.kind == 1 else 0)
-        end = TIMER.bracket("encode_fwd", nbytes=n_samples * per_sample + n_rays * per_ray,
-                            fn="encode_fwd_lds_kernel" if ld <= 128 else "encode_fwd_kernel")
-    st = _lib.load().nerf_encode_fwd(ctypes.byref(params), _ptr(x), _ptr(xdir), _ptr(ray_o), _ptr(ray_d),
-                                     _ptr(t_start), _ptr(t_end), _ptr(pixel_width), n_samples, samples_per_ray,
-                                     n_rays, _ptr(out), ld, _stream(out.device))
-    if end is not None:
-        end.record()
-    _lib.check(st, "nerf_encode_fwd")
+            # per-row features of x (directions): generated per sample from ray m / samples_per_ray,
+            # the divisor being the consumer's (set when the kernel is launched)
+            e.ray_d = _ptr(x)
+            e.samples_per_ray, e.n_rays, e.per_ray = 1, n_samples, 1
+        e.out, e.ld, e.out_dim = _ptr(out), ld, out_dim
+        out._nerf_deferred = DeferredEncoding(e, (x, ray_o, ray_d, t_start, t_end, pixel_width, out), fill)
+        return out
+    fill()
     return out
+
+
+class DeferredEncoding:
+    """The pending rows of an encoding output: ``spec`` (nerf_fused_encoding: what the fused field
+    MLP needs to generate them in-kernel; its pointers stay valid through ``keep``) and ``fill`` (the
+    stand-alone encoding launch, for any other consumer)."""
+
+    __slots__ = ("spec", "keep", "fill")
+
+    def __init__(self, spec, keep, fill):
+        self.spec, self.keep, self.fill = spec, keep, fill
+
+
+def deferred(t) -> "DeferredEncoding | None":
+    return getattr(t, "_nerf_deferred", None) if t is not None else None
+
+
+def materialize(t) -> None:
+    """Fill a deferred encoding's rows now (no-op for an ordinary tensor)."""
+    d = deferred(t)
+    if d is not None:
+        t._nerf_deferred = None
+        d.fill()
+
+
+def mark_filled(t) -> None:
+    """The fused kernel has written a deferred encoding's rows."""
+    if deferred(t) is not None:
+        t._nerf_deferred = None
 
 
 def encode_bwd(params: NerfPEParams, x: torch.Tensor, grad_out: torch.Tensor, dx: torch.Tensor | None = None,

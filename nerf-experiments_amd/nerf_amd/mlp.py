@@ -270,10 +270,16 @@ class MLPFunction(torch.autograd.Function):
                 masks.append(torch.empty(M, 32, device=pos.device, dtype=torch.uint8)
                              if keep_all and lp.relu and plan.consumed[idx] and lp.N <= 256 else None)
             col_t = {li: torch.empty(M, device=pos.device, dtype=torch.float32) for li, _ in plan.column_outputs}
-            fused.run(M, pos, dirs, dir_rd, acts, masks, col_t)
+            # deferred encodings (render_raw) are generated by the kernel itself, their rows stored by
+            # the first layer that reads them
+            fused.run(M, pos, dirs, dir_rd, acts, masks, col_t, (K.deferred(pos), K.deferred(dirs)))
+            K.mark_filled(pos)
+            K.mark_filled(dirs)
             cols = tuple(col_t[li] for li, _ in plan.column_outputs)
             ctx.fused_forward = True
         else:
+            K.materialize(pos)
+            K.materialize(dirs)
             for idx, lp in enumerate(plan.layers):
                 lp.pack(prec)
                 segs = []

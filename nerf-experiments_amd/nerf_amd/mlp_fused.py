@@ -202,14 +202,30 @@ class FusedForward:
     def pack(self):
         _pack_image(self)
 
-    def run(self, M: int, pos: torch.Tensor, dirs: torch.Tensor | None, dir_rd: int, acts, masks, col_outs):
+    def run(self, M: int, pos: torch.Tensor, dirs: torch.Tensor | None, dir_rd: int, acts, masks, col_outs,
+            gens=(None, None)):
         """Launch on the current stream.  acts[l]: [M, out_ld] fp32 or None (not stored),
-        masks[l]: [M, 32] uint8 or None, col_outs: {layer: [M] fp32}."""
+        masks[l]: [M, 32] uint8 or None, col_outs: {layer: [M] fp32}.  gens: the DeferredEncoding
+        of pos / dirs or None: generated in-kernel (kernels.encode_fwd(defer=True)); the first layer
+        reading one also writes its rows into the tensor."""
         self.pack()
         L = len(self.plan.layers)
         descs = (_lib.NerfFusedLayer * L)()
+        encs = (_lib.NerfFusedEncoding * 2)()
+        gen_of = {}
+        for e, (kind, g) in enumerate((("pos", gens[0]), ("dir", gens[1]))):
+            if g is None:
+                continue
+            if not any(s.kind == kind for idx in range(L) for s in self.layers[idx][2]):
+                K.materialize(pos if kind == "pos" else dirs)      # not read by the kernel
+                continue
+            ctypes.memmove(ctypes.byref(encs[e]), ctypes.byref(g.spec), ctypes.sizeof(g.spec))
+            if kind == "dir":
+                encs[e].samples_per_ray = dir_rd
+            gen_of[kind] = e + 1
         flops = 0.0
         nbytes = 0.0
+        stored = set()
         for idx, lp in enumerate(self.plan.layers):
             kbr, kbh, hbm, nb, n16, off, hbm_off, bias_off = self.layers[idx]
             d = descs[idx]
@@ -226,6 +242,18 @@ class FusedForward:
                 d.seg_rows[si] = t.shape[0]
                 d.seg_ld[si] = t.stride(0)
                 d.seg_ptr[si] = t.data_ptr()
+                e = gen_of.get(s.kind, 0)
+                if e:
+                    d.seg_gen[si] = e | (8 if s.kind not in stored else 0)
+                    if s.kind not in stored:
+                        stored.add(s.kind)
+                        # rows written once; the inputs (t_start [, t_end] per sample, o, d [, pw] per ray)
+                        nbytes += 4.0 * t.stride(0) * t.shape[0]
+                    spec = encs[e - 1]
+                    nbytes += (8.0 * M + 28.0 * spec.n_rays) if not spec.per_ray else 12.0 * spec.n_rays
+                else:
+                    # algorithmic bytes: an HBM-fed encoding read
+                    nbytes += 4.0 * d.seg_k[si] * d.seg_rows[si]
             d.chunk_units = 2 * kbr
             d.col_idx = -1
             # a layer without a tensor (inference: not an exposed output) has its stores dropped
@@ -239,14 +267,14 @@ class FusedForward:
             d.hbm_off = hbm_off
             d.bias_off = bias_off
             flops += 2.0 * M * lp.module.out_features * lp.module.in_features
-            # algorithmic bytes: HBM-fed encodings read, stored outputs / mask bits / columns written
-            nbytes += sum(4.0 * d.seg_k[si] * d.seg_rows[si] for si in range(d.nseg))
+            # algorithmic bytes: stored outputs / mask bits / columns written
             nbytes += (4.0 * M * acts[idx].shape[1] if acts[idx] is not None else 0.0) \
                 + (32.0 * M if masks[idx] is not None else 0.0) + (4.0 * M if idx in col_outs else 0.0)
         end = K.TIMER.bracket("mlp_fused_fwd", flops, nbytes + self.image.numel() * self.image.element_size(),
                               fn="mlp_fused_kernel<0>") \
             if K.TIMER is not None else None
-        st = _lib.load().nerf_mlp_fused_fwd(descs, L, self.image.data_ptr(), M, K._stream(self.device))
+        st = _lib.load().nerf_mlp_fused_fwd(descs, L, self.image.data_ptr(), M, encs if gen_of else None,
+                                            K._stream(self.device))
         if end is not None:
             end.record()
         _lib.check(st, "nerf_mlp_fused_fwd")
@@ -436,7 +464,7 @@ class FusedInputGrad:
         end = K.TIMER.bracket("mlp_fused_dgrad", flops, nbytes + self.image.numel() * self.image.element_size(),
                               fn="mlp_fused_kernel<1>") \
             if K.TIMER is not None else None
-        st = _lib.load().nerf_mlp_fused_fwd(descs, S, self.image.data_ptr(), M, K._stream(self.device))
+        st = _lib.load().nerf_mlp_fused_fwd(descs, S, self.image.data_ptr(), M, None, K._stream(self.device))
         if end is not None:
             end.record()
         _lib.check(st, "nerf_mlp_fused_fwd (input-gradient chain)")

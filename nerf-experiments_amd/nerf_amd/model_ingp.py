@@ -196,15 +196,17 @@ class INGPEncoding(nn.Module):
                                  t_start, t_end, samples_per_ray, n, *tables)
 
     # -- kernel-facing API (the NerfModel lowering's encoder interface) -------------------------
-    def encode_padded(self, x: th.Tensor, dir=None, pixel_width=None, t_start=None, t_end=None) -> th.Tensor:
-        """[N, pad32(output_dim)] features of explicit positions x [N, 3]."""
+    def encode_padded(self, x: th.Tensor, dir=None, pixel_width=None, t_start=None, t_end=None,
+                      defer: bool = False) -> th.Tensor:
+        """[N, pad32(output_dim)] features of explicit positions x [N, 3] (defer: accepted, ignored —
+        hash features are never generated inside the fused MLP)."""
         if x.dim() != 2 or x.shape[1] != 3:
             raise ValueError(f"x must be [N, 3] (got {tuple(x.shape)})")
         x = x.detach().contiguous()
         return self._run(x, None, None, None, None, 1, 1, x.shape[0])
 
     def encode_rays(self, ray_origs, ray_dirs, t_start, t_end, pixel_width, samples_per_ray: int, query: int,
-                    pw_mode: int = 0) -> th.Tensor:
+                    pw_mode: int = 0, defer: bool = False) -> th.Tensor:
         """Features of the samples o + t_q d generated in-kernel (no gradient to the rays)."""
         n = t_start.numel()
         return self._run(None, ray_origs.detach().contiguous(), ray_dirs.detach().contiguous(),

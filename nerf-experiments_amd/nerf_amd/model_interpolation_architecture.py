@@ -15,14 +15,18 @@ outputs are handed to the compositing kernel which applies the activations.
 """
 from __future__ import annotations
 
+import os
 from typing import Iterator, Literal
 
 import torch as th
 import torch.nn as nn
 import torch.nn.functional as F
-
 from .mlp import MLPFunction, nerf_model_plan
 from .positional_encodings import PositionalEncoding
+
+# encodings generated inside the fused field-MLP kernel (NERF_FUSE_ENC=0: stand-alone encoding
+# launches, for A/B timing; results are bitwise the same)
+FUSE_ENCODINGS = os.environ.get("NERF_FUSE_ENC", "1") != "0"
 
 
 class NerfBaseModel(nn.Module):
@@ -146,8 +150,10 @@ class NerfModel(NerfBaseModel):
         """Raw head outputs for every (ray, sample); positions generated in-kernel.  Differentiable
         w.r.t. ray_origs / ray_dirs (pose refinement): the position encoding's ray-mode backward plus
         the per-ray direction encoding's backward."""
+        # both encodings go straight to the field MLP: their rows may be generated inside the fused
+        # kernel (kernels.encode_fwd(defer=True); MLPFunction fills them itself on any other path)
         pos_pe = self.position_encoder.encode_rays(ray_origs, ray_dirs, t_start, t_end, pixel_width,
-                                                   samples_per_ray, query, pw_mode)
-        dir_pe = self.direction_encoder.encode_padded(ray_dirs)
+                                                   samples_per_ray, query, pw_mode, defer=FUSE_ENCODINGS)
+        dir_pe = self.direction_encoder.encode_padded(ray_dirs, defer=FUSE_ENCODINGS)
         z_last, head, dens = self._run_mlp(pos_pe, dir_pe, samples_per_ray)
         return self._heads(z_last, head, dens)

@@ -33,12 +33,12 @@ class _EncodeFn(th.autograd.Function):
     gradient BARF-style pose refinement needs.  Fourier/BARF encodings ignore dir."""
 
     @staticmethod
-    def forward(ctx, x, xdir, pixel_width, t_start, t_end, enc: "PositionalEncoding"):
+    def forward(ctx, x, xdir, pixel_width, t_start, t_end, enc: "PositionalEncoding", defer: bool = False):
         params = enc._pe_params(query=1, pw_mode=2)
         n = x.shape[0]
         out = K.encode_fwd(params, enc.output_dim, x=x, xdir=xdir, t_start=t_start, t_end=t_end,
                            pixel_width=pixel_width, n_samples=n, samples_per_ray=1, n_rays=n,
-                           out_ld=enc.padded_dim, device=x.device)
+                           out_ld=enc.padded_dim, device=x.device, defer=defer)
         ctx.params = params
         ctx.kind = params.kind
         if params.kind == 1:
@@ -60,7 +60,7 @@ class _EncodeFn(th.autograd.Function):
         elif ctx.needs_input_grad[0]:
             (x,) = ctx.saved_tensors
             dx = K.encode_bwd(ctx.params, x, g)
-        return dx, ddir, None, None, None, None
+        return dx, ddir, None, None, None, None, None
 
 
 class _EncodeRaysFn(th.autograd.Function):
@@ -70,13 +70,13 @@ class _EncodeRaysFn(th.autograd.Function):
 
     @staticmethod
     def forward(ctx, ray_o, ray_d, t_start, t_end, pixel_width, enc: "PositionalEncoding", samples_per_ray: int,
-                query: int, pw_mode: int):
+                query: int, pw_mode: int, defer: bool = False):
         params = enc._pe_params(query=query, pw_mode=pw_mode)
         n_rays = ray_o.shape[0]
         out = K.encode_fwd(params, enc.output_dim, ray_o=ray_o, ray_d=ray_d, t_start=t_start, t_end=t_end,
                            pixel_width=pixel_width, n_samples=n_rays * samples_per_ray,
                            samples_per_ray=samples_per_ray, n_rays=n_rays, out_ld=enc.padded_dim,
-                           device=ray_o.device)
+                           device=ray_o.device, defer=defer)
         ctx.params = params
         ctx.S = samples_per_ray
         ctx.has_pw = pixel_width is not None
@@ -92,7 +92,7 @@ class _EncodeRaysFn(th.autograd.Function):
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             d_o, d_d = K.encode_bwd_rays(ctx.params, ray_o, ray_d, t0, t1, pw if ctx.has_pw else None, g, ctx.S,
                                          ctx.needs_input_grad[0], ctx.needs_input_grad[1])
-        return d_o, d_d, None, None, None, None, None, None, None
+        return d_o, d_d, None, None, None, None, None, None, None, None
 
 
 def _as_rows(t, n: int, device=None) -> th.Tensor | None:
@@ -130,22 +130,26 @@ class PositionalEncoding(nn.Module):
             raise ValueError(f"Input shape {tuple(x.shape)} does not match space dimensionality "
                              f"{self.space_dimensions}")
 
-    def encode_padded(self, x, dir=None, pixel_width=None, t_start=None, t_end=None) -> th.Tensor:
+    def encode_padded(self, x, dir=None, pixel_width=None, t_start=None, t_end=None, defer: bool = False) -> th.Tensor:
+        """defer: the rows may be left to the consuming fused field-MLP kernel (kernels.encode_fwd);
+        only for a tensor handed straight to the field MLP."""
         self._check_x(x)
         n = x.shape[0]
         x = x.contiguous()
         return _EncodeFn.apply(x, dir.contiguous() if dir is not None else None,
                                _as_rows(pixel_width, n, x.device), _as_rows(t_start, n, x.device),
-                               _as_rows(t_end, n, x.device), self)
+                               _as_rows(t_end, n, x.device), self, defer)
 
     def encode_rays(self, ray_origs: th.Tensor, ray_dirs: th.Tensor, t_start: th.Tensor, t_end: th.Tensor,
-                    pixel_width: th.Tensor | None, samples_per_ray: int, query: int, pw_mode: int) -> th.Tensor:
-        """Encoding of o + t_query*d for every (ray, sample); differentiable w.r.t. the rays."""
+                    pixel_width: th.Tensor | None, samples_per_ray: int, query: int, pw_mode: int,
+                    defer: bool = False) -> th.Tensor:
+        """Encoding of o + t_query*d for every (ray, sample); differentiable w.r.t. the rays.  defer: as
+        encode_padded."""
         pw = None
         if isinstance(self, (IntegratedFourierFeatures, IntegratedBarfFourierFeatures)):
             pw = pixel_width.reshape(-1).contiguous().float()
         return _EncodeRaysFn.apply(ray_origs.contiguous(), ray_dirs.contiguous(), t_start.contiguous(),
-                                   t_end.contiguous(), pw, self, samples_per_ray, query, pw_mode)
+                                   t_end.contiguous(), pw, self, samples_per_ray, query, pw_mode, defer)
 
 
 class IdentityPositionalEncoding(PositionalEncoding):
@@ -282,12 +286,12 @@ class IntegratedFourierFeatures(PositionalEncoding):
                                 pixel_width_sigma=self._pws(), distribute_variance=bool(self.distribute_variance),
                                 pw_mode=pw_mode, mask=self._mask())
 
-    def encode_padded(self, x, dir=None, pixel_width=None, t_start=None, t_end=None) -> th.Tensor:
+    def encode_padded(self, x, dir=None, pixel_width=None, t_start=None, t_end=None, defer: bool = False) -> th.Tensor:
         if dir is None or pixel_width is None or t_start is None or t_end is None:
             raise ValueError("integrated encodings need dir, pixel_width, t_start and t_end")
         if x.dim() != 2 or x.shape[1] != 3:
             raise ValueError(f"Only 3D supported - was {x.shape[1] if x.dim() == 2 else x.dim()}D")
-        return PositionalEncoding.encode_padded(self, x, dir, pixel_width, t_start, t_end)
+        return PositionalEncoding.encode_padded(self, x, dir, pixel_width, t_start, t_end, defer)
 
 
 class IntegratedBarfFourierFeatures(BarfPositionalEncoding):

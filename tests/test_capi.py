@@ -44,10 +44,23 @@ def test_exported_dynamic_symbols_with_nm():
 def test_abi_version_and_status_strings():
     from nerf_amd import _lib
     lib = _lib.load()
-    assert lib.nerf_abi_version() == 4
+    assert lib.nerf_abi_version() == 5
     assert lib.nerf_status_string(0) == b"ok"
     assert b"invalid" in lib.nerf_status_string(-1)
     assert b"workspace" in lib.nerf_status_string(-4)
+
+
+def test_struct_layouts_match_the_library():
+    """Every argument struct of the binding has the C struct's size (load() checks it too)."""
+    import ctypes
+    from nerf_amd import _lib
+    lib = _lib.load()
+    for which, st in enumerate(_lib.STRUCTS):
+        assert lib.nerf_struct_size(which) == ctypes.sizeof(st), st.__name__
+    assert lib.nerf_struct_size(len(_lib.STRUCTS)) == -1
+    # field offsets the fused kernel reads from its kernel arguments
+    assert _lib.NerfFusedLayer.seg_gen.offset == ctypes.sizeof(_lib.NerfFusedLayer) - 8
+    assert _lib.NerfFusedEncoding.out.offset == ctypes.sizeof(_lib.NerfPEParams) + 5 * 8 + 4
 
 
 def test_argument_validation_returns_status_without_launch():
@@ -131,3 +144,51 @@ def test_missing_library_fails_loudly(tmp_path):
     from nerf_amd import _lib
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         _lib.load(str(tmp_path / "absent.so"))
+
+
+def test_fused_forward_rejects_bad_generated_segments_without_launch():
+    """nerf_mlp_fused_fwd with an in-kernel encoding: checked like nerf_encode_fwd before any launch."""
+    import ctypes
+    from nerf_amd import _lib
+    lib = _lib.load()
+    img = ctypes.create_string_buffer(4096)
+    out = ctypes.create_string_buffer(64 * 32 * 4 + 16)
+    L = (_lib.NerfFusedLayer * 1)()
+    d = L[0]
+    d.type, d.N, d.nb, d.relu, d.nseg = 1, 16, 1, 1, 1
+    d.seg_kb[0], d.seg_k[0], d.seg_rd[0], d.seg_rows[0], d.seg_ld[0] = 1, 32, 1, 64, 32
+    d.chunk_units, d.col_idx, d.img_off, d.hbm_off, d.bias_off = 0, -1, 0, 0, 2048
+    d.seg_gen[0] = 1 | 8
+    enc = (_lib.NerfFusedEncoding * 2)()
+    e = enc[0]
+    e.params.kind, e.params.levels, e.params.include_identity, e.params.scale = 0, 5, 0, 1.0
+    buf = ctypes.create_string_buffer(4096)
+    e.ray_o = e.ray_d = e.t_start = ctypes.addressof(buf)
+    e.n_rays, e.samples_per_ray, e.per_ray, e.out_dim = 8, 8, 0, 30
+    # no encodings array for a generated segment
+    assert lib.nerf_mlp_fused_fwd(L, 1, img, 64, None, None) == -1
+    # out_dim inconsistent with the parameters
+    e.out_dim = 31
+    assert lib.nerf_mlp_fused_fwd(L, 1, img, 64, enc, None) == -1
+    e.out_dim = 30
+    # fewer rays x samples than rows
+    e.n_rays = 7
+    assert lib.nerf_mlp_fused_fwd(L, 1, img, 64, enc, None) == -1
+    e.n_rays = 8
+    # a per-ray (direction) encoding must be plain Fourier features
+    e.per_ray, e.params.kind = 1, 1
+    assert lib.nerf_mlp_fused_fwd(L, 1, img, 64, enc, None) == -1
+    e.per_ray, e.params.kind = 0, 0
+    # misaligned / too narrow output rows
+    e.out, e.ld = ctypes.addressof(out) + 4, 32
+    assert lib.nerf_mlp_fused_fwd(L, 1, img, 64, enc, None) == -1
+    e.out, e.ld = ctypes.addressof(out) + (-ctypes.addressof(out)) % 16, 28
+    assert lib.nerf_mlp_fused_fwd(L, 1, img, 64, enc, None) == -1
+    # generator index out of range, or a generated segment in the input-gradient chain
+    e.ld = 32
+    d.seg_gen[0] = 3
+    assert lib.nerf_mlp_fused_fwd(L, 1, img, 64, enc, None) == -1
+    d.seg_gen[0] = 1
+    d.mask_in = ctypes.addressof(buf)
+    d.relu = 0
+    assert lib.nerf_mlp_fused_fwd(L, 1, img, 64, enc, None) == -1

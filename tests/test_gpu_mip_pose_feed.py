@@ -15,7 +15,10 @@ split-precision error to stay within 2 x 2^9 x the fp32 reference's own error (2
 the per-product error bounds, 2^-15 for three bf16 products vs 2^-24; tools/pose_grad_conditioning.py prints the numbers:
 translation: fp32 1.7e-4, "highest" 1.8e-4, "high" 5.5e-2;
 rotation: fp32 5.0e-6, "highest" 4.9e-6, "high" 2.8e-3 — the reference's TF32 "high" setting, 2^-11 per
-product, would be another 32x worse); feed: gathers bit-exact, directions 3e-7
+product, would be another 32x worse).  The split-precision bounds are stated per quantity
+(HIGH_POSE_GRAD_BOUND: rotation 4.5e-3, translation 8e-2 of the largest gradient), and
+test_gpu_barf_fit_precision.py shows on a fixed-seed BARF fit that this error leaves PSNR and pose
+convergence unchanged within its stated bounds; feed: gathers bit-exact, directions 3e-7
 (the kernel recomputes each pixel's direction instead of gathering the reference's batched matmul)."""
 import math
 
@@ -125,6 +128,10 @@ def _oracle_pose_grads_fp64(g):
     return {"drot": rot.grad.numpy(), "dtrans": trans.grad.numpy()}
 
 
+# split-precision pose-gradient error vs fp64, relative to the largest |gradient|
+HIGH_POSE_GRAD_BOUND = {"drot": 4.5e-3, "dtrans": 8e-2}
+
+
 @pytest.mark.parametrize("precision,tol,gtol", [("highest", 1e-4, 1e-3), ("high", 2e-4, None)])
 def test_pose_gradients_through_rendering(golden, precision, tol, gtol):
     from nerf_amd import BarfPositionalEncoding, NerfInterpolation, NerfModel
@@ -156,6 +163,10 @@ def test_pose_gradients_through_rendering(golden, precision, tol, gtol):
             assert np.abs(got - want).max() <= gtol * np.abs(want).max(), (name, np.abs(got - want).max())
             assert err <= 4 * fp32_err + 1e-6, (name, err, fp32_err)
         else:
+            # stated bounds on this fixture (measured 2.8e-3 / 5.5e-2): within the
+            # conditioning bound 2^10 x fp32_err above, and shown harmless to pose convergence by the
+            # fixed-seed fit of test_gpu_barf_fit_precision.py
+            assert err <= HIGH_POSE_GRAD_BOUND[name], (name, err, fp32_err)
             assert err <= 2 * 2 ** 9 * fp32_err + 1e-5, (name, err, fp32_err)
 
 
