@@ -705,8 +705,12 @@ def main():
                        "coarse_samples": wl["coarse"], "fine_samples": wl["fine"], "global_rays": wl["rays"] * world,
                        "parallelism": f"ray-batch dp{world}" + (" (RCCL bucketed all-reduce from post-accumulate-grad hooks)" if world > 1 else "")},
             "roofline": roofline,
-            "roofline_hbm": {"kernel": "encode_fwd + composite_fwd + composite_bwd (positional encoding and "
-                                       "alpha compositing; algorithmic bytes per launch)",
+            "roofline_hbm": {"kernel": ("encode_fwd + composite_fwd + composite_bwd (positional encoding and "
+                                        "alpha compositing; algorithmic bytes per launch)" if "encode_fwd" in ks else
+                                        "composite_fwd + composite_bwd (alpha compositing; algorithmic bytes per "
+                                        "launch); the positional encodings have no launch of their own: they are "
+                                        "generated inside mlp_fused_kernel<0>, whose bytes include their rows"),
+                             "encode_launches_per_step": ks.get("encode_fwd", {}).get("launches", 0) / args.steps,
                              "bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": hbm_gbs / HBM_PEAK_GBS,
                              "us_per_step": hbm_ms * 1e3 / args.steps,

@@ -339,11 +339,14 @@ typedef struct nerf_fused_layer {
     int64_t ldo2;
     int32_t n1;            /* chunks written to out (= nb when out2 is unused) */
     int32_t hbm_off;       /* byte offset of the layer's HBM-fed weight fragments in the image */
-    int32_t seg_gen[2];    /* 0: segment s is read from seg_ptr; 1 + e: generated by encodings[e]
-                              (+ 8: this layer also stores the generated rows to encodings[e].out) */
+    int32_t seg_gen[2];    /* 0: segment s is read from seg_ptr; 1 + e (first layer, one segment):
+                              the rows of encodings[e] generated at the tile start, read from LDS */
 } nerf_fused_layer;
 
-/* An encoding generated inside the fused kernel (a segment with seg_gen = 1 + e). */
+/* An encoding generated inside the fused forward: every entry with out_dim > 0 is computed at the
+ * start of each 128-sample tile (exactly as nerf_encode_fwd computes it) and its rows are stored
+ * to out (required), where later layers (seg_ptr = out) and the weight gradients read them; the
+ * first layer may take them straight from LDS (seg_gen). */
 typedef struct nerf_fused_encoding {
     nerf_pe_params params;     /* as nerf_encode_fwd takes it (ray mode: query, pw_mode) */
     const float* ray_o;        /* [n_rays][3] */
@@ -351,8 +354,7 @@ typedef struct nerf_fused_encoding {
     const float* t_start;      /* [M] (position encodings) */
     const float* t_end;        /* [M] (midpoint queries, IPE) */
     const float* pixel_width;  /* IPE, addressed by params.pw_mode */
-    float* out;                /* rows stored by the layer with seg_gen & 8: [M][ld], or [n_rays][ld]
-                                  when per_ray; NULL: not stored */
+    float* out;                /* the rows: [M][ld], or [n_rays][ld] when per_ray (ld <= 64) */
     int64_t ld;
     int64_t n_rays;
     int32_t samples_per_ray;   /* sample m belongs to ray m / samples_per_ray */

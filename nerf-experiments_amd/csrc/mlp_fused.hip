@@ -76,11 +76,13 @@ constexpr int ST_AUX = NERF_FUSED_STORE_AUX;
 // starts: the predecessor's 4 epilogue stores (absent outputs included, as dropped stores) and the
 // bias load at the start of the chunk itself
 constexpr int AFTER_DMA_VM = 1 + 2 * SB;
-// Layer-output stores in chunk pairs (NERF_FUSED_PAIR, default 1): a 16-row chunk is 64 B of each
-// sample row, half a 128-B line.  The even chunk's values wait in registers for the odd one's, and
-// the pair leaves as two stores each covering whole lines of 8 samples (lanes s and s ^ 8 trade
-// halves by a DPP row rotate), not two half-line stores per sample a chunk apart.  Every chunk
-// still issues 2 stores per column block (counted waits assume at least that many).
+// Layer-output stores in chunk pairs: a 16-row chunk is 64 B of each sample row, half a 128-B line.
+// The even chunk's values wait in registers for the odd one's, and the pair leaves as two stores
+// each covering whole lines of 8 samples (lanes s and s ^ 8 trade halves by a DPP row rotate), not
+// two half-line stores per sample a chunk apart.  Every chunk still issues 2 stores per column
+// block (counted waits assume at least that many).  NERF_FUSED_PAIR: 0 none, 1 the input-gradient
+// chain only (default: chain 3.73 -> 3.55 ms per mip step, while the forward ran 3.55 -> 3.69),
+// 2 both.
 #ifndef NERF_FUSED_PAIR
 #define NERF_FUSED_PAIR 1
 #endif
@@ -90,6 +92,8 @@ struct FusedArgs {
     nerf_fused_encoding enc[2];
     const char* img;
     int img_bytes;
+    int gen_mask;      // bit e: encoding e is generated at the start of every tile (forward only)
+    int gen_lds;       // the encoding the first layer reads from LDS (generated last), or -1
     int n_layers;
     int M;
     int ntiles;
@@ -242,44 +246,134 @@ struct GenArgs {
     int64_t n_rays;
 };
 
-// Columns col .. col + 7 of encoding e for sample m (zeros past out_dim and for rows past M), as
-// nerf_encode_fwd computes them (bitwise: the same functions, fp contraction off), split into the
-// bf16 hi/lo operand halves; `store`: also written to the encoding's output rows for the weight
-// gradients (a per-ray encoding by the ray's first sample).
-__device__ __forceinline__ void gen_block(const Ctx& c, int e, bool store, int m, bool ok, int col, bf16x8& h,
-                                          bf16x8& lo) {
-#pragma clang fp contract(off)
-    const int per_ray = EF(int, per_ray, e);
-    const int S = EF(int, samples_per_ray, e);
-    const float* ray_d = EF(cfptr_t, ray_d, e);
-    const GenArgs a{EF(nerf_pe_params, params, e), per_ray ? ray_d : nullptr, nullptr, EF(cfptr_t, ray_o, e), ray_d,
-                    EF(cfptr_t, t_start, e), EF(cfptr_t, t_end, e), EF(cfptr_t, pixel_width, e), S,
-                    EF(int64_t, n_rays, e)};
-    const int out_dim = EF(int, out_dim, e);
-    const int L = a.p.levels, id = a.p.include_identity ? 3 : 0;
-    f8 v = {};
-    if (ok) {
-        const int64_t n = per_ray ? (int64_t)((unsigned)m / (unsigned)S) : (int64_t)m;
-        float p[3], dv[3], pm[3];
-        load_pos_dir(a, n, p, dv);
-        IpeSample q;
-        if (a.p.kind == 1) {
-            q = ipe_sample(a.p, p, dv, a.t0[n], a.t1[n], a.pw ? pixel_width_at(a, n) : 0.f);
-            pm[0] = q.pm[0]; pm[1] = q.pm[1]; pm[2] = q.pm[2];
-        } else {
-            pm[0] = p[0]; pm[1] = p[1]; pm[2] = p[2];
-        }
+// Rows of encoding e for the wave's samples base .. base + SPW - 1, written into LDS (the wave's
+// operand-image region, unused before a layer's chunk loop): row r, columns [0, 64) (zeros past
+// out_dim), as nerf_encode_fwd computes them (the same encode_common.h functions, fp contraction
+// off: bitwise equal).  The wave shares the work like encode_fwd_lds_kernel: per-sample terms
+// (position, IPE mean shift and variances) once per sample, then one sincos per (sample, d, k)
+// task for both its cos and sin columns.  Rows past M hold values of a zero position (their
+// outputs are dropped).
+constexpr int GEN_LD = 68;                    // floats per LDS row: 64 columns + 16-B pad
+static_assert(SPW * (GEN_LD + 8) * 4 <= XIMG_BYTES, "generator scratch");
+// The per-sample inputs of encoding e for lanes < SPW (sample base + lane): o xyz, d xyz, t0, t1,
+// pixel width for ray-mode positions; x xyz for per-ray directions.  Loads only, so that the
+// tile's inputs of both encodings are in flight together (one memory round trip per tile).
+__device__ __forceinline__ void gen_load(const Ctx& c, int e, int base, float (&v)[9]) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = col + j < out_dim ? enc_column(a.p, L, id, col + j, pm, q) : 0.f;
-        float* out = EF(fptr_t, out, e);
-        if (store && out != nullptr && (!per_ray || (unsigned)m % (unsigned)S == 0u)) {
-            const int64_t ld = EF(int64_t, ld, e);
-            float* r = out + n * ld + col;
-            if (col < ld) *reinterpret_cast<f4*>(r) = v.lo;
-            if (col + 4 < ld) *reinterpret_cast<f4*>(r + 4) = v.hi;
+    for (int j = 0; j < 9; ++j) v[j] = 0.f;
+    const int m = base + c.lane;
+    if (c.lane >= SPW || m >= c.M) return;
+    const int per_ray = EF(int, per_ray, e);
+    const unsigned S = (unsigned)EF(int, samples_per_ray, e);
+    const float* ray_d = EF(cfptr_t, ray_d, e);
+    const int64_t ray = (int64_t)((unsigned)m / S);
+    if (per_ray) {
+        v[0] = ray_d[ray * 3 + 0]; v[1] = ray_d[ray * 3 + 1]; v[2] = ray_d[ray * 3 + 2];
+        return;
+    }
+    const float* o = EF(cfptr_t, ray_o, e);
+    const __attribute__((address_space(4))) nerf_pe_params& p = EF(nerf_pe_params, params, e);
+    v[0] = o[ray * 3 + 0]; v[1] = o[ray * 3 + 1]; v[2] = o[ray * 3 + 2];
+    v[3] = ray_d[ray * 3 + 0]; v[4] = ray_d[ray * 3 + 1]; v[5] = ray_d[ray * 3 + 2];
+    v[6] = EF(cfptr_t, t_start, e)[m];
+    if (p.query != 0 || p.kind == 1) v[7] = EF(cfptr_t, t_end, e)[m];
+    const float* pw = EF(cfptr_t, pixel_width, e);
+    if (p.kind == 1 && pw != nullptr) {
+        const GenArgs a{p, nullptr, nullptr, o, ray_d, nullptr, nullptr, pw, (int)S, EF(int64_t, n_rays, e)};
+        v[8] = pixel_width_at(a, m);
+    }
+}
+
+// Rows of encoding e from its inputs (gen_load) into the wave's LDS scratch.
+__device__ __forceinline__ void gen_rows_lds(const Ctx& c, int e, int base, const float (&v)[9]) {
+#pragma clang fp contract(off)
+    float* R = reinterpret_cast<float*>(c.ximg);          // [SPW][GEN_LD]
+    float* P = R + SPW * GEN_LD;                            // [SPW][8]: pm xyz, vb xyz
+    const __attribute__((address_space(4))) nerf_pe_params& prm = EF(nerf_pe_params, params, e);
+    const int per_ray = EF(int, per_ray, e);
+    const int out_dim = EF(int, out_dim, e);
+    const int L = prm.levels, id = prm.include_identity ? 3 : 0;
+    if (c.lane < SPW) {
+        float pm[3] = {0.f, 0.f, 0.f}, vb[3] = {0.f, 0.f, 0.f};
+        if (base + c.lane < c.M) {
+            // as load_pos_dir (encode_common.h): x, or o + tq d
+            float p[3], dv[3];
+            if (per_ray) {
+                p[0] = v[0]; p[1] = v[1]; p[2] = v[2];
+                dv[0] = dv[1] = dv[2] = 0.f;
+            } else {
+                const float tq = prm.query == 0 ? v[6] : (v[6] + v[7]) / 2.0f;
+                dv[0] = v[3]; dv[1] = v[4]; dv[2] = v[5];
+                p[0] = v[0] + tq * dv[0];
+                p[1] = v[1] + tq * dv[1];
+                p[2] = v[2] + tq * dv[2];
+            }
+            if (prm.kind == 1) {
+                const IpeSample q = ipe_sample(prm, p, dv, v[6], v[7], v[8]);
+                pm[0] = q.pm[0]; pm[1] = q.pm[1]; pm[2] = q.pm[2];
+                vb[0] = q.vb[0]; vb[1] = q.vb[1]; vb[2] = q.vb[2];
+            } else {
+                pm[0] = p[0]; pm[1] = p[1]; pm[2] = p[2];
+            }
+        }
+        float* pr = P + c.lane * 8;
+        pr[0] = pm[0]; pr[1] = pm[1]; pr[2] = pm[2];
+        pr[3] = vb[0]; pr[4] = vb[1]; pr[5] = vb[2];
+        float* row = R + c.lane * GEN_LD;
+        for (int col = 0; col < id; ++col) row[col] = pm[col];
+        for (int col = out_dim; col < 64; ++col) row[col] = 0.f;
+    }
+    const GenArgs a{prm, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1, 1};
+    // (same wave: its LDS operations complete in order, so the terms above are visible below)
+    const int na = 3 * L;
+    for (int i = c.lane; i < SPW * na; i += 64) {
+        const int r = i / na, j = i - r * na;
+        const int dd = j >= 2 * L ? 2 : (j >= L ? 1 : 0);
+        const int k = j - dd * L;
+        const float sc = a.p.scale * (float)(1u << k);
+        float sn, cs;
+        sincos_enc(P[r * 8 + dd] * sc, &sn, &cs);
+        if (a.p.kind == 1) {
+            // mip-NeRF weight exp(-(var_d * 4^k) / 2) (positional_encodings.py:213-232)
+            const float w = expf((-(P[r * 8 + 3 + dd] * (float)(1u << (2 * k)))) / 2.0f);
+            cs = cs * w;
+            sn = sn * w;
+        }
+        if (a.p.use_mask) {
+            const float mk = a.p.mask[k];
+            cs = mk * cs;
+            sn = mk * sn;
+        }
+        R[r * GEN_LD + id + j] = cs;
+        R[r * GEN_LD + id + na + j] = sn;
+    }
+}
+
+// The generated rows of the wave's samples into the encoding's rows in HBM (read back by later
+// layers of the launch and by the weight gradients; a per-ray encoding by the ray's first sample):
+// each instruction stores 1 KB of consecutive 16-byte row pieces.
+__device__ __forceinline__ void gen_store(const Ctx& c, int e, int base) {
+    const float* R = reinterpret_cast<const float*>(c.ximg);
+    float* out = EF(fptr_t, out, e);
+    const int per_ray = EF(int, per_ray, e);
+    const unsigned S = (unsigned)EF(int, samples_per_ray, e);
+    const int ld = (int)EF(int64_t, ld, e);
+    const int q4 = ld >> 2;                                   // 16-byte pieces per row (ld <= 64)
+    for (int i = c.lane; i < SPW * q4; i += 64) {
+        const int r = i / q4, q = i - r * q4;
+        const int m = base + r;
+        if (m < c.M && (!per_ray || (unsigned)m % S == 0u)) {
+            const int64_t n = per_ray ? (int64_t)((unsigned)m / S) : (int64_t)m;
+            *reinterpret_cast<f4*>(out + n * ld + 4 * q) = *reinterpret_cast<const f4*>(R + r * GEN_LD + 4 * q);
         }
     }
-    split8(v, h, lo);
+}
+
+// Columns col .. col + 7 of generated row r (gen_rows_lds), split into the bf16 hi/lo operand halves.
+__device__ __forceinline__ void gen_block(const Ctx& c, int r, int col, bf16x8& h, bf16x8& lo) {
+    const float* R = reinterpret_cast<const float*>(c.ximg) + r * GEN_LD + col;
+    const f4 v0 = *reinterpret_cast<const f4*>(R), v1 = *reinterpret_cast<const f4*>(R + 4);
+    split8(__builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7), h, lo);
 }
 
 struct LayerState {
@@ -375,7 +469,7 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 v[r] = __builtin_bit_cast(float, max(__builtin_bit_cast(int, v[r] + b[r]), st.floor_i));
-#if NERF_FUSED_PAIR
+#if NERF_FUSED_PAIR >= 2
             if (!pair_odd(ch)) {
                 // even chunk: held for the pair (alone if it is the layer's last); the column output
                 // (col_idx is a multiple of 32: always an even chunk)
@@ -528,6 +622,8 @@ __device__ __forceinline__ void reg_steps(Ctx& c, LayerState& st, unsigned sa, b
             lds_frag<(KB_I + FA) * 2048>(f[0], sa);
             lds_frag<(KB_I + FA) * 2048 + 1024>(f[1], sa);
         }
+        // (placing the epilogue parts of the two waves of a SIMD at different stages, 0-2 and 4-6,
+        // measured slower: chain 3.78 -> 4.03-4.09 ms, forward 3.86 -> 3.94-4.00 per mip step)
         if constexpr (KB_I == EPI0) bias_wait<(KBR > 0 ? DMA_PER_WAVE : 0) + 2 * KBH>(pb);
         if constexpr (KB_I >= EPI0 && KB_I < EPI0 + 3) epi_part<MODE>(c, st, KB_I - EPI0, ch - 1, pv, pb);
         __builtin_amdgcn_sched_barrier(0);
@@ -624,11 +720,9 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
             const int sg = kh < kb0 ? 0 : 1;            // segment of this block
             const int khl = sg ? kh - kb0 : kh;
             const int gen = MODE != MODE_FWD ? 0 : sg ? LFI(int, seg_gen, 1, l) : LFI(int, seg_gen, 0, l);
-            if (gen != 0) {                             // generated in-kernel (encodings[gen & 7 - 1])
+            if (gen != 0) {                             // generated at the tile start, still in LDS
 #pragma unroll
-                for (int sb = 0; sb < SB; ++sb)
-                    gen_block(c, (gen & 7) - 1, (gen & 8) != 0, sample[sb], row_ok[sb], 32 * khl + 8 * g,
-                              hh[kh][sb], hl[kh][sb]);
+                for (int sb = 0; sb < SB; ++sb) gen_block(c, 16 * sb + (c.lane & 15), 32 * khl + 8 * g, hh[kh][sb], hl[kh][sb]);
                 continue;
             }
             const float* p = sg ? LFI(cfptr_t, seg_ptr, 1, l) : LFI(cfptr_t, seg_ptr, 0, l);
@@ -773,6 +867,25 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
         }
     for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
         const int base = tile * TILE + c.wave * SPW;
+        if (MODE == MODE_FWD && a.gen_mask != 0) {
+            // the tile's in-kernel encodings (one code copy for every layer type): the inputs of both
+            // loaded together, then each into the wave's LDS scratch and out to its HBM rows; the one
+            // the first layer reads last, so that its rows are still in LDS
+            float v0[9], v1[9];
+            if (a.gen_mask & 1) gen_load(c, 0, base, v0);
+            if (a.gen_mask & 2) gen_load(c, 1, base, v1);
+#pragma nounroll
+            for (int i = 0; i < 2; ++i) {
+                const int e = a.gen_lds == 0 ? 1 - i : i;
+                if ((a.gen_mask >> e) & 1) {
+                    float v[9];
+#pragma unroll
+                    for (int j = 0; j < 9; ++j) v[j] = e == 0 ? v0[j] : v1[j];
+                    gen_rows_lds(c, e, base, v);
+                    gen_store(c, e, base);
+                }
+            }
+        }
         for (int l = 0; l < a.n_layers; ++l) {
             switch (LF(int, type, l)) {
                 case 1: fused_layer<MODE, 0, 1>(c, l, base); break;
@@ -868,6 +981,7 @@ extern "C" int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_laye
     NERF_REQUIRE(M >= 1 && M <= (int64_t)1 << 30);
     FusedArgs a;
     int64_t img_end = 0;
+    int gen_lds = -1;
     // the input-gradient chain (a layer multiplies by ReLU bits or routes rows to a second output):
     // no bias, no ReLU, no mask bits or column outputs; otherwise the forward, which has none of those
     bool dgrad = false;
@@ -908,10 +1022,11 @@ extern "C" int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_laye
             const int gen = s < L.nseg ? L.seg_gen[s] : 0;
             NERF_REQUIRE(s < L.nseg || L.seg_gen[s] == 0);
             if (gen == 0) continue;
-            // generated: encodings[e] (e = (gen & 7) - 1), its columns within the segment's blocks
-            NERF_REQUIRE(!dgrad && encodings != nullptr && (gen & ~15) == 0 && ((gen & 7) == 1 || (gen & 7) == 2));
-            const nerf_fused_encoding& e = encodings[(gen & 7) - 1];
-            NERF_REQUIRE(encoding_ok(e, M) && e.out_dim <= 32 * L.seg_kb[s]);
+            // read from the rows generated at the tile start: the first layer only, one segment
+            NERF_REQUIRE(!dgrad && l == 0 && encodings != nullptr && (gen == 1 || gen == 2) && gen_lds < 0);
+            const nerf_fused_encoding& e = encodings[gen - 1];
+            NERF_REQUIRE(e.out_dim > 0 && e.out_dim <= 32 * L.seg_kb[s] && 32 * L.seg_kb[s] <= 64);
+            gen_lds = gen - 1;
         }
         for (int s = 0; s < L.nseg; ++s) {
             kbs += L.seg_kb[s];
@@ -936,10 +1051,21 @@ extern "C" int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_laye
         if (L.nseg < 1) a.L[l].seg_gen[0] = 0;
     }
     NERF_REQUIRE(img_end < ((int64_t)1 << 31));
+    // generated encodings (out_dim > 0): checked as nerf_encode_fwd checks its arguments; their rows
+    // are always stored (later layers and the weight gradients read them)
+    int gen_mask = 0;
     for (int e = 0; e < 2; ++e) {
-        if (encodings != nullptr) a.enc[e] = encodings[e];
-        else memset(&a.enc[e], 0, sizeof(a.enc[e]));
+        if (encodings != nullptr && encodings[e].out_dim > 0) {
+            NERF_REQUIRE(!dgrad && encoding_ok(encodings[e], M) && encodings[e].out != nullptr && encodings[e].ld <= 64);
+            a.enc[e] = encodings[e];
+            gen_mask |= 1 << e;
+        } else {
+            memset(&a.enc[e], 0, sizeof(a.enc[e]));
+        }
     }
+    NERF_REQUIRE(gen_lds < 0 || ((gen_mask >> gen_lds) & 1));
+    a.gen_mask = gen_mask;
+    a.gen_lds = gen_lds;
     a.img = static_cast<const char*>(image);
     a.img_bytes = (int)img_end;
     a.n_layers = n_layers;

@@ -206,13 +206,14 @@ class FusedForward:
             gens=(None, None)):
         """Launch on the current stream.  acts[l]: [M, out_ld] fp32 or None (not stored),
         masks[l]: [M, 32] uint8 or None, col_outs: {layer: [M] fp32}.  gens: the DeferredEncoding
-        of pos / dirs or None: generated in-kernel (kernels.encode_fwd(defer=True)); the first layer
-        reading one also writes its rows into the tensor."""
+        of pos / dirs or None: generated in-kernel at every tile start (kernels.encode_fwd(defer=True))
+        and stored into the tensor, which later layers read; the first layer reads them from LDS."""
         self.pack()
         L = len(self.plan.layers)
         descs = (_lib.NerfFusedLayer * L)()
         encs = (_lib.NerfFusedEncoding * 2)()
         gen_of = {}
+        nbytes = 0.0
         for e, (kind, g) in enumerate((("pos", gens[0]), ("dir", gens[1]))):
             if g is None:
                 continue
@@ -223,9 +224,12 @@ class FusedForward:
             if kind == "dir":
                 encs[e].samples_per_ray = dir_rd
             gen_of[kind] = e + 1
+            # generated at every tile start and stored: rows written once, the inputs read
+            # (t_start [, t_end] per sample, o, d [, pw] per ray; directions per ray)
+            t = pos if kind == "pos" else dirs
+            nbytes += 4.0 * t.stride(0) * t.shape[0]
+            nbytes += (8.0 * M + 28.0 * encs[e].n_rays) if not encs[e].per_ray else 12.0 * encs[e].n_rays
         flops = 0.0
-        nbytes = 0.0
-        stored = set()
         for idx, lp in enumerate(self.plan.layers):
             kbr, kbh, hbm, nb, n16, off, hbm_off, bias_off = self.layers[idx]
             d = descs[idx]
@@ -242,17 +246,12 @@ class FusedForward:
                 d.seg_rows[si] = t.shape[0]
                 d.seg_ld[si] = t.stride(0)
                 d.seg_ptr[si] = t.data_ptr()
-                e = gen_of.get(s.kind, 0)
-                if e:
-                    d.seg_gen[si] = e | (8 if s.kind not in stored else 0)
-                    if s.kind not in stored:
-                        stored.add(s.kind)
-                        # rows written once; the inputs (t_start [, t_end] per sample, o, d [, pw] per ray)
-                        nbytes += 4.0 * t.stride(0) * t.shape[0]
-                    spec = encs[e - 1]
-                    nbytes += (8.0 * M + 28.0 * spec.n_rays) if not spec.per_ray else 12.0 * spec.n_rays
+                if idx == 0 and s.kind in gen_of:
+                    # the first layer takes the rows generated at the tile start straight from LDS
+                    d.seg_gen[si] = gen_of[s.kind]
                 else:
-                    # algorithmic bytes: an HBM-fed encoding read
+                    # algorithmic bytes: an HBM-fed encoding read (generated ones: the rows the kernel
+                    # stored at the tile start)
                     nbytes += 4.0 * d.seg_k[si] * d.seg_rows[si]
             d.chunk_units = 2 * kbr
             d.col_idx = -1

@@ -147,48 +147,62 @@ def test_missing_library_fails_loudly(tmp_path):
 
 
 def test_fused_forward_rejects_bad_generated_segments_without_launch():
-    """nerf_mlp_fused_fwd with an in-kernel encoding: checked like nerf_encode_fwd before any launch."""
+    """nerf_mlp_fused_fwd with in-kernel encodings: checked like nerf_encode_fwd before any launch."""
     import ctypes
     from nerf_amd import _lib
     lib = _lib.load()
     img = ctypes.create_string_buffer(4096)
     out = ctypes.create_string_buffer(64 * 32 * 4 + 16)
-    L = (_lib.NerfFusedLayer * 1)()
+    aligned = ctypes.addressof(out) + (-ctypes.addressof(out)) % 16
+    L = (_lib.NerfFusedLayer * 2)()
     d = L[0]
     d.type, d.N, d.nb, d.relu, d.nseg = 1, 16, 1, 1, 1
     d.seg_kb[0], d.seg_k[0], d.seg_rd[0], d.seg_rows[0], d.seg_ld[0] = 1, 32, 1, 64, 32
+    d.seg_ptr[0] = aligned
     d.chunk_units, d.col_idx, d.img_off, d.hbm_off, d.bias_off = 0, -1, 0, 0, 2048
-    d.seg_gen[0] = 1 | 8
+    d.seg_gen[0] = 1
     enc = (_lib.NerfFusedEncoding * 2)()
     e = enc[0]
     e.params.kind, e.params.levels, e.params.include_identity, e.params.scale = 0, 5, 0, 1.0
     buf = ctypes.create_string_buffer(4096)
     e.ray_o = e.ray_d = e.t_start = ctypes.addressof(buf)
     e.n_rays, e.samples_per_ray, e.per_ray, e.out_dim = 8, 8, 0, 30
+    e.out, e.ld = aligned, 32
+
+    def call(n_layers=1, encs=enc):
+        return lib.nerf_mlp_fused_fwd(L, n_layers, img, 64, encs, None)
     # no encodings array for a generated segment
-    assert lib.nerf_mlp_fused_fwd(L, 1, img, 64, None, None) == -1
+    assert call(encs=None) == -1
     # out_dim inconsistent with the parameters
     e.out_dim = 31
-    assert lib.nerf_mlp_fused_fwd(L, 1, img, 64, enc, None) == -1
+    assert call() == -1
     e.out_dim = 30
     # fewer rays x samples than rows
     e.n_rays = 7
-    assert lib.nerf_mlp_fused_fwd(L, 1, img, 64, enc, None) == -1
+    assert call() == -1
     e.n_rays = 8
     # a per-ray (direction) encoding must be plain Fourier features
     e.per_ray, e.params.kind = 1, 1
-    assert lib.nerf_mlp_fused_fwd(L, 1, img, 64, enc, None) == -1
+    assert call() == -1
     e.per_ray, e.params.kind = 0, 0
-    # misaligned / too narrow output rows
-    e.out, e.ld = ctypes.addressof(out) + 4, 32
-    assert lib.nerf_mlp_fused_fwd(L, 1, img, 64, enc, None) == -1
-    e.out, e.ld = ctypes.addressof(out) + (-ctypes.addressof(out)) % 16, 28
-    assert lib.nerf_mlp_fused_fwd(L, 1, img, 64, enc, None) == -1
-    # generator index out of range, or a generated segment in the input-gradient chain
+    # the rows must be stored: no, misaligned or too narrow output rows
+    e.out = None
+    assert call() == -1
+    e.out, e.ld = aligned + 4, 32
+    assert call() == -1
+    e.out, e.ld = aligned, 28
+    assert call() == -1
     e.ld = 32
+    # generator index out of range; a generated segment read by a later layer or in the chain
     d.seg_gen[0] = 3
-    assert lib.nerf_mlp_fused_fwd(L, 1, img, 64, enc, None) == -1
+    assert call() == -1
+    d.seg_gen[0] = 9
+    assert call() == -1
+    d.seg_gen[0] = 0
+    L[1] = L[0]
+    L[1].type, L[1].seg_gen[0] = 7, 1
+    assert call(2) == -1
     d.seg_gen[0] = 1
     d.mask_in = ctypes.addressof(buf)
     d.relu = 0
-    assert lib.nerf_mlp_fused_fwd(L, 1, img, 64, enc, None) == -1
+    assert call() == -1
