@@ -278,7 +278,9 @@ int nerf_pack_weight(const float* W, int32_t N, int32_t K_orig, const int32_t* c
  * ceil(N/128)*128 rows of ld = Kp, Wt_x has ceil(Kp/128)*128 + 128 rows of ld = ldwt).
  * 32 < N <= 256 runs a 256-row tile staged by LDS-DMA; other N a 128 x 128 tile.
  * nerf_linear_wgrad_x3 writes the same workspace as nerf_linear_wgrad (reduce with
- * nerf_linear_wgrad_reduce).
+ * nerf_linear_wgrad_reduce, same M, K and N rounded up to 4); its N may be the true row count
+ * (ld_dy >= pad4(N)): N <= 257 with N or K above 128 and K <= 256 runs as one 256 x 256 tile
+ * per M split, row 256 on the vector ALUs in fp32. 
  * ------------------------------------------------------------------------- */
 int nerf_linear_fwd_x3(const nerf_seg* segs, int32_t n_segs, int64_t M,
                        const void* W_x, int32_t ldw, int32_t N, const float* bias,

@@ -550,6 +550,15 @@ __global__ void pack_weight_kernel(const float* __restrict__ W, int N, int K_ori
 // shared with linear_x3.hip (same slab layout and reduce)
 int nerf_wgrad_choose_splits(int64_t M, int tiles) { return choose_splits(M, tiles); }
 
+// The tile count the M split is chosen for: a layer the split-precision weight gradient runs as one
+// 256 x 256 tile (plus, for N = 257, one row on the vector ALUs: NerfModel's density + feature
+// layer, whose workspace and reduce see it padded to 260) counts as the four 128 x 128 tiles it
+// covers, whatever its 128-tile grid
+int nerf_wgrad_split_tiles(int N, int K) {
+    if (N <= 260 && K <= 256 && (N > 128 || K > 128)) return 4;
+    return ((N + TB - 1) / TB) * ((K + TB - 1) / TB);
+}
+
 extern "C" int nerf_linear_fwd(const nerf_seg* segs, int32_t n_segs, int64_t M, const float* W, int32_t ldw, int32_t N,
                                const float* bias, float* out, int64_t ldo, int32_t epilogue, const float* aux,
                                int64_t ld_aux, void* stream) {
@@ -589,7 +598,7 @@ extern "C" int nerf_linear_fwd(const nerf_seg* segs, int32_t n_segs, int64_t M, 
 
 extern "C" size_t nerf_linear_wgrad_workspace(int64_t M, int32_t N, int32_t K) {
     const int ntn = (N + TB - 1) / TB, ntk = (K + TB - 1) / TB;
-    const int splits = choose_splits(M, ntn * ntk);
+    const int splits = choose_splits(M, nerf_wgrad_split_tiles(N, K));
     return (size_t)splits * ntn * TB * (size_t)ntk * TB * sizeof(float) + (size_t)splits * ntn * TB * sizeof(float);
 }
 
@@ -600,7 +609,7 @@ extern "C" int nerf_linear_wgrad(const float* dY, int64_t ld_dy, int32_t N, cons
     SegList L;
     NERF_REQUIRE(build_segs(segs, n_segs, L));
     const int ntn = (N + TB - 1) / TB, ntk = (L.ktot + TB - 1) / TB;
-    const int splits = choose_splits(M, ntn * ntk);
+    const int splits = choose_splits(M, nerf_wgrad_split_tiles(N, L.ktot));
     const size_t need = nerf_linear_wgrad_workspace(M, N, L.ktot);
     if (!workspace || workspace_bytes < need || !aligned16(workspace)) return NERF_ERR_WORKSPACE;
     float* slab = reinterpret_cast<float*>(workspace);
@@ -619,7 +628,7 @@ extern "C" int nerf_linear_wgrad_reduce(int64_t M, int32_t N, int32_t K, int32_t
                                         int32_t accumulate, void* stream) {
     NERF_REQUIRE(workspace && dW && N >= 1 && K >= 1 && n_valid >= 1 && n_valid <= N);
     const int ntn = (N + TB - 1) / TB, ntk = (K + TB - 1) / TB;
-    const int splits = choose_splits(M, ntn * ntk);
+    const int splits = choose_splits(M, nerf_wgrad_split_tiles(N, K));
     const float* slab = reinterpret_cast<const float*>(workspace);
     const float* db_slab = slab + (size_t)splits * ntn * TB * (size_t)ntk * TB;
     const int64_t total = (int64_t)n_valid * K;

@@ -982,7 +982,12 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     const float* dxp = dx_ok ? pick4(a.X.ptr, dxs) + dxoff : a.X.ptr[0];
     const int64_t dxld = dx_ok ? pick4(a.X.ld, dxs) : a.X.ld[0];
     const unsigned dxrd = dx_ok ? (unsigned)pick4(a.X.row_div, dxs) : (unsigned)a.X.row_div[0];
-    // wave w brings rows 2w, 2w + 1 of both operands
+    // wave w brings rows 2w, 2w + 1 of both operands.  Lanes whose 4 columns lie past N / the
+    // packed K fetch nothing (their LDS bytes keep stale values, zeroed by the conversion's column
+    // mask): a 64-column X (the first layer) moves 256 B per row, not 1 KB.  Lane 0's columns are
+    // always valid, so every DMA instruction issues (the counted waits count them).
+    const bool y_fetch = 4 * lane < a.N;
+    const bool x_fetch = dx_ok;
     auto issue = [&](int step) __attribute__((always_inline)) {
         char* st = ring + (step % NRAW) * WS_RAW;
 #pragma unroll
@@ -991,10 +996,11 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             int m = mbeg + step * WS_T + r;
             m = m < mend ? m : mbeg;                       // past the split: any valid row (zeroed)
             const float* ys = a.dY + (int64_t)m * a.lddy + ycol;
-            __builtin_amdgcn_global_load_lds((glb_void_t*)ys, (lds_void_t*)(st + r * 1024), 16, 0, 0);
+            if (y_fetch) __builtin_amdgcn_global_load_lds((glb_void_t*)ys, (lds_void_t*)(st + r * 1024), 16, 0, 0);
             const unsigned xr = dxrd == 1u ? (unsigned)m : (unsigned)m / dxrd;
             const float* xsrc = dxp + (int64_t)xr * dxld;
-            __builtin_amdgcn_global_load_lds((glb_void_t*)xsrc, (lds_void_t*)(st + (WS_T + r) * 1024), 16, 0, 0);
+            if (x_fetch)
+                __builtin_amdgcn_global_load_lds((glb_void_t*)xsrc, (lds_void_t*)(st + (WS_T + r) * 1024), 16, 0, 0);
         }
     };
 
@@ -1009,6 +1015,20 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         c_ok = xs >= 0 && xoff < pick4(a.X.k, xs);
     }
     float db = 0.f;
+    // N = 257 (NerfModel's density + feature layer): row 256 of dW / db on the X conversion threads,
+    // dW[256][c] = sum over the split's samples (in order) of dY[m][256] * X[m][c] as fp32 FMAs; the
+    // step's 16 dY[m][256] values by scalar loads (uniform addresses), issued with the ring reads
+    const bool xrow = a.N > 256 && op == 1;
+    float dacc = 0.f, dbx = 0.f;
+    float yd[WS_T];
+    auto yd_load = [&](int step) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < WS_T; ++r) {
+            int m = mbeg + step * WS_T + r;
+            m = m < mend ? m : mbeg;
+            yd[r] = *(const __attribute__((address_space(4))) float*)(a.dY + (int64_t)m * a.lddy + 256);
+        }
+    };
     // the conversion in two halves, so that a step's ring reads can be issued ahead of the MFMAs
     // and its split / image writes scheduled between them (one basic block: no branch inside);
     // past the last step it converts stale ring rows into an image stage nobody reads again, all
@@ -1018,6 +1038,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         const float* src = reinterpret_cast<const float*>(ring + (step % NRAW) * WS_RAW + op * WS_T * 1024) + c;
 #pragma unroll
         for (int r = 0; r < WS_T; ++r) v[r] = src[r * 256];
+        if (xrow) yd_load(step);
     };
     auto conv_store = [&](int step, float (&v)[WS_T]) __attribute__((always_inline)) {
         __bf16* dst = reinterpret_cast<__bf16*>(img + (step % NIMG) * WS_IMG + op * 256 * 64);
@@ -1033,6 +1054,12 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         if (op == 0) {                                      // wave-uniform: the dY threads
 #pragma unroll
             for (int r = 0; r < WS_T; ++r) db += v[r];
+        }
+        if (xrow) {                                         // wave-uniform: the X threads of N = 257
+#pragma unroll
+            for (int r = 0; r < WS_T; ++r) dacc = __builtin_fmaf(yd[r], v[r], dacc);   // v is 0 past the split
+#pragma unroll
+            for (int r = 0; r < WS_T; ++r) dbx += r < valid ? yd[r] : 0.f;
         }
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
@@ -1146,6 +1173,10 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             }
         }
     if (op == 0 && c < npad) a.db_slab[(size_t)split * npad + c] = db;
+    if (xrow) {
+        slab[(size_t)256 * kpad + c] = dacc;
+        if (c == 0) a.db_slab[(size_t)split * npad + 256] = dbx;
+    }
 }
 
 // Interleaved split weights: element (r, c) of a [rows][ld] matrix goes to
@@ -1214,6 +1245,7 @@ int cu_count_x3() {
 // same split policy as the fp32 weight-gradient (shared workspace / reduce kernel)
 extern "C" size_t nerf_linear_wgrad_workspace(int64_t M, int32_t N, int32_t K);
 int nerf_wgrad_choose_splits(int64_t M, int tiles);
+int nerf_wgrad_split_tiles(int N, int K);
 
 extern "C" int nerf_linear_fwd_x3(const nerf_seg* segs, int32_t n_segs, int64_t M, const void* W_x, int32_t ldw,
                                   int32_t N, const float* bias, float* out, int64_t ldo, int32_t epilogue,
@@ -1343,12 +1375,14 @@ extern "C" int nerf_linear_gauss_x3(const nerf_seg* segs, int32_t n_segs, int64_
 
 extern "C" int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N, const nerf_seg* segs, int32_t n_segs,
                                     int64_t M, void* workspace, size_t workspace_bytes, void* stream) {
-    NERF_REQUIRE(dY && N >= 1 && M >= 0 && M < (1ll << 31) && aligned16(dY) && (ld_dy % 4) == 0 && (N % 4) == 0 &&
-                 ld_dy >= N);
+    // N need not be a multiple of 4: the kernels read dY in 4-column pieces up to pad4(N) <= ld_dy;
+    // slab rows past N are left unspecified (nerf_linear_wgrad_reduce's n_valid <= N)
+    NERF_REQUIRE(dY && N >= 1 && M >= 0 && M < (1ll << 31) && aligned16(dY) && (ld_dy % 4) == 0 &&
+                 ld_dy >= (N + 3) / 4 * 4);
     SegList L;
     NERF_REQUIRE(build_segs(segs, n_segs, L));
     const int ntn = (N + TB - 1) / TB, ntk = (L.ktot + TB - 1) / TB;
-    const int splits = nerf_wgrad_choose_splits(M, ntn * ntk);
+    const int splits = nerf_wgrad_choose_splits(M, nerf_wgrad_split_tiles(N, L.ktot));
     const size_t need = nerf_linear_wgrad_workspace(M, N, L.ktot);
     if (!workspace || workspace_bytes < need || !aligned16(workspace)) return NERF_ERR_WORKSPACE;
     float* slab = reinterpret_cast<float*>(workspace);
@@ -1356,8 +1390,8 @@ extern "C" int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N, c
     int64_t mps = (M + splits - 1) / splits;
     mps = ((mps + TBM - 1) / TBM) * TBM;
     TNArgs a{dY, ld_dy, N, L, (int)M, (int)mps, splits, slab, db_slab};
-    if ((N > 128 || L.ktot > 128) && N <= 256 && L.ktot <= 256) {   // one 256 x 256 tile covers the layer
-        const int64_t blocks = (int64_t)splits * ((N + 255) / 256) * ((L.ktot + 255) / 256);
+    if ((N > 128 || L.ktot > 128) && N <= 257 && L.ktot <= 256) {   // one 256 x 256 tile (+ row 256)
+        const int64_t blocks = splits;
         hipLaunchKernelGGL((linear_wgrad_x3_stream_kernel<3, 2>), dim3((unsigned)blocks), dim3(512), 0,
                            as_stream(stream), a, ntn * TB, ntk * TB);
         NERF_CHECK_LAUNCH();

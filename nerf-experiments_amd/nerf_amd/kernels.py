@@ -504,12 +504,15 @@ def linear_gauss_x3(segs, M: int, Wx: torch.Tensor, ldw: int, N: int, out: torch
 
 
 def linear_wgrad_x3(dY: torch.Tensor, N4: int, segs, M: int, workspace: torch.Tensor) -> None:
+    """Split-precision weight-gradient slabs (nerf_linear_wgrad_x3).  N4 is the row count: rounded
+    up to 4 over a padded dY, or the true count (257: one 256 x 256 tile + a vector-ALU row); the
+    workspace and the reduce take it rounded up to 4."""
     arr = make_segs(segs)
     kt = sum(k for _, k, _ in segs)
     # algorithmic bytes: dY and X read once, dW written once (the split-M slabs are the kernel's)
     # the C side runs one 256 x 256 tile per M split when the layer fits it (nerf_linear_wgrad_x3)
     kpad = sum(pad32(k) for _, k, _ in segs)
-    wide = (N4 > 128 or kpad > 128) and N4 <= 256 and kpad <= 256
+    wide = (N4 > 128 or kpad > 128) and N4 <= 257 and kpad <= 256
     end = TIMER.bracket("linear_wgrad_x3", 2.0 * M * N4 * kt, 4.0 * M * N4 + _segs_bytes(segs, M) + 4.0 * N4 * kt,
                         fn="linear_wgrad_x3_stream_kernel" if wide else "linear_wgrad_x3_kernel") \
         if TIMER is not None else None

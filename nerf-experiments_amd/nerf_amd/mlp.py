@@ -20,6 +20,7 @@ it, and a stale pack would silently train on old weights).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -44,6 +45,10 @@ def matmul_precision() -> str:
 
 
 PRECISION_OVERRIDE: str | None = None
+
+# the 257-row (density + feature) layer's split-precision weight gradient as one 256 x 256 tile + a
+# vector-ALU row (NERF_WGRAD_257=0: the 128-tile kernel over the row count padded to 260)
+WGRAD_ROW257 = os.environ.get("NERF_WGRAD_257", "1") != "0"
 
 # Gaussian activation fused into the split-precision GEMM epilogues (nerf_linear_gauss_x3); False
 # runs the separate nerf_gauss_act_fwd / _bwd passes (tests compare the two)
@@ -470,7 +475,8 @@ class MLPFunction(torch.autograd.Function):
             else:
                 gW, gb, acc = torch.empty_like(w), torch.empty_like(lp.module.bias), False
             if ctx.prec == "x3":
-                K.linear_wgrad_x3(dZ, N4, segs, M, workspace)
+                # the true row count: 257 (density + features) runs as one 256 x 256 tile + a row
+                K.linear_wgrad_x3(dZ, lp.N if (lp.N == 257 and WGRAD_ROW257) else N4, segs, M, workspace)
             else:
                 K.linear_wgrad(dZ, N4, segs, M, workspace)
             K.linear_wgrad_reduce(M, N4, lp.Kp, lp.N, workspace, lp.col_map, gW, gb, accumulate=acc)

@@ -345,7 +345,9 @@ def _split_bf16(W):
                                        # one 256 x 256 weight-gradient tile (LDS-DMA kernel): ragged
                                        # splits, per-ray rows, fewer chunks than ring slots
                                        (5003, 256, (200, 24), (1, 7)), (777, 200, (128, 60), (1, 3)),
-                                       (50, 256, (256,), (1,)), (10, 160, (64,), (1,))])
+                                       (50, 256, (256,), (1,)), (10, 160, (64,), (1,)),
+                                       # 257 rows by their true count: the 256 x 256 tile + row 256
+                                       (70000, 257, (256,), (1,)), (40, 257, (200,), (3,))])
 def test_linear_x3_fwd_wgrad(M, N, ks, rd):
     """3 x bf16 split-precision GEMMs (hi*hi + hi*lo + lo*hi, fp32 accumulate).
 
@@ -419,6 +421,15 @@ def test_linear_x3_fwd_wgrad(M, N, ks, rd):
     bw = 2.0 ** -15 * (dY[:, :N].T.double().abs() @ Xd.abs()) + 1e-6
     assert ((dW.cpu().double() - refw).abs() <= bw).all()
     np.testing.assert_allclose(db.cpu().numpy(), dY[:, :N].sum(0).numpy(), atol=2e-4, rtol=1e-4)
+    if N == 257:
+        # the true row count (nerf_linear_wgrad_x3 with N = 257: one 256 x 256 tile per split, row 256
+        # as fp32 FMAs on the vector ALUs); a NaN-filled workspace: every slab entry the reduce reads
+        # is written, rows past N are never read
+        ws.fill_(float("nan"))
+        K.linear_wgrad_x3(dY.to(DEV), N, segs, M, ws)
+        K.linear_wgrad_reduce(M, N4, Kp, N, ws, cmd, dW, db)
+        assert ((dW.cpu().double() - refw).abs() <= bw).all()
+        np.testing.assert_allclose(db.cpu().numpy(), dY[:, :N].sum(0).numpy(), atol=2e-4, rtol=1e-4)
 
 
 # ----------------------------------------------------------------------------- field MLP
