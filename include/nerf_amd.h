@@ -289,6 +289,14 @@ int nerf_linear_fwd_x3(const nerf_seg* segs, int32_t n_segs, int64_t M,
 int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N,
                          const nerf_seg* segs, int32_t n_segs, int64_t M,
                          void* workspace, size_t workspace_bytes, void* stream);
+/* The same over two blocks of rows summed into one gradient (the two passes of a field used
+ * twice per step: one launch and one reduce instead of two each): rows [0, M0) of (dY, segs),
+ * then rows [0, M1) of (dY1, segs1), whose segments have the same widths; workspace and reduce
+ * for M = M0 + M1.  M1 = 0: nerf_linear_wgrad_x3. */
+int nerf_linear_wgrad_x3_rows(const float* dY, int64_t ld_dy, const nerf_seg* segs, int64_t M0,
+                              const float* dY1, int64_t ld_dy1, const nerf_seg* segs1, int64_t M1,
+                              int32_t n_segs, int32_t N, void* workspace, size_t workspace_bytes,
+                              void* stream);
 int nerf_pack_weight_x3(const float* W, int32_t N, int32_t K_orig, const int32_t* col_map,
                         int32_t Kp, void* Wp_x, void* Wt_x, int32_t ldwt, void* stream);
 

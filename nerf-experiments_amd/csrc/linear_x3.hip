@@ -745,6 +745,12 @@ struct TNArgs {
     int splits;
     float* slab;
     float* db_slab;
+    // a second block of rows (the other pass of a field used twice per step): rows m >= M0 read
+    // dY1 / X1 row m - M0 (M0 = M and the block unused for a single block); X1 has X's segment
+    // structure, only its pointers, row strides and row divisors differ
+    int M0;
+    const float* dY1; int64_t lddy1;
+    const float* x1ptr[MAX_SEGS]; int64_t x1ld[MAX_SEGS]; int x1rd[MAX_SEGS];
 };
 
 __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
@@ -781,9 +787,9 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
     const int st = t & 127;
     const int cg = st & 31;              // column group (4 columns)
     const int rg = st >> 5;              // row group (8 samples) of the 32-sample stage
-    const float* gptr;
-    int64_t gld;
-    unsigned grd = 1;
+    const float *gptr, *gptr1;
+    int64_t gld, gld1;
+    unsigned grd = 1, grd1 = 1;
     bool col_ok;
     int gcol;
     if (!isx) {
@@ -791,6 +797,8 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
         col_ok = gcol < a.N;
         gptr = a.dY;
         gld = a.lddy;
+        gptr1 = a.dY1;
+        gld1 = a.lddy1;
     } else {
         const int kx = k0 + cg * 4;
         int xs = -1, xoff = 0;
@@ -801,6 +809,9 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
         gptr = col_ok ? pick4(a.X.ptr, xs) : a.dY;
         gld = col_ok ? pick4(a.X.ld, xs) : 0;
         grd = col_ok ? (unsigned)pick4(a.X.row_div, xs) : 1u;
+        gptr1 = col_ok ? pick4(a.x1ptr, xs) : a.dY;
+        gld1 = col_ok ? pick4(a.x1ld, xs) : 0;
+        grd1 = col_ok ? (unsigned)pick4(a.x1rd, xs) : 1u;
         gcol = xoff;
     }
     if (!col_ok) gcol = 0;
@@ -818,15 +829,17 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
     unsigned mmask = 0;
     // waves whose lanes all read one source row per sample take the pointer walk below (decided
     // per wave: a wave mixing the two forms would run both)
-    const bool wave_rd1 = __ballot(grd != 1u) == 0;
+    const bool wave_rd1 = __ballot(grd != 1u || grd1 != 1u) == 0;
     auto gload = [&](int mc) __attribute__((always_inline)) {
         const int m0 = mc + rg * 8;
-        if (wave_rd1 && m0 + 8 <= mend) {
-            // all 8 rows inside the split, one source row per sample: a pointer walk
-            const float* p = gptr + (int64_t)m0 * gld + gcol;
+        const bool in1 = m0 >= a.M0;                    // the 8 rows' block (when they share one)
+        if (wave_rd1 && m0 + 8 <= mend && (in1 || m0 + 8 <= a.M0)) {
+            // all 8 rows inside the split and one block, one source row per sample: a pointer walk
+            const int64_t ld = in1 ? gld1 : gld;
+            const float* p = (in1 ? gptr1 : gptr) + (int64_t)(in1 ? m0 - a.M0 : m0) * ld + gcol;
             mmask = 0xffu;
 #pragma unroll
-            for (int r = 0; r < 8; ++r, p += gld) rv[r] = *reinterpret_cast<const f4*>(p);
+            for (int r = 0; r < 8; ++r, p += ld) rv[r] = *reinterpret_cast<const f4*>(p);
         } else {
             mmask = 0;
 #pragma unroll
@@ -834,8 +847,11 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
                 const int m = m0 + r;
                 const bool mok = m < mend;
                 mmask |= (mok ? 1u : 0u) << r;
-                const unsigned mm = (unsigned)(mok ? m : mbeg);
-                rv[r] = *reinterpret_cast<const f4*>(gptr + (int64_t)(grd == 1u ? mm : mm / grd) * gld + gcol);
+                const int mm = mok ? m : mbeg;
+                const bool b1 = mm >= a.M0;
+                const unsigned row = (unsigned)(b1 ? mm - a.M0 : mm), rd = b1 ? grd1 : grd;
+                rv[r] = *reinterpret_cast<const f4*>((b1 ? gptr1 : gptr) + (int64_t)(rd == 1u ? row : row / rd) *
+                                                                              (b1 ? gld1 : gld) + gcol);
             }
         }
     };
@@ -982,6 +998,9 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     const float* dxp = dx_ok ? pick4(a.X.ptr, dxs) + dxoff : a.X.ptr[0];
     const int64_t dxld = dx_ok ? pick4(a.X.ld, dxs) : a.X.ld[0];
     const unsigned dxrd = dx_ok ? (unsigned)pick4(a.X.row_div, dxs) : (unsigned)a.X.row_div[0];
+    const float* dxp1 = dx_ok ? pick4(a.x1ptr, dxs) + dxoff : a.x1ptr[0];     // the second block's
+    const int64_t dxld1 = dx_ok ? pick4(a.x1ld, dxs) : a.x1ld[0];
+    const unsigned dxrd1 = dx_ok ? (unsigned)pick4(a.x1rd, dxs) : (unsigned)a.x1rd[0];
     // wave w brings rows 2w, 2w + 1 of both operands.  Lanes whose 4 columns lie past N / the
     // packed K fetch nothing (their LDS bytes keep stale values, zeroed by the conversion's column
     // mask): a 64-column X (the first layer) moves 256 B per row, not 1 KB.  Lane 0's columns are
@@ -995,10 +1014,13 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             const int r = 2 * wave + q;
             int m = mbeg + step * WS_T + r;
             m = m < mend ? m : mbeg;                       // past the split: any valid row (zeroed)
-            const float* ys = a.dY + (int64_t)m * a.lddy + ycol;
+            const bool b1 = m >= a.M0;                     // wave-uniform: the row's block
+            const int mr = b1 ? m - a.M0 : m;
+            const float* ys = (b1 ? a.dY1 : a.dY) + (int64_t)mr * (b1 ? a.lddy1 : a.lddy) + ycol;
             if (y_fetch) __builtin_amdgcn_global_load_lds((glb_void_t*)ys, (lds_void_t*)(st + r * 1024), 16, 0, 0);
-            const unsigned xr = dxrd == 1u ? (unsigned)m : (unsigned)m / dxrd;
-            const float* xsrc = dxp + (int64_t)xr * dxld;
+            const unsigned rd = b1 ? dxrd1 : dxrd;
+            const unsigned xr = rd == 1u ? (unsigned)mr : (unsigned)mr / rd;
+            const float* xsrc = (b1 ? dxp1 : dxp) + (int64_t)xr * (b1 ? dxld1 : dxld);
             if (x_fetch)
                 __builtin_amdgcn_global_load_lds((glb_void_t*)xsrc, (lds_void_t*)(st + (WS_T + r) * 1024), 16, 0, 0);
         }
@@ -1026,7 +1048,9 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         for (int r = 0; r < WS_T; ++r) {
             int m = mbeg + step * WS_T + r;
             m = m < mend ? m : mbeg;
-            yd[r] = *(const __attribute__((address_space(4))) float*)(a.dY + (int64_t)m * a.lddy + 256);
+            const bool b1 = m >= a.M0;
+            yd[r] = *(const __attribute__((address_space(4))) float*)((b1 ? a.dY1 : a.dY) +
+                                                                       (int64_t)(b1 ? m - a.M0 : m) * (b1 ? a.lddy1 : a.lddy) + 256);
         }
     };
     // the conversion in two halves, so that a step's ring reads can be issued ahead of the MFMAs
@@ -1373,11 +1397,14 @@ extern "C" int nerf_linear_gauss_x3(const nerf_seg* segs, int32_t n_segs, int64_
     return nerf::gauss_reduce(part, slabs, N, inv_std, grad_inv_std, accumulate, part + slabs * N, st);
 }
 
-extern "C" int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N, const nerf_seg* segs, int32_t n_segs,
-                                    int64_t M, void* workspace, size_t workspace_bytes, void* stream) {
+extern "C" int nerf_linear_wgrad_x3_rows(const float* dY, int64_t ld_dy, const nerf_seg* segs, int64_t M0,
+                                         const float* dY1, int64_t ld_dy1, const nerf_seg* segs1, int64_t M1,
+                                         int32_t n_segs, int32_t N, void* workspace, size_t workspace_bytes,
+                                         void* stream) {
     // N need not be a multiple of 4: the kernels read dY in 4-column pieces up to pad4(N) <= ld_dy;
     // slab rows past N are left unspecified (nerf_linear_wgrad_reduce's n_valid <= N)
-    NERF_REQUIRE(dY && N >= 1 && M >= 0 && M < (1ll << 31) && aligned16(dY) && (ld_dy % 4) == 0 &&
+    const int64_t M = M0 + M1;
+    NERF_REQUIRE(dY && N >= 1 && M0 >= 0 && M1 >= 0 && M < (1ll << 31) && aligned16(dY) && (ld_dy % 4) == 0 &&
                  ld_dy >= (N + 3) / 4 * 4);
     SegList L;
     NERF_REQUIRE(build_segs(segs, n_segs, L));
@@ -1389,7 +1416,29 @@ extern "C" int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N, c
     float* db_slab = slab + (size_t)splits * ntn * TB * (size_t)ntk * TB;
     int64_t mps = (M + splits - 1) / splits;
     mps = ((mps + TBM - 1) / TBM) * TBM;
-    TNArgs a{dY, ld_dy, N, L, (int)M, (int)mps, splits, slab, db_slab};
+    TNArgs a{dY, ld_dy, N, L, (int)M, (int)mps, splits, slab, db_slab, (int)M0, dY, ld_dy, {}, {}, {}};
+    for (int i = 0; i < MAX_SEGS; ++i) {
+        a.x1ptr[i] = L.ptr[i];
+        a.x1ld[i] = L.ld[i];
+        a.x1rd[i] = L.row_div[i];
+    }
+    if (M1 > 0) {
+        // the second block: the same segment structure (widths, packed offsets), its own rows
+        NERF_REQUIRE(dY1 && aligned16(dY1) && (ld_dy1 % 4) == 0 && ld_dy1 >= (N + 3) / 4 * 4);
+        SegList L1;
+        NERF_REQUIRE(build_segs(segs1, n_segs, L1) && L1.n == L.n && L1.ktot == L.ktot);
+        for (int i = 0; i < L.n; ++i) NERF_REQUIRE(L1.k[i] == L.k[i] && L1.kp[i] == L.kp[i]);
+        a.dY1 = dY1;
+        a.lddy1 = ld_dy1;
+        for (int i = 0; i < MAX_SEGS; ++i) {
+            a.x1ptr[i] = L1.ptr[i];
+            a.x1ld[i] = L1.ld[i];
+            a.x1rd[i] = L1.row_div[i];
+        }
+    } else {
+        a.M0 = (int)M;
+    }
+    // (M = 0 still launches: every split writes its zero slab, which the reduce reads)
     if ((N > 128 || L.ktot > 128) && N <= 257 && L.ktot <= 256) {   // one 256 x 256 tile (+ row 256)
         const int64_t blocks = splits;
         hipLaunchKernelGGL((linear_wgrad_x3_stream_kernel<3, 2>), dim3((unsigned)blocks), dim3(512), 0,
@@ -1401,6 +1450,12 @@ extern "C" int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N, c
     hipLaunchKernelGGL(linear_wgrad_x3_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
     NERF_CHECK_LAUNCH();
     return NERF_OK;
+}
+
+extern "C" int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N, const nerf_seg* segs, int32_t n_segs,
+                                    int64_t M, void* workspace, size_t workspace_bytes, void* stream) {
+    return nerf_linear_wgrad_x3_rows(dY, ld_dy, segs, M, nullptr, 0, nullptr, 0, n_segs, N, workspace,
+                                     workspace_bytes, stream);
 }
 
 extern "C" int nerf_pack_weight_x3(const float* W, int32_t N, int32_t K_orig, const int32_t* col_map, int32_t Kp,

@@ -401,10 +401,12 @@ struct LayerState {
 // by a shift / a mask instead of a second conversion)
 __device__ __forceinline__ void split2(float x, float y, unsigned& hi, unsigned& lo) {
     typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    typedef float f2 __attribute__((ext_vector_type(2)));
     const bf16x2 h = __builtin_convertvector((f4{x, y, 0.f, 0.f}).xy, bf16x2);
     hi = __builtin_bit_cast(unsigned, h);
-    const float hx = __builtin_bit_cast(float, hi << 16), hy = __builtin_bit_cast(float, hi & 0xffff0000u);
-    lo = __builtin_bit_cast(unsigned, __builtin_convertvector((f4{x - hx, y - hy, 0.f, 0.f}).xy, bf16x2));
+    const f2 hf = {__builtin_bit_cast(float, hi << 16), __builtin_bit_cast(float, hi & 0xffff0000u)};
+    const f2 d = f2{x, y} - hf;                     // one packed subtract (exact: hi is x rounded)
+    lo = __builtin_bit_cast(unsigned, __builtin_convertvector(d, bf16x2));
 }
 
 #if NERF_FUSED_PAIR
@@ -507,7 +509,7 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const unsigned word = st.mi[sb][2 * r] ^ ((st.mi[sb][2 * r] ^ st.mi[sb][2 * r + 1]) & hm);
-                const int keep = sec ? -1 : -(int)((word >> sh) & 1u);
+                const int keep = sec ? -1 : __builtin_amdgcn_sbfe((int)word, (unsigned)sh, 1u);   // 0 / -1
                 // (through a scalar: __builtin_bit_cast of the vector element lvalue v[r] reads element 0)
                 const float x = v[r];
                 v[r] = __builtin_bit_cast(float, __builtin_bit_cast(int, x) & keep);
@@ -584,6 +586,22 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
     }
 }
 
+// Epilogue parts in the MFMA stream: the parts that do anything (1 only with SB = 2) go to
+// consecutive register-fed stages from EPI0 on, part 3 (the hi/lo split into the next layer's
+// operand image) included when the chunk has the stages (NERF_FUSED_P3S = 1; 0: part 3 after the
+// chunk's HBM-fed MFMAs, as parts that do not fit)
+#ifndef NERF_FUSED_P3S
+#define NERF_FUSED_P3S 1
+#endif
+constexpr int EPI_NP = NERF_FUSED_P3S ? (SB > 1 ? 4 : 3) : 3;   // parts placed in stages
+__host__ __device__ constexpr int epi_part_of(int i) {         // i-th placed part
+    return (NERF_FUSED_P3S && SB == 1) ? (i == 0 ? 0 : i + 1) : i;
+}
+template <int KBR, int EPI0>
+__host__ __device__ constexpr int epi_placed() {                 // parts placed in the stages
+    return KBR - EPI0 < EPI_NP ? (KBR - EPI0 > 0 ? KBR - EPI0 : 0) : EPI_NP;
+}
+
 // k-steps of weight fragments read ahead of the step being multiplied
 #ifndef NERF_FUSED_FA
 #define NERF_FUSED_FA 2
@@ -610,6 +628,9 @@ __device__ __forceinline__ void reg_steps(Ctx& c, LayerState& st, unsigned sa, b
         bf16x8(&f)[2] = fr[KB_I % FA];
         // this step's fragments have landed (the reads of the steps after it may still be in flight)
         constexpr int later = (KB_I + FA - 1 < KBR - 1 ? KB_I + FA - 1 : KBR - 1) - KB_I;
+        // (epilogue part 3's operand-image writes in the previous stage may land on either side of
+        // that stage's fragment reads — the asm reads carry no memory clobber — so they are not
+        // counted as younger: waiting for them too is the safe side)
         lds_wait<2 * later>(f[0], f[1]);
         // products lo*hi + hi*lo + hi*hi per accumulator (small terms first, as linear_x3.hip)
 #pragma unroll
@@ -625,7 +646,8 @@ __device__ __forceinline__ void reg_steps(Ctx& c, LayerState& st, unsigned sa, b
         // (placing the epilogue parts of the two waves of a SIMD at different stages, 0-2 and 4-6,
         // measured slower: chain 3.78 -> 4.03-4.09 ms, forward 3.86 -> 3.94-4.00 per mip step)
         if constexpr (KB_I == EPI0) bias_wait<(KBR > 0 ? DMA_PER_WAVE : 0) + 2 * KBH>(pb);
-        if constexpr (KB_I >= EPI0 && KB_I < EPI0 + 3) epi_part<MODE>(c, st, KB_I - EPI0, ch - 1, pv, pb);
+        if constexpr (KB_I >= EPI0 && KB_I < EPI0 + epi_placed<KBR, EPI0>())
+            epi_part<MODE>(c, st, epi_part_of(KB_I - EPI0), ch - 1, pv, pb);
         __builtin_amdgcn_sched_barrier(0);
         reg_steps<MODE, KBR, KBH, KB_I + 1>(c, st, sa, fr, a, pv, pb, ch);
     }
@@ -796,8 +818,10 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
             __builtin_amdgcn_sched_barrier(0);
         }
         if constexpr (KBR == 0) bias_wait<0>(pb);
+        // the parts the stages did not take (all of them for the first layer)
 #pragma unroll
-        for (int p = KBR >= EPI0 + 3 ? 3 : (KBR > EPI0 ? KBR - EPI0 : 0); p < 4; ++p) epi_part<MODE>(c, st, p, ch - 1, pv, pb);
+        for (int i = epi_placed<KBR, EPI0>(); i < EPI_NP; ++i) epi_part<MODE>(c, st, epi_part_of(i), ch - 1, pv, pb);
+        if constexpr (!NERF_FUSED_P3S) epi_part<MODE>(c, st, 3, ch - 1, pv, pb);
         if constexpr (KBR > 0) c.cur ^= 1;
 #pragma unroll
         for (int sb = 0; sb < SB; ++sb) pv[sb] = a[sb];

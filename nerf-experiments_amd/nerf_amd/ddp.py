@@ -126,6 +126,9 @@ class BucketedGradAllReduce:
         self._owned = {id(p) for p in plist}
         self._expected: dict[int, int] = {}
         self._arrived: dict[int, int] = {}
+        # (MLP, layer) -> ((dY, X, rows, ...), flush): a weight gradient held back for the other
+        # pass of a field used twice per step (nerf_amd.mlp: one launch over both passes' rows)
+        self.stash: dict = {}
         if direct:
             from . import mlp
             if mlp.GRAD_SINK is not None and mlp.GRAD_SINK is not self:
@@ -179,6 +182,10 @@ class BucketedGradAllReduce:
             return p.grad, False
         return p.grad, True
 
+    def remaining(self, p) -> int:
+        """Contributions of p still expected this step (claimed, not yet landed)."""
+        return self._expected.get(id(p), 0) - self._arrived.get(id(p), 0)
+
     def landed(self, p) -> None:
         k = id(p)
         n = self._arrived.get(k, 0) + 1
@@ -225,6 +232,10 @@ class BucketedGradAllReduce:
             self._next += 1
 
     def finish(self) -> None:
+        # weight gradients held back for a pass whose backward never ran: computed alone now
+        pending, self.stash = list(self.stash.values()), {}
+        for entry, flush in pending:
+            flush(entry, self)
         arrived = self._arrived
         self._expected, self._arrived = {}, {}
         if not self.active:

@@ -523,6 +523,29 @@ def linear_wgrad_x3(dY: torch.Tensor, N4: int, segs, M: int, workspace: torch.Te
     _lib.check(st, "nerf_linear_wgrad_x3")
 
 
+def linear_wgrad_x3_rows(blocks, N4: int, workspace: torch.Tensor) -> None:
+    """Split-precision weight-gradient slabs over two blocks of rows summed into one gradient
+    (nerf_linear_wgrad_x3_rows): blocks = [(dY, segs, M), (dY1, segs1, M1)], the segments of the
+    same widths; the workspace and the reduce take M + M1."""
+    (dY, segs, M), (dY1, segs1, M1) = blocks
+    if any(k != k1 for (_, k, _), (_, k1, _) in zip(segs, segs1)) or len(segs) != len(segs1):
+        raise ValueError("linear_wgrad_x3_rows: the blocks' segments differ in width")
+    a0, a1 = make_segs(segs), make_segs(segs1)
+    kt = sum(k for _, k, _ in segs)
+    kpad = sum(pad32(k) for _, k, _ in segs)
+    wide = (N4 > 128 or kpad > 128) and N4 <= 257 and kpad <= 256
+    end = TIMER.bracket("linear_wgrad_x3", 2.0 * (M + M1) * N4 * kt,
+                        4.0 * (M + M1) * N4 + _segs_bytes(segs, M) + _segs_bytes(segs1, M1) + 4.0 * N4 * kt,
+                        fn="linear_wgrad_x3_stream_kernel" if wide else "linear_wgrad_x3_kernel") \
+        if TIMER is not None else None
+    st = _lib.load().nerf_linear_wgrad_x3_rows(_ptr(dY), dY.stride(0), a0, M, _ptr(dY1), dY1.stride(0), a1, M1,
+                                               len(segs), N4, _ptr(workspace),
+                                               workspace.numel() * workspace.element_size(), _stream(dY.device))
+    if end is not None:
+        end.record()
+    _lib.check(st, "nerf_linear_wgrad_x3_rows")
+
+
 def pack_weight_x3(W: torch.Tensor, col_map: torch.Tensor, Kp: int, Wpx: torch.Tensor | None,
                    Wtx: torch.Tensor | None, ldwt: int) -> None:
     N, K_orig = W.shape

@@ -50,6 +50,35 @@ PRECISION_OVERRIDE: str | None = None
 # vector-ALU row (NERF_WGRAD_257=0: the 128-tile kernel over the row count padded to 260)
 WGRAD_ROW257 = os.environ.get("NERF_WGRAD_257", "1") != "0"
 
+# With a direct gradient sink, the split-precision weight gradient of a field used twice per step
+# (coarse and fine passes of one NerfModel) runs once over both passes' rows: the first backward
+# stashes each layer's (dY, X) in the sink, the second sums both blocks in one launch and one
+# reduce (nerf_linear_wgrad_x3_rows; NERF_MERGE_PASSES=0: one launch per pass and an accumulating
+# reduce).  The result differs from the per-pass sum only in fp32 summation order.
+MERGE_PASSES = os.environ.get("NERF_MERGE_PASSES", "1") != "0"
+
+
+def _wgrad_workspace(ws: torch.Tensor, M: int, N4: int, Kp: int) -> torch.Tensor:
+    need = K.linear_wgrad_workspace_bytes(M, N4, Kp)
+    if ws.numel() * ws.element_size() >= need:
+        return ws
+    return torch.empty((need + 3) // 4, device=ws.device, dtype=torch.float32)
+
+
+def _flush_wgrad(entry, sink) -> None:
+    """A stashed pass whose partner never ran its backward (BucketedGradAllReduce.finish()): its
+    weight gradient alone, landed as the sink expects."""
+    dZ, segs, M, nrow, N4, lp = entry
+    w, b = lp.module.weight, lp.module.bias
+    gW, acc = sink.target(w)
+    gb, _ = sink.target(b)
+    ws = torch.empty((K.linear_wgrad_workspace_bytes(M, N4, lp.Kp) + 3) // 4, device=dZ.device, dtype=torch.float32)
+    K.linear_wgrad_x3(dZ, nrow, segs, M, ws)
+    K.linear_wgrad_reduce(M, N4, lp.Kp, lp.N, ws, lp.col_map, gW, gb, accumulate=acc)
+    sink.landed(w)
+    sink.landed(b)
+
+
 # Gaussian activation fused into the split-precision GEMM epilogues (nerf_linear_gauss_x3); False
 # runs the separate nerf_gauss_act_fwd / _bwd passes (tests compare the two)
 GAUSS_EPILOGUE = True
@@ -467,24 +496,41 @@ class MLPFunction(torch.autograd.Function):
                 segs.append((t, s.k_seg, rd))
             # ---- weight and bias gradients
             N4 = (lp.N + 3) // 4 * 4
-            if sink is not None:
-                gW, acc = sink.target(w)
-                gb, acc_b = sink.target(lp.module.bias)
-                if acc != acc_b:
-                    raise RuntimeError("direct gradient sink: weight and bias of one layer out of step")
+            # the true row count: 257 (density + features) runs as one 256 x 256 tile + a row
+            nrow = lp.N if (lp.N == 257 and WGRAD_ROW257) else N4
+            merge = sink is not None and ctx.prec == "x3" and MERGE_PASSES and gs is None
+            prev = sink.stash.pop((id(plan), li), (None, None))[0] if merge else None
+            if merge and prev is None and sink.remaining(w) >= 2:
+                # another pass of this field lands its contribution later in this backward: its
+                # weight gradient runs once over both passes' rows (one launch, one reduce); the
+                # sink flushes the stash alone if that pass never comes
+                sink.stash[(id(plan), li)] = ((dZ, segs, M, nrow, N4, lp), _flush_wgrad)
+                layer_grads[li] = [None, None]
             else:
-                gW, gb, acc = torch.empty_like(w), torch.empty_like(lp.module.bias), False
-            if ctx.prec == "x3":
-                # the true row count: 257 (density + features) runs as one 256 x 256 tile + a row
-                K.linear_wgrad_x3(dZ, lp.N if (lp.N == 257 and WGRAD_ROW257) else N4, segs, M, workspace)
-            else:
-                K.linear_wgrad(dZ, N4, segs, M, workspace)
-            K.linear_wgrad_reduce(M, N4, lp.Kp, lp.N, workspace, lp.col_map, gW, gb, accumulate=acc)
-            if sink is not None:
-                sink.landed(w)
-                sink.landed(lp.module.bias)
-                gW = gb = None
-            layer_grads[li] = [gW, gb] + ([gs] if gs is not None else [])
+                if sink is not None:
+                    gW, acc = sink.target(w)
+                    gb, acc_b = sink.target(lp.module.bias)
+                    if acc != acc_b:
+                        raise RuntimeError("direct gradient sink: weight and bias of one layer out of step")
+                else:
+                    gW, gb, acc = torch.empty_like(w), torch.empty_like(lp.module.bias), False
+                if prev is not None:
+                    pdZ, psegs, pM = prev[0], prev[1], prev[2]
+                    ws = _wgrad_workspace(workspace, M + pM, N4, lp.Kp)
+                    K.linear_wgrad_x3_rows([(pdZ, psegs, pM), (dZ, segs, M)], nrow, ws)
+                    K.linear_wgrad_reduce(M + pM, N4, lp.Kp, lp.N, ws, lp.col_map, gW, gb, accumulate=acc)
+                elif ctx.prec == "x3":
+                    K.linear_wgrad_x3(dZ, nrow, segs, M, workspace)
+                    K.linear_wgrad_reduce(M, N4, lp.Kp, lp.N, workspace, lp.col_map, gW, gb, accumulate=acc)
+                else:
+                    K.linear_wgrad(dZ, N4, segs, M, workspace)
+                    K.linear_wgrad_reduce(M, N4, lp.Kp, lp.N, workspace, lp.col_map, gW, gb, accumulate=acc)
+                if sink is not None:
+                    for _ in range(2 if prev is not None else 1):     # the stashed pass's too
+                        sink.landed(w)
+                        sink.landed(lp.module.bias)
+                    gW = gb = None
+                layer_grads[li] = [gW, gb] + ([gs] if gs is not None else [])
             # ---- input gradients
             if chain:
                 continue

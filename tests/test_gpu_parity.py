@@ -432,6 +432,43 @@ def test_linear_x3_fwd_wgrad(M, N, ks, rd):
         np.testing.assert_allclose(db.cpu().numpy(), dY[:, :N].sum(0).numpy(), atol=2e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize("M0,M1,N,ks,rd0,rd1", [(3000, 5000, 256, (256,), (1,), (1,)),
+                                                (70000, 33333, 257, (256,), (1,), (1,)),
+                                                (2000, 1500, 256, (256, 64), (1, 1), (1, 1)),
+                                                (4096, 2048, 128, (256, 32), (1, 64), (1, 32)),
+                                                (1000, 37, 260, (200,), (1,), (3,))])
+def test_linear_x3_wgrad_two_row_blocks(M0, M1, N, ks, rd0, rd1):
+    """nerf_linear_wgrad_x3_rows: the weight gradient of two passes' rows (own dY / X pointers,
+    row strides and row divisors) in one launch and one reduce, against fp64 over the
+    concatenated rows with the split-precision bound; the row-256 path (N = 257) included."""
+    from nerf_amd import kernels as K
+    torch.manual_seed(M0 + M1 + N)
+    N4 = (N + 3) // 4 * 4
+    Kp = sum(K.pad32(k) for k in ks)
+    blocks, Xs, Ys = [], [], []
+    for M, rd, ld_extra in ((M0, rd0, 0), (M1, rd1, 8)):
+        segs_cpu = [torch.randn((M + r - 1) // r, k) for k, r in zip(ks, rd)]
+        dY = torch.randn(M, N4 + ld_extra)
+        dY[:, N:] = 0
+        Xs.append(torch.cat([sg.repeat_interleave(r, dim=0)[:M] for sg, r in zip(segs_cpu, rd)], dim=1))
+        Ys.append(dY[:, :N])
+        blocks.append((dY.to(DEV), [(sg.to(DEV), k, r) for sg, k, r in zip(segs_cpu, ks, rd)], M))
+    ws = torch.full(((K.linear_wgrad_workspace_bytes(M0 + M1, N4, Kp) + 3) // 4,), float("nan"), device=DEV)
+    K.linear_wgrad_x3_rows(blocks, N, ws)
+    cm = []
+    for k in ks:
+        cm += [len([c for c in cm if c >= 0]) + j for j in range(k)] + [-1] * (K.pad32(k) - k)
+    dW = torch.empty(N, sum(ks), device=DEV)
+    db = torch.empty(N, device=DEV)
+    K.linear_wgrad_reduce(M0 + M1, N4, Kp, N, ws, torch.tensor(cm, dtype=torch.int32, device=DEV), dW, db)
+    X = torch.cat(Xs).double()
+    Y = torch.cat(Ys).double()
+    refw = Y.T @ X
+    bw = 2.0 ** -15 * (Y.abs().T @ X.abs()) + 1e-6
+    assert ((dW.cpu().double() - refw).abs() <= bw).all()
+    np.testing.assert_allclose(db.cpu().numpy(), Y.sum(0).numpy(), atol=2e-4, rtol=1e-4)
+
+
 # ----------------------------------------------------------------------------- field MLP
 def _make_models():
     from nerf_amd import BarfPositionalEncoding, FourierFeatures, NerfModel
