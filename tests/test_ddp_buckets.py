@@ -27,6 +27,9 @@ def _free_port():
 def _setup_env(rank, world, port):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
+    # groups this module initialises itself rendezvous through a file (no TCP port to race for);
+    # bench.init_distributed (env://) keeps MASTER_PORT
+    os.environ["NERF_GLOO_RDV"] = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"nerf_gloo_{port}_{world}")
     for p in (ROOT, os.path.join(ROOT, "nerf-experiments_amd")):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -65,7 +68,8 @@ def _worker_grads(rank, world, port, q):
     try:
         _setup_env(rank, world, port)
         import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", init_method="file://" + os.environ["NERF_GLOO_RDV"], rank=rank,
+                                world_size=world)
         from nerf_amd.ddp import BucketedGradAllReduce, shard_rays
         m, only1, unused = _model()
         ar = BucketedGradAllReduce(_params(m, only1, unused), bucket_bytes=48 * 1024)
@@ -108,7 +112,8 @@ def _worker_adam(rank, world, port, q):
     try:
         _setup_env(rank, world, port)
         import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", init_method="file://" + os.environ["NERF_GLOO_RDV"], rank=rank,
+                                world_size=world)
         from nerf_amd.ddp import BucketedGradAllReduce, shard_rays
         m, only1, unused = _model()
         opt = torch.optim.Adam(_params(m, only1, unused), lr=1e-3, eps=1e-5)
@@ -177,12 +182,17 @@ def _run(target, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
+    rdv = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"nerf_gloo_{port}_{world}")   # see _setup_env
+    if os.path.exists(rdv):
+        os.unlink(rdv)
     ps = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=240) for _ in range(world))
     for p in ps:
         p.join(timeout=60)
+    if os.path.exists(rdv):
+        os.unlink(rdv)
     for r in range(world):
         assert res[r] == "ok", f"rank {r}:\n{res[r]}"
 

@@ -10,17 +10,16 @@ import torch.multiprocessing as mp
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A rendezvous for the gloo group: a fresh file (file:// init, no TCP port to race for)."""
+    import tempfile
+    fd, path = tempfile.mkstemp(prefix="nerf_gloo_")
+    os.close(fd)
+    os.unlink(path)
+    return path
 
 
 def _worker(rank, world, port, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         import sys
         sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -44,9 +43,7 @@ def _worker(rank, world, port, q):
 def _worker_unused(rank, world, port, q):
     """A parameter used by one rank only keeps its gradient (mean over ranks); a parameter no rank
     used ends with grad None on every rank, as with one process."""
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         import sys
         sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -74,6 +71,8 @@ def test_grad_allreduce_unused_parameters_gloo_world2():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
+    if os.path.exists(port):
+        os.unlink(port)
     for r in (0, 1):
         ga, gb, cnone = res[r]
         assert torch.allclose(ga, torch.full((4,), 1.5))
@@ -92,6 +91,8 @@ def test_grad_allreduce_gloo_world2():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
+    if os.path.exists(port):
+        os.unlink(port)
     # reference: full-batch gradient on one process
     torch.manual_seed(0)
     model = torch.nn.Sequential(torch.nn.Linear(6, 16), torch.nn.ReLU(), torch.nn.Linear(16, 3))
