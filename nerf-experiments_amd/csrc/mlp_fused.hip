@@ -72,6 +72,11 @@ constexpr int RSRC_W3 = 0x00020000;
 #define NERF_FUSED_STORE_AUX 2
 #endif
 constexpr int ST_AUX = NERF_FUSED_STORE_AUX;
+// the input-gradient chain's stores (dY rows) on their own knob
+#ifndef NERF_FUSED_STORE_AUX_DG
+#define NERF_FUSED_STORE_AUX_DG NERF_FUSED_STORE_AUX
+#endif
+constexpr int ST_AUX_DG = NERF_FUSED_STORE_AUX_DG;
 // vector-memory ops issued after a chunk's DMA (at the start of its predecessor) before the chunk
 // starts: the predecessor's 4 epilogue stores (absent outputs included, as dropped stores) and the
 // bias load at the start of the chunk itself
@@ -395,6 +400,7 @@ struct LayerState {
     int last_even;            // NC - 1 for an odd chunk count (stored alone), else -1
 #endif
     unsigned mi[SB][8];   // mask_in: the sample rows of those bits
+    unsigned mcur[SB][4]; // the words of the current chunk's columns (mi[2 r], mi[2 r + 1], all ones)
 };
 
 // hi = bf16(v), lo = bf16(v - hi) of two values, packed (the rounded pair's halves read back as fp32
@@ -503,17 +509,35 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
             // column 16 ch + 4 g + r = 32 q + 16 bb + 4 g + r is bit 8 (q & 3) + 4 bb + g of word
             // 2 r + (q >> 2) (all ones without mask_in)
             const int sh = 8 * (q & 3) + 4 * bb + g;
-            // word 2 r or 2 r + 1 by a uniform bit mask (a select here becomes a runtime-indexed
-            // private array, i.e. scratch)
-            const unsigned hm = (unsigned)__builtin_amdgcn_readfirstlane(q >= 4 ? -1 : 0);
+            // word 2 r while q < 4, 2 r + 1 from chunk 8 on, all ones from the first out2 chunk on:
+            // chunks come in order, so the layer switches mcur twice by uniform branches (a per-chunk
+            // select of the two words cost three VALU per value)
+            if (ch == 8 && ch < st.n1) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) st.mcur[sb][r] = st.mi[sb][2 * r + 1];
+            }
+            if (ch == st.n1) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) st.mcur[sb][r] = ~0u;
+            }
+#ifndef NERF_FUSED_DIAG_NOMASKIN   // diagnostic: the ReLU bits not applied
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const unsigned word = st.mi[sb][2 * r] ^ ((st.mi[sb][2 * r] ^ st.mi[sb][2 * r + 1]) & hm);
-                const int keep = sec ? -1 : __builtin_amdgcn_sbfe((int)word, (unsigned)sh, 1u);   // 0 / -1
+                const int keep = __builtin_amdgcn_sbfe((int)st.mcur[sb][r], (unsigned)sh, 1u);   // 0 / -1
                 // (through a scalar: __builtin_bit_cast of the vector element lvalue v[r] reads element 0)
                 const float x = v[r];
                 v[r] = __builtin_bit_cast(float, __builtin_bit_cast(int, x) & keep);
             }
+#else
+            (void)sh;
+#endif
+#ifdef NERF_FUSED_DIAG_NOSTORE
+            return;
+#endif
+#ifdef NERF_FUSED_DIAG_DROPSTORE       // diagnostic: every chain store addressed past the buffer
+            st.colok = st.colok2 = -1 << 20;
+            st.pa[sb] = st.pb[sb] = st.pa2[sb] = st.pb2[sb] = st.row_off[sb] = st.row_off2[sb] = OOB;
+#endif
 #if NERF_FUSED_PAIR
             if (!pair_odd(ch)) {
                 // even chunk: held for the pair (alone if it is the layer's last); n1 is even, so
@@ -523,28 +547,28 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
                 const unsigned off1 = alone && !sec && 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
                 const unsigned off2 =
                     alone && sec && 16 * (ch - st.n1) < st.colok2 ? st.row_off2[sb] + 64u * (unsigned)(ch - st.n1) : OOB;
-                __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, off1, 0, ST_AUX);
-                __builtin_amdgcn_raw_buffer_store_b128(v, st.ro2, off2, 0, ST_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, off1, 0, ST_AUX_DG);
+                __builtin_amdgcn_raw_buffer_store_b128(v, st.ro2, off2, 0, ST_AUX_DG);
             } else if (!sec) {
                 f4 va, vb;
                 unsigned oa, ob;
                 pair_stores(c, st, sb, ch, st.colok, st.pa[sb], st.pb[sb], v, va, vb, oa, ob);
-                __builtin_amdgcn_raw_buffer_store_b128(va, st.ro, oa, 0, ST_AUX);
-                __builtin_amdgcn_raw_buffer_store_b128(vb, st.ro, ob, 0, ST_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(va, st.ro, oa, 0, ST_AUX_DG);
+                __builtin_amdgcn_raw_buffer_store_b128(vb, st.ro, ob, 0, ST_AUX_DG);
             } else {
                 f4 va, vb;
                 unsigned oa, ob;
                 pair_stores(c, st, sb, ch - st.n1, st.colok2, st.pa2[sb], st.pb2[sb], v, va, vb, oa, ob);
-                __builtin_amdgcn_raw_buffer_store_b128(va, st.ro2, oa, 0, ST_AUX);
-                __builtin_amdgcn_raw_buffer_store_b128(vb, st.ro2, ob, 0, ST_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(va, st.ro2, oa, 0, ST_AUX_DG);
+                __builtin_amdgcn_raw_buffer_store_b128(vb, st.ro2, ob, 0, ST_AUX_DG);
             }
 #else
             // one store to each output, the one not addressed dropped (a select of the two resources
             // or offsets here becomes a runtime-indexed private array, i.e. scratch)
             const unsigned off1 = !sec && ch >= 0 && 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
             const unsigned off2 = sec && 16 * (ch - st.n1) < st.colok2 ? st.row_off2[sb] + 64u * (unsigned)(ch - st.n1) : OOB;
-            __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, off1, 0, ST_AUX);
-            __builtin_amdgcn_raw_buffer_store_b128(v, st.ro2, off2, 0, ST_AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, off1, 0, ST_AUX_DG);
+            __builtin_amdgcn_raw_buffer_store_b128(v, st.ro2, off2, 0, ST_AUX_DG);
 #endif
         }
     } else if (p == 2) {
@@ -729,6 +753,8 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) st.mi[sb][i] = ~0u;
             }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) st.mcur[sb][r] = st.mi[sb][2 * r];
         }
     }
 
