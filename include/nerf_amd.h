@@ -45,7 +45,7 @@ extern "C" {
 #define NERF_ERR_LAUNCH (-3)
 #define NERF_ERR_WORKSPACE (-4)
 
-/* Library / ABI version (bumped on any signature change). */
+/* Library / ABI version (bumped on any signature or data-layout change; 6: NERF_FUSED_MASK). */
 int nerf_abi_version(void);
 const char* nerf_status_string(int status);
 /* sizeof of the argument structs, for bindings to check their layouts against:
@@ -315,12 +315,17 @@ int nerf_pack_weight_x3(const float* W, int32_t N, int32_t K_orig, const int32_t
  * (seg_gen): the position encoding of the samples o + tq d of rays, or the encoding of the
  * rays' directions, exactly as nerf_encode_fwd computes them (the first layer reading it also
  * stores the rows for the weight gradients).  out[m, n] for n < ldo (columns >= N are written as
- * 0), ReLU mask bits as NERF_EPI_MASKOUT (N <= 256), column col_idx (a multiple of 32)
+ * 0), ReLU mask bits in the NERF_FUSED_MASK layout (N <= 256), column col_idx (a multiple of 32)
  * additionally into col_out[m].  Buffers: byte extents < 2^31.
  * The same launch runs the input-gradient chain of the backward (layers in reverse, images of
  * W^T, no bias, mask_in instead of ReLU): each step's output is the previous layer's
  * pre-activation gradient, kept in registers for the next step and stored for the weight gradients.
  * ------------------------------------------------------------------------- */
+/* NERF_FUSED_MASK: row m of a fused mask buffer is 8 uint32 words at (char*)mask + 32 m; column
+ * n = 16 c + 4 g + r (c < 16, g, r < 4) is bit 4 (7 - (c & 7)) + r of word 2 g + (c >> 3) (each
+ * MFMA lane's own bits: the forward sets them and the chain reads them with no cross-lane step).
+ * A set bit marks a dead unit: !(out > 0).  It is not the NERF_EPI_MASKOUT layout (set bit =
+ * out > 0, other positions) of the layer-by-layer kernels. */
 #define NERF_FUSED_MAX_LAYERS 16
 typedef struct nerf_fused_layer {
     int32_t type;          /* 3*(kbr/4) + kbh */
@@ -338,11 +343,11 @@ typedef struct nerf_fused_layer {
     const float* seg_ptr[2];
     float* out;            /* [M][ldo] fp32; NULL with ldo 0 drops the layer's stores */
     int64_t ldo;
-    uint8_t* mask;         /* [M][32] ReLU bits or NULL */
+    uint8_t* mask;         /* [M][32] ReLU bits (NERF_FUSED_MASK) or NULL */
     float* col_out;        /* [M] or NULL */
     int64_t img_off;       /* byte offset of the layer's first chunk in the image */
     int64_t bias_off;      /* byte offset of the layer's [nb][32] fp32 biases in the image */
-    const uint8_t* mask_in;/* NULL, or [M][32] ReLU bits (NERF_EPI_MASKOUT layout) multiplied into the
+    const uint8_t* mask_in;/* NULL, or [M][32] ReLU bits (NERF_FUSED_MASK layout) multiplied into the
                               output (the input-gradient chain: dL/dz_{l-1} = (dL/dz_l W_l) * (z_{l-1} > 0)) */
     float* out2;           /* chunks >= n1 (input-gradient chain: the rows of an encoding input) go to
                               out2[m, 32 (chunk - n1) + ...] (row stride ldo2), unmasked, not fed forward */

@@ -152,7 +152,11 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
 }
 template <int OFF>
 __device__ __forceinline__ void lds_frag(bf16x8& f, unsigned addr) {
+#ifndef NERF_FUSED_DIAG_NOFRAG     // diagnostic builds only: MFMAs on stale fragments, no LDS reads
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f) : "v"(addr), "n"(OFF));
+#else
+    asm volatile("; %1" : "=v"(f) : "v"(addr));
+#endif
 }
 template <int N>
 __device__ __forceinline__ void lds_wait(bf16x8& f0, bf16x8& f1) {
@@ -174,6 +178,13 @@ __device__ __forceinline__ void buf_load16(f4& v, unsigned off, __amdgpu_buffer_
 }
 __device__ __forceinline__ void buf_load16(bf16x8& v, unsigned off, __amdgpu_buffer_rsrc_t r) {
     asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r));
+}
+
+// t + t + !(x > 0): shifts the "dead ReLU" bit of x in (v_cmp + v_addc; plain C came out as
+// compare, select and shift-or).  !(x > 0) holds for NaN, as the reference's (out > 0) is false.
+__device__ __forceinline__ unsigned shift_in_dead(unsigned t, float x) {
+    asm("v_cmp_nlt_f32 vcc, 0, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(t) : "v"(x) : "vcc");
+    return t;
 }
 
 // kernel modes: the forward (bias, ReLU, mask bits and column outputs) and the backward's
@@ -392,15 +403,15 @@ struct LayerState {
     unsigned sample_off[SB];  // sample * 4 for lane group 0 (OOB otherwise / past M)
     unsigned mrow_off[SB];    // this lane's 8 bytes of the sample's mask row (OOB past M)
     __amdgpu_buffer_rsrc_t ro, rm, rc, ro2;
-    unsigned mw[SB][2];   // ReLU mask words 2g, 2g + 1 of this lane's sample rows
+    unsigned mw[SB][2];   // this lane's ReLU mask words (NERF_FUSED_MASK layout; [1] accumulates)
 #if NERF_FUSED_PAIR
     f4 stash[SB];             // the even chunk's values, stored with the odd chunk's
     unsigned pa[SB], pb[SB];  // row offsets (+16 g) of the samples this lane writes in the pair's
     unsigned pa2[SB], pb2[SB];  // stores A (samples 0-7 of the block) and B (8-15), in out / out2
     int last_even;            // NC - 1 for an odd chunk count (stored alone), else -1
 #endif
-    unsigned mi[SB][8];   // mask_in: the sample rows of those bits
-    unsigned mcur[SB][4]; // the words of the current chunk's columns (mi[2 r], mi[2 r + 1], all ones)
+    unsigned mi[SB][2];   // mask_in: this lane's two words of the sample's bits (NERF_FUSED_MASK layout)
+    unsigned mcur[SB];    // the word of the current chunk (mi[0], mi[1] from chunk 8, zero past n1)
 };
 
 // hi = bf16(v), lo = bf16(v - hi) of two values, packed (the rounded pair's halves read back as fp32
@@ -467,7 +478,6 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
 #ifdef NERF_FUSED_DIAG_NOSPLIT    // diagnostic: no next-operand split / image writes
     if (p == 3) return;
 #endif
-    const int g = c.lane >> 4;
     const int q = ch >> 1, bb = ch & 1;
     if (p < 2) {
         if (p >= SB) return;
@@ -506,27 +516,23 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
 #endif
         } else {
             const bool sec = ch >= st.n1;          // an encoding input's rows (out2): not masked
-            // column 16 ch + 4 g + r = 32 q + 16 bb + 4 g + r is bit 8 (q & 3) + 4 bb + g of word
-            // 2 r + (q >> 2) (all ones without mask_in)
-            const int sh = 8 * (q & 3) + 4 * bb + g;
-            // word 2 r while q < 4, 2 r + 1 from chunk 8 on, all ones from the first out2 chunk on:
-            // chunks come in order, so the layer switches mcur twice by uniform branches (a per-chunk
-            // select of the two words cost three VALU per value)
-            if (ch == 8 && ch < st.n1) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) st.mcur[sb][r] = st.mi[sb][2 * r + 1];
-            }
-            if (ch == st.n1) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) st.mcur[sb][r] = ~0u;
-            }
+            // column 16 ch + 4 g + r is (dead) bit 4 (7 - (ch & 7)) + r of this lane's word ch >> 3 (zero
+            // without mask_in: an empty buffer reads 0); chunks come in order, so the layer switches
+            // mcur twice by uniform branches (to word 1 at chunk 8, to zero at the first out2 chunk).
+            // No chunk before 0 (its stores are dropped): the words are first read in the second
+            // chunk, after its DMA wait has covered their load
+            const int sh = 4 * (7 - (ch & 7));
+            if (ch == 8 && ch < st.n1) st.mcur[sb] = st.mi[sb][1];
+            if (ch == st.n1) st.mcur[sb] = 0u;
 #ifndef NERF_FUSED_DIAG_NOMASKIN   // diagnostic: the ReLU bits not applied
+            if (ch >= 0) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int keep = __builtin_amdgcn_sbfe((int)st.mcur[sb][r], (unsigned)sh, 1u);   // 0 / -1
-                // (through a scalar: __builtin_bit_cast of the vector element lvalue v[r] reads element 0)
-                const float x = v[r];
-                v[r] = __builtin_bit_cast(float, __builtin_bit_cast(int, x) & keep);
+                for (int r = 0; r < 4; ++r) {
+                    const int dead = __builtin_amdgcn_sbfe((int)st.mcur[sb], (unsigned)(sh + r), 1u);   // 0 / -1
+                    // (through a scalar: __builtin_bit_cast of the vector element lvalue v[r] reads element 0)
+                    const float x = v[r];
+                    v[r] = __builtin_bit_cast(float, __builtin_bit_cast(int, x) & ~dead);
+                }
             }
 #else
             (void)sh;
@@ -573,22 +579,26 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
         }
     } else if (p == 2) {
         if constexpr (MODE == MODE_FWD) {
-            // NERF_EPI_MASKOUT layout; byte r of t collects row r's bits over the lane groups, lane
-            // group g keeps the byte of r = g (a variant setting each lane's own bits in 8 words and
-            // OR-ing the lanes once per layer measured 0.13 ms slower per mip step)
-            const unsigned keep = (ch >= 0 && ch < 2 * KBMAX) ? 0xffu : 0u;
+            // NERF_FUSED_MASK layout: the lane's own bits, no cross-lane step.  The bits of rows
+            // 4 g + r of chunks 0-7 / 8-15 shift into a word of their own, !(a > 0) entering as the
+            // carry of t + t (two VALU per value; the NERF_EPI_MASKOUT layout's per-sample words
+            // took an OR across the lane groups and a word select: ~20 VALU per chunk, and the
+            // chain 8 words per sample).  Bits mark dead units, so that an absent mask reads as 0.
+            if (ch >= 0 && ch < 2 * KBMAX) {
 #pragma unroll
-            for (int sb = 0; sb < SB; ++sb) {
-                unsigned t = 0;
+                for (int sb = 0; sb < SB; ++sb) {
+                    unsigned t = st.mw[sb][1];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) t |= (a[sb][r] > 0.f ? 1u : 0u) << (8 * r + 4 * bb + g);
-                const auto x16 = __builtin_amdgcn_permlane16_swap(t, t, false, false);   // OR with lane ^ 16
-                t = x16[0] | x16[1];
-                const auto x32 = __builtin_amdgcn_permlane32_swap(t, t, false, false);   // OR with lane ^ 32
-                t = x32[0] | x32[1];
-                const unsigned byte = ((t >> (8 * g)) & keep) << (8 * (q & 3));
-                st.mw[sb][0] |= q < 4 ? byte : 0u;
-                st.mw[sb][1] |= q < 4 ? 0u : byte;
+                    for (int r = 3; r >= 0; --r) t = shift_in_dead(t, a[sb][r]);
+                    st.mw[sb][1] = t;
+                }
+                if (ch == 7) {
+#pragma unroll
+                    for (int sb = 0; sb < SB; ++sb) {
+                        st.mw[sb][0] = st.mw[sb][1];
+                        st.mw[sb][1] = 0;
+                    }
+                }
             }
         }
     } else {
@@ -741,20 +751,14 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
         const uint8_t* mi = LF(cu8ptr_t, mask_in, l);
         const __amdgpu_buffer_rsrc_t rmi =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(mi), 0, mi != nullptr ? c.M * 32 : 0, RSRC_W3);
-        typedef unsigned u4 __attribute__((ext_vector_type(4)));
 #pragma unroll
         for (int sb = 0; sb < SB; ++sb) {
-            const unsigned off = row_ok[sb] ? (unsigned)sample[sb] * 32u : OOB;
-            const u4 w0 = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rmi, off, 0, 0));
-            const u4 w1 = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rmi, off + 16, 0, 0));
-            st.mi[sb][0] = w0.x; st.mi[sb][1] = w0.y; st.mi[sb][2] = w0.z; st.mi[sb][3] = w0.w;
-            st.mi[sb][4] = w1.x; st.mi[sb][5] = w1.y; st.mi[sb][6] = w1.z; st.mi[sb][7] = w1.w;
-            if (mi == nullptr) {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) st.mi[sb][i] = ~0u;
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) st.mcur[sb][r] = st.mi[sb][2 * r];
+            const unsigned off = st.mrow_off[sb];
+            typedef unsigned u2 __attribute__((ext_vector_type(2)));
+            const u2 w = __builtin_bit_cast(u2, __builtin_amdgcn_raw_buffer_load_b64(rmi, off, 0, 0));
+            st.mi[sb][0] = w.x;
+            st.mi[sb][1] = w.y;
+            st.mcur[sb] = w.x;
         }
     }
 
@@ -860,7 +864,18 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
         for (int p = 0; p < 4; ++p) epi_part<MODE>(c, st, p, NC - 1, pv, lb);
     }
     if constexpr (MODE == MODE_FWD) {
-        // the sample rows' ReLU mask words 2g, 2g + 1
+        // the lane's two mask words, each chunk's nibble at 4 (7 - (ch & 7)) whatever the chunk count
+        const int nb = NC < 2 * KBMAX ? NC : 2 * KBMAX;
+        if (nb < 8) {
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) {
+                st.mw[sb][0] = st.mw[sb][1] << (4 * (8 - nb));
+                st.mw[sb][1] = 0;
+            }
+        } else if (nb > 8) {
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) st.mw[sb][1] <<= 4 * (16 - nb);
+        }
         typedef unsigned u2 __attribute__((ext_vector_type(2)));
 #pragma unroll
         for (int sb = 0; sb < SB; ++sb)

@@ -234,7 +234,7 @@ def load(path: str | None = None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.nerf_abi_version() != 5:
+    if lib.nerf_abi_version() != 6:
         raise RuntimeError("nerf_amd: ABI version mismatch between Python binding and libnerf_amd.so")
     for which, st in enumerate(STRUCTS):
         if lib.nerf_struct_size(which) != ctypes.sizeof(st):

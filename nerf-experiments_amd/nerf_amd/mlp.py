@@ -556,7 +556,9 @@ class MLPFunction(torch.autograd.Function):
                         epi |= NERF_EPI_TANH_BWD       # * (1 - y^2) from the stored activation
                         aux = acts[j]
                     if prod.relu:
-                        if ctx.masks[j] is not None:
+                        # (the fused forward's bits are in the NERF_FUSED_MASK layout, which only
+                        # the fused chain reads: this path takes the stored activation instead)
+                        if ctx.masks[j] is not None and not ctx.fused_forward:
                             epi |= NERF_EPI_MASK | NERF_EPI_MASKBITS
                             aux = ctx.masks[j]
                         else:

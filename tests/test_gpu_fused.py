@@ -105,19 +105,42 @@ def test_fused_forward_matches_layerwise(name, M, rd):
         if ma is None:
             continue
         n = plan.layers[li].N
-        bits_a = np.unpackbits(ma.cpu().numpy(), axis=1, bitorder="little")
-        bits_b = np.unpackbits(mb.cpu().numpy(), axis=1, bitorder="little")
-        # bit b of word 2e+h <-> column 4(32h+b)+e
-        cols = np.empty(256, dtype=np.int64)
-        for w in range(8):
-            e, h = w // 2, w % 2
-            for b in range(32):
-                cols[32 * w + b] = 4 * (32 * h + b) + e
+        # both layouts mapped to columns: NERF_EPI_MASKOUT (layer by layer) and NERF_FUSED_MASK
+        bits_a = np.unpackbits(ma.cpu().numpy(), axis=1, bitorder="little")[:, _maskout_order()]
+        bits_b = 1 - np.unpackbits(mb.cpu().numpy(), axis=1, bitorder="little")[:, _fused_mask_order()]   # dead bits
         act = a_ref[li][:, :n].cpu().numpy()
         near0 = np.abs(act) <= 1e-5 * max(1.0, np.abs(act).max())
-        valid = cols < n
-        diff = (bits_a != bits_b)[:, valid] & ~near0[:, cols[valid]]
+        diff = (bits_a[:, :n] != bits_b[:, :n]) & ~near0
         assert not diff.any(), (li, int(diff.sum()))
+        # and the bits are the activations' signs (away from zero)
+        sign = act > 0
+        assert not ((bits_b[:, :n] != sign) & ~near0).any()
+
+
+def _maskout_order():
+    """row bit index of column n in the NERF_EPI_MASKOUT layout: bit b of word 2e+h <-> column 4(32h+b)+e"""
+    order = np.empty(256, dtype=np.int64)
+    for w in range(8):
+        e, h = w // 2, w % 2
+        for b in range(32):
+            order[4 * (32 * h + b) + e] = 32 * w + b
+    return order
+
+
+def _fused_mask_order():
+    """row bit index of column n in the NERF_FUSED_MASK layout (include/nerf_amd.h): column
+    16 c + 4 g + r is bit 4 (7 - (c & 7)) + r of word 2 g + (c >> 3) (set: a dead unit)"""
+    order = np.empty(256, dtype=np.int64)
+    for c in range(16):
+        for g in range(4):
+            for r in range(4):
+                order[16 * c + 4 * g + r] = 32 * (2 * g + (c >> 3)) + 4 * (7 - (c & 7)) + r
+    return order
+
+
+def test_mask_layout_orders_are_permutations():
+    assert sorted(_maskout_order().tolist()) == list(range(256))
+    assert sorted(_fused_mask_order().tolist()) == list(range(256))
 
 
 def test_fused_forward_vs_oracle_subset():
@@ -213,6 +236,44 @@ def test_fused_input_gradient_chain_matches_layerwise(M, rd):
         finally:
             mlp_fused.ENABLED = saved
         assert (mlp_fused.FusedInputGrad.runs > runs) == fused
+        grads[fused] = {n: p.grad.detach().double() for n, p in model.named_parameters()}
+    ref = _fp64_param_grads(pos_pe, dir_pe, rd, w_out)
+    for n, r in ref.items():
+        scale = max(r.abs().max().item(), 1e-12)
+        e_layer = (grads[False][n] - r).abs().max().item() / scale
+        e_fused = (grads[True][n] - r).abs().max().item() / scale
+        assert e_fused <= e_layer + 1e-2 and e_fused < 5e-2, (n, e_fused, e_layer)
+
+
+def test_fused_forward_with_layerwise_backward(monkeypatch):
+    """A fused forward whose backward cannot run the chain (forced here) takes the layer-by-layer
+    input-gradient GEMMs: they must not read the fused NERF_FUSED_MASK bits as NERF_EPI_MASKOUT
+    words (mlp.py uses the stored activations instead).  Gradients against the all-layerwise
+    run and fp64 (bound as in the chain test above)."""
+    from nerf_amd import mlp_fused
+    from nerf_amd.mlp import MLPFunction
+    M, rd = 4096 * 4 + 7, 1
+    g = torch.Generator(device=DEV).manual_seed(17)
+    pos_pe = torch.zeros(M, 64, device=DEV)
+    pos_pe[:, :60] = torch.rand(M, 60, device=DEV, generator=g) * 2 - 1
+    dir_pe = torch.zeros(M, 32, device=DEV)
+    dir_pe[:, :24] = torch.rand(M, 24, device=DEV, generator=g) * 2 - 1
+    w_out = torch.randn(M, 4, device=DEV, generator=g)
+    monkeypatch.setattr(mlp_fused, "dgrad_eligible", lambda plan, M: False)
+    grads = {}
+    for fused in (False, True):
+        model = _model("n2v").to(DEV)
+        plan = model._get_plan()
+        saved = mlp_fused.ENABLED
+        mlp_fused.ENABLED = fused
+        runs = mlp_fused.FusedInputGrad.runs
+        try:
+            outs = MLPFunction.apply(plan, M, pos_pe, dir_pe, rd, *plan.params())
+            (outs[1][:, :4] * w_out).sum().backward()
+            torch.cuda.synchronize()
+        finally:
+            mlp_fused.ENABLED = saved
+        assert mlp_fused.FusedInputGrad.runs == runs
         grads[fused] = {n: p.grad.detach().double() for n, p in model.named_parameters()}
     ref = _fp64_param_grads(pos_pe, dir_pe, rd, w_out)
     for n, r in ref.items():
