@@ -971,10 +971,23 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     char* const img = smem + NRAW * WS_RAW;
 
     const int split = blockIdx.x;
+#ifndef NERF_WS_INTERLEAVE
     const int mbeg = split * a.m_per_split;
     int mend = mbeg + a.m_per_split;
     if (mend > a.M) mend = a.M;
     const int steps = mbeg < mend ? (mend - mbeg + WS_T - 1) / WS_T : 0;
+    // first row of step i, rows of the split past mend read any valid row (zeroed)
+#define WS_ROW0(i) (mbeg + (i) * WS_T)
+#define WS_VALID(i) (mend - WS_ROW0(i))
+#else
+    // tuning: 16-row steps dealt round-robin over the splits (split s: steps s, s + splits, ...)
+    const int mbeg = split * WS_T;
+    const int nst = (a.M + WS_T - 1) / WS_T;
+    const int steps = split < nst ? (nst - split + (int)gridDim.x - 1) / (int)gridDim.x : 0;
+    const int mend = a.M;
+#define WS_ROW0(i) ((split + (i) * (int)gridDim.x) * WS_T)
+#define WS_VALID(i) (a.M - WS_ROW0(i))
+#endif
 
     const int t = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
@@ -1012,8 +1025,8 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int r = 2 * wave + q;
-            int m = mbeg + step * WS_T + r;
-            m = m < mend ? m : mbeg;                       // past the split: any valid row (zeroed)
+            int m = WS_ROW0(step) + r;
+            m = m < mend && r < WS_VALID(step) ? m : mbeg;   // past the split: any valid row (zeroed)
             const bool b1 = m >= a.M0;                     // wave-uniform: the row's block
             const int mr = b1 ? m - a.M0 : m;
             const float* ys = (b1 ? a.dY1 : a.dY) + (int64_t)mr * (b1 ? a.lddy1 : a.lddy) + ycol;
@@ -1046,8 +1059,8 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     auto yd_load = [&](int step) __attribute__((always_inline)) {
 #pragma unroll
         for (int r = 0; r < WS_T; ++r) {
-            int m = mbeg + step * WS_T + r;
-            m = m < mend ? m : mbeg;
+            int m = WS_ROW0(step) + r;
+            m = m < mend && r < WS_VALID(step) ? m : mbeg;
             const bool b1 = m >= a.M0;
             yd[r] = *(const __attribute__((address_space(4))) float*)((b1 ? a.dY1 : a.dY) +
                                                                        (int64_t)(b1 ? m - a.M0 : m) * (b1 ? a.lddy1 : a.lddy) + 256);
@@ -1066,7 +1079,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     };
     auto conv_store = [&](int step, float (&v)[WS_T]) __attribute__((always_inline)) {
         __bf16* dst = reinterpret_cast<__bf16*>(img + (step % NIMG) * WS_IMG + op * 256 * 64);
-        const int valid = mend - (mbeg + step * WS_T);      // rows of this step inside the split
+        const int valid = WS_VALID(step);                   // rows of this step inside the split
         // masking only where a row or the column is invalid (the split's last step, padded
         // columns: a branch around it that full steps skip)
         if (!(c_ok && valid >= WS_T)) {
@@ -1097,9 +1110,11 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         }
     };
     auto convert = [&](int step) __attribute__((always_inline)) {
+#ifndef NERF_WS_DIAG_NOCONV       // diagnostic builds only: no conversion (the images keep stale bytes)
         float v[WS_T];
         conv_load(step, v);
         conv_store(step, v);
+#endif
     };
     auto barrier = []() __attribute__((always_inline)) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1164,12 +1179,18 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             // NIMG = 2: step i + 1's conversion overlaps step i's MFMAs (other image stage)
             if (NIMG == 2) {
                 if (active) {
+#ifndef NERF_WS_DIAG_NOCONV
                     float v[WS_T];
                     conv_load(i + 1, v);
+#endif
                     __builtin_amdgcn_sched_barrier(0);      // the ring reads fly while the MFMAs run
+#ifndef NERF_WS_DIAG_NOMFMA       // diagnostic builds only: no MFMA step
                     mfma_step(i);
+#endif
                     __builtin_amdgcn_sched_barrier(0);
+#ifndef NERF_WS_DIAG_NOCONV
                     conv_store(i + 1, v);
+#endif
                 } else {
                     convert(i + 1);
                 }
@@ -1184,6 +1205,8 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         }
     }
 
+#undef WS_ROW0
+#undef WS_VALID
     float* slab = a.slab + (size_t)split * npad * kpad;
 #pragma unroll
     for (int i = 0; i < 4; ++i)

@@ -905,6 +905,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
     c.n_layers = a.n_layers;
     c.dsink = 0.f;
     if ((int)blockIdx.x >= a.ntiles) return;
+#ifdef NERF_FUSED_PRIO_HALF      // tuning: static issue priority for the second-dispatched half of the waves
+    if (c.wave >= NWAVE / 2) __builtin_amdgcn_s_setprio(1);
+#endif
     const int my_tiles = (a.ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
     int per_tile = 0;
     for (int l = 0; l < a.n_layers; ++l)
