@@ -502,6 +502,19 @@ def _roofline(ks_fn: dict, x3: bool, steps: int, workload: str):
             "pmc": pmc}
 
 
+def _hbm_roofline(ks, hbm_bytes, hbm_ms, hbm_gbs, steps):
+    """roofline_hbm of a step that launches the encoding / compositing kernels (NERF_FUSE_ENC=0,
+    NERF_FUSE_COMPOSITE=0, or rays that do not fill the fused kernel's tiles)."""
+    names = [k for k in ("encode_fwd", "composite_fwd", "composite_bwd") if k in ks]
+    return {"kernel": " + ".join(names) + " (algorithmic bytes per launch)",
+            "encode_launches_per_step": ks.get("encode_fwd", {}).get("launches", 0) / steps,
+            "composite_launches_per_step": (ks.get("composite_fwd", {}).get("launches", 0)
+                                            + ks.get("composite_bwd", {}).get("launches", 0)) / steps,
+            "bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": hbm_gbs / HBM_PEAK_GBS, "us_per_step": hbm_ms * 1e3 / steps,
+            "bytes_per_step": hbm_bytes / steps}
+
+
 def frame_roofline(ren, wl: dict, device, H: int = 800, W: int = 800, reps: int = 3):
     """HBM roofline of the same positional-encoding and compositing kernels at ONE full-frame
     launch: H*W rays (800 x 800: the C3 view size) x the workload's coarse and fine sample counts,
@@ -705,16 +718,15 @@ def main():
                        "coarse_samples": wl["coarse"], "fine_samples": wl["fine"], "global_rays": wl["rays"] * world,
                        "parallelism": f"ray-batch dp{world}" + (" (RCCL bucketed all-reduce from post-accumulate-grad hooks)" if world > 1 else "")},
             "roofline": roofline,
-            "roofline_hbm": {"kernel": ("encode_fwd + composite_fwd + composite_bwd (positional encoding and "
-                                        "alpha compositing; algorithmic bytes per launch)" if "encode_fwd" in ks else
-                                        "composite_fwd + composite_bwd (alpha compositing; algorithmic bytes per "
-                                        "launch); the positional encodings have no launch of their own: they are "
-                                        "generated inside mlp_fused_kernel<0>, whose bytes include their rows"),
-                             "encode_launches_per_step": ks.get("encode_fwd", {}).get("launches", 0) / args.steps,
-                             "bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": hbm_gbs / HBM_PEAK_GBS,
-                             "us_per_step": hbm_ms * 1e3 / args.steps,
-                             "bytes_per_step": hbm_bytes / args.steps},
+            "roofline_hbm": (_hbm_roofline(ks, hbm_bytes, hbm_ms, hbm_gbs, args.steps) if hbm_ms > 0 else
+                             {"kernel": "none: the positional encodings and the alpha compositing have no launch "
+                                        "of their own in this step; they run inside mlp_fused_kernel<0> (encoding "
+                                        "rows generated per tile, rays composited at the tile end) and "
+                                        "mlp_fused_kernel<1> (the compositing's gradient from per-sample "
+                                        "coefficients), whose algorithmic bytes include theirs (DESIGN.md §3)",
+                              "encode_launches_per_step": 0.0, "composite_launches_per_step": 0.0,
+                              "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": None, "us_per_step": 0.0, "bytes_per_step": 0.0}),
             "kernels": {k: {"launches_per_step": v["launches"] / args.steps, "ms_per_step": v["ms"] / args.steps,
                             "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["ms"] > 0 else 0.0,
                             "gbs": (v["bytes"] / (v["ms"] * 1e-3) / 1e9) if v["ms"] > 0 else 0.0}

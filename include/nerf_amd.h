@@ -45,12 +45,13 @@ extern "C" {
 #define NERF_ERR_LAUNCH (-3)
 #define NERF_ERR_WORKSPACE (-4)
 
-/* Library / ABI version (bumped on any signature or data-layout change; 6: NERF_FUSED_MASK). */
+/* Library / ABI version (bumped on any signature or data-layout change; 6: NERF_FUSED_MASK;
+ * 7: nerf_fused_composite / nerf_mlp_fused_render). */
 int nerf_abi_version(void);
 const char* nerf_status_string(int status);
 /* sizeof of the argument structs, for bindings to check their layouts against:
  * 0 nerf_pe_params, 1 nerf_fused_layer, 2 nerf_fused_encoding, 3 nerf_hashgrid_params,
- * 4 nerf_adam_batch, 5 nerf_seg; -1 for an unknown index. */
+ * 4 nerf_adam_batch, 5 nerf_seg, 6 nerf_fused_composite; -1 for an unknown index. */
 int64_t nerf_struct_size(int32_t which);
 
 /* ---------------------------------------------------------------------------
@@ -355,7 +356,9 @@ typedef struct nerf_fused_layer {
     int32_t n1;            /* chunks written to out (= nb when out2 is unused) */
     int32_t hbm_off;       /* byte offset of the layer's HBM-fed weight fragments in the image */
     int32_t seg_gen[2];    /* 0: segment s is read from seg_ptr; 1 + e (first layer, one segment):
-                              the rows of encodings[e] generated at the tile start, read from LDS */
+                              the rows of encodings[e] generated at the tile start, read from LDS;
+                              3 / 4 (input-gradient chain): the composite's head / density gradient
+                              from its coefficient rows (nerf_mlp_fused_render) */
 } nerf_fused_layer;
 
 /* An encoding generated inside the fused forward: every entry with out_dim > 0 is computed at the
@@ -381,6 +384,52 @@ typedef struct nerf_fused_encoding {
 /* encodings: NULL, or 2 entries (generated segments index them) */
 int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_layers, const void* image, int64_t M,
                        const nerf_fused_encoding* encodings, void* stream);
+
+/* Alpha compositing fused into the field MLP (a4 inside a7: barf/model_interpolation.py:316-353 on
+ * the heads of model_interpolation_architecture.py:128-141, replacing nerf_composite_fwd/bwd with
+ * act = 1 for rays whose samples fill whole 128-sample tiles: 128 % S == 0, 16 <= S <= 128, with
+ * 128 / S rays per tile and M = n_rays * S).
+ *
+ * Forward (the forward launch): at the end of every tile the waves hand their samples' raw heads
+ * (rgb = rows 0..2 of layer head_layer, which has one 16-row chunk; sigma = the column output of
+ * sigma_layer, or row 3 of the head layer when sigma_layer < 0) to one wave per ray through LDS,
+ * which composites the ray exactly as nerf_composite_fwd (the same instructions: rgb and weights
+ * bitwise equal) and writes rgb[ray][3], weights[n] (or not, NULL) and the backward's per-sample
+ * coefficients coef[n][8] (or not, NULL):
+ *   coef[n][0..2] = dL/d rgb-raw_n,ch per unit grad_rgb_ch = w_n * c_n,ch * (1 - c_n,ch)
+ *   coef[n][4..6] = dL/d sigma-raw_n per unit grad_rgb_ch
+ *                 = -(((A_n,ch * sb) * sa) * delta_n) * softplus'(raw - shift),
+ *     A_n,ch = (-c_n,ch T_n e^{b_n}) + sum_{i > n} c_i,ch w_i   (fp64 suffix sums), [3], [7] = 0,
+ * so that the backward of the compositing is linear in grad_rgb per sample: no scan.
+ * Input-gradient chain (the chain launch, grad_rgb != NULL): a step whose HBM segment has seg_gen 3
+ * takes, per sample, [g_0 coef0, g_1 coef1, g_2 coef2, sigma_layer < 0 ? <g, coef4..6> : 0]
+ * (g = grad_rgb of the sample's ray; seg_ptr = coef, seg_ld = seg_k = 8) as its input rows and
+ * stores them to grad_head[n * ld_head + 0..3] (the head layer's dY for its weight gradient); seg_gen
+ * 4 takes [<g, coef4..6>, 0, 0, 0] (the density column) and stores it to grad_sigma[n * ld_sigma +
+ * 0..3] (the density layer's dY columns 256..259).  The weights output is non-differentiable
+ * (the renderer only resamples from it). */
+typedef struct nerf_fused_composite {
+    const float* dist;         /* forward: [M] interval lengths t_end - t_start */
+    float* rgb;                /* forward: [n_rays][3] */
+    float* weights;            /* forward: [M] or NULL */
+    float* coef;               /* forward: [M][8] backward coefficients or NULL */
+    const float* grad_rgb;     /* chain: [n_rays][3] */
+    float* grad_head;          /* chain: seg_gen 3 rows, or NULL */
+    int64_t ld_head;
+    float* grad_sigma;         /* chain: seg_gen 4 rows (16-B aligned), or NULL */
+    int64_t ld_sigma;
+    int32_t samples_per_ray;
+    int32_t head_layer;        /* forward: the layer whose rows 0..2 (3) are the raw rgb (sigma) */
+    int32_t sigma_layer;       /* the layer whose column output is the raw density, or -1 (head row 3) */
+    float scale_a, scale_b;    /* density factor (reference: 3 * MAGIC_NUMBER) */
+    float density_shift;       /* sigma = softplus(raw - shift, threshold 8), c = sigmoid(raw) */
+    int32_t reserved;
+} nerf_fused_composite;
+
+/* nerf_mlp_fused_fwd with compositing fused in (composite: NULL = nerf_mlp_fused_fwd). */
+int nerf_mlp_fused_render(const nerf_fused_layer* layers, int32_t n_layers, const void* image, int64_t M,
+                          const nerf_fused_encoding* encodings, const nerf_fused_composite* composite,
+                          void* stream);
 
 /* Gather + split packer for the fused image: for i < n, v = srcs[map_src[i] >> 24][map_src[i] & 0xffffff]
  * (0 if map_src[i] < 0); map_dst[i] >= 0: bf16 element index of hi = bf16(v) (lo = bf16(v - hi)

@@ -1,7 +1,7 @@
 // Library-level C-ABI helpers (version, status strings).
 #include "common.h"
 
-extern "C" int nerf_abi_version(void) { return 6; }
+extern "C" int nerf_abi_version(void) { return 7; }
 
 extern "C" int64_t nerf_struct_size(int32_t which) {
     switch (which) {
@@ -11,6 +11,7 @@ extern "C" int64_t nerf_struct_size(int32_t which) {
         case 3: return (int64_t)sizeof(nerf_hashgrid_params);
         case 4: return (int64_t)sizeof(nerf_adam_batch);
         case 5: return (int64_t)sizeof(nerf_seg);
+        case 6: return (int64_t)sizeof(nerf_fused_composite);
         default: return -1;
     }
 }

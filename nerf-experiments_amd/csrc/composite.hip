@@ -16,6 +16,7 @@
 // computes).  No LDS, no atomics; HBM traffic = the algorithmic bytes (sigma,
 // rgb, delta in; w, rgb out).
 #include "common.h"
+#include "composite_common.h"
 
 using namespace nerf;
 
@@ -69,45 +70,18 @@ template <int R>
 __device__ __forceinline__ void composite_fwd_ray(const CompositeArgs& a, int64_t ray, int lane, const float (&rd)[R],
                                                   const float (&del)[R], const float (&rc)[R][3],
                                                   float* __restrict__ rgb_out, float* __restrict__ w_out) {
-#pragma clang fp contract(off)
     const int64_t base = ray * a.S;
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
-    double carry = 0.0;            // sum of b over the previous 64-sample segments
+    float w[R], rgb[3], cc[R][3], cs[R][3];
+    composite_ray<R, false>(a.S, a.sa, a.sb, a.act, a.shift, lane, rd, del, rc, w, rgb, cc, cs);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int s = r * NERF_WAVE + lane;
-        float sig = rd[r];
-        float c0 = rc[r][0], c1 = rc[r][1], c2 = rc[r][2];
-        if (a.act && s < a.S) {
-            sig = softplus_thr8(sig - a.shift);
-            c0 = sigmoidf_(c0);
-            c1 = sigmoidf_(c1);
-            c2 = sigmoidf_(c2);
-        }
-        // ((-sigma * delta) * 3) * MAGIC — two fp32 multiplies, as the reference.
-        float bb = ((-sig) * del[r]) * a.sa;
-        bb = bb * a.sb;
-        if (s >= a.S) bb = 0.f;
-        const double incl = wave_inclusive_scan((double)bb);
-        const double ex = carry + (incl - (double)bb);      // exclusive prefix
-        carry += __shfl(incl, NERF_WAVE - 1, NERF_WAVE);
-        const float T = (s == 0) ? 1.0f : expf((float)ex);
-        const float alpha = 1.0f - expf(bb);
-        const float w = T * alpha;
-        if (s < a.S) {
-            if (w_out) w_out[base + s] = w;
-            acc0 += w * c0;
-            acc1 += w * c1;
-            acc2 += w * c2;
-        }
+        if (s < a.S && w_out) w_out[base + s] = w[r];
     }
-    acc0 = wave_sum_f(acc0);
-    acc1 = wave_sum_f(acc1);
-    acc2 = wave_sum_f(acc2);
     if (lane == 0) {
-        rgb_out[ray * 3 + 0] = acc0;
-        rgb_out[ray * 3 + 1] = acc1;
-        rgb_out[ray * 3 + 2] = acc2;
+        rgb_out[ray * 3 + 0] = rgb[0];
+        rgb_out[ray * 3 + 1] = rgb[1];
+        rgb_out[ray * 3 + 2] = rgb[2];
     }
 }
 

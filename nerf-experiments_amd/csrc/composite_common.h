@@ -1,0 +1,85 @@
+// Per-ray compositing arithmetic shared by the stand-alone kernels (composite.hip) and the
+// compositing fused into the field MLP's forward (mlp_fused.hip): the same instructions, so both
+// produce bitwise the same rgb and weights.
+//
+// Reference: NerfInterpolation._render_rays, barf/model_interpolation.py:316-353
+//   b_s = ((-sigma_s * delta_s) * scale_a) * scale_b,  T_s = exp(sum_{j<s} b_j) (fp64 prefix),
+//   w_s = T_s * (1 - exp(b_s)),  rgb = sum_s w_s c_s.
+// One wavefront per ray; lane l owns the R samples s = 64 r + l.
+#pragma once
+#include "common.h"
+
+namespace nerf {
+
+// rd / del / rc: raw density, interval length, raw (act) or activated colour of the lane's samples
+// (anything past S is ignored).  Outputs: w[r] (valid for s < S), rgb (every lane: the wave sum).
+// COEF: also the per-sample backward coefficients of the act = 1 form (include/nerf_amd.h,
+// nerf_fused_composite): cc[r][ch] = w c (1 - c), cs[r][ch] = d sigma-raw / d grad_rgb_ch.
+template <int R, bool COEF>
+__device__ __forceinline__ void composite_ray(int S, float sa, float sb, int act, float shift, int lane,
+                                              const float (&rd)[R], const float (&del)[R], const float (&rc)[R][3],
+                                              float (&w)[R], float (&rgb)[3], float (&cc)[R][3],
+                                              float (&cs)[R][3]) {
+#pragma clang fp contract(off)
+    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
+    double carry = 0.0;            // sum of b over the previous 64-sample segments
+    float c[R][3], T[R], e[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int s = r * NERF_WAVE + lane;
+        float sig = rd[r];
+        c[r][0] = rc[r][0]; c[r][1] = rc[r][1]; c[r][2] = rc[r][2];
+        if (act && s < S) {
+            sig = softplus_thr8(sig - shift);
+            c[r][0] = sigmoidf_(c[r][0]);
+            c[r][1] = sigmoidf_(c[r][1]);
+            c[r][2] = sigmoidf_(c[r][2]);
+        }
+        // ((-sigma * delta) * 3) * MAGIC — two fp32 multiplies, as the reference.
+        float bb = ((-sig) * del[r]) * sa;
+        bb = bb * sb;
+        if (s >= S) bb = 0.f;
+        const double incl = wave_inclusive_scan((double)bb);
+        const double ex = carry + (incl - (double)bb);      // exclusive prefix
+        carry += __shfl(incl, NERF_WAVE - 1, NERF_WAVE);
+        T[r] = (s == 0) ? 1.0f : expf((float)ex);
+        e[r] = expf(bb);
+        w[r] = T[r] * (1.0f - e[r]);
+        if (s < S) {
+            acc0 += w[r] * c[r][0];
+            acc1 += w[r] * c[r][1];
+            acc2 += w[r] * c[r][2];
+        }
+    }
+    rgb[0] = wave_sum_f(acc0);
+    rgb[1] = wave_sum_f(acc1);
+    rgb[2] = wave_sum_f(acc2);
+    if constexpr (COEF) {
+        // dL/db_n = sum_ch g_ch A_n,ch with A_n,ch = -c_n,ch T_n e^{b_n} + sum_{i>n} c_i,ch w_i
+        // (nerf_composite_bwd with gw = <g, c> split per channel), suffix sums in fp64
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            double qincl[R];
+            double qcarry = 0.0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int s = r * NERF_WAVE + lane;
+                const double q = s < S ? (double)c[r][ch] * (double)w[r] : 0.0;
+                const double qi = wave_inclusive_scan(q);
+                qincl[r] = qcarry + qi;
+                qcarry += __shfl(qi, NERF_WAVE - 1, NERF_WAVE);
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int s = r * NERF_WAVE + lane;
+                const float a = (float)((double)((-c[r][ch] * T[r]) * e[r]) + (qcarry - qincl[r]));
+                float d = -(((a * sb) * sa) * del[r]);
+                if (act && s < S) d = d * softplus_thr8_grad(rd[r] - shift);
+                cs[r][ch] = d;
+                cc[r][ch] = act ? (w[r] * (1.0f - c[r][ch])) * c[r][ch] : w[r];
+            }
+        }
+    }
+}
+
+}  // namespace nerf

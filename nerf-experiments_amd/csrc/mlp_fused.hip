@@ -36,6 +36,7 @@
 
 #include "common.h"
 #include "encode_common.h"
+#include "composite_common.h"
 
 using namespace nerf;
 
@@ -102,6 +103,8 @@ struct FusedArgs {
     int n_layers;
     int M;
     int ntiles;
+    int comp_on;       // forward: composite every tile's rays (nerf_mlp_fused_render)
+    nerf_fused_composite comp;
 };
 
 typedef __attribute__((address_space(4))) const char kchar_t;
@@ -125,6 +128,11 @@ typedef const uint8_t* cu8ptr_t;
     (*(const __attribute__((address_space(4))) T*)(c.kargs + offsetof(FusedArgs, enc) +                      \
                                                    (size_t)(e) * sizeof(nerf_fused_encoding) +               \
                                                    offsetof(nerf_fused_encoding, f)))
+
+// fields of the fused composite, from the kernel-argument segment
+#define CF(T, f)                                                                                             \
+    (*(const __attribute__((address_space(4))) T*)(c.kargs + offsetof(FusedArgs, comp) +                    \
+                                                   offsetof(nerf_fused_composite, f)))
 
 __device__ __forceinline__ f4 mfma16(bf16x8 a, bf16x8 b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -209,6 +217,10 @@ struct Ctx {
     // the current layer's register-fed input (B operand): [32-deep k-block][16-sample column block]
     bf16x8 xh[KBMAX][SB], xl[KBMAX][SB];
     float dsink;          // diagnostic builds only
+    // fused compositing (forward): the last layer's values (rows 4 g .. 4 g + 3), the density column
+    // output and the interval length of the lane's samples (lanes g = 0)
+    f4 head[SB];
+    float sig[SB], cdist[SB];
 };
 
 __device__ __forceinline__ int dma_units(Ctx& c, int l) { return LF(int, chunk_units, l); }
@@ -392,6 +404,39 @@ __device__ __forceinline__ void gen_block(const Ctx& c, int r, int col, bf16x8& 
     split8(__builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7), h, lo);
 }
 
+// Input rows of a chain step fed by the fused composite (seg_gen 3: head gradient, 4: density
+// gradient; include/nerf_amd.h nerf_fused_composite): per sample the coefficient row (coef [M][8])
+// times its ray's grad_rgb, stored for the weight gradients and split into the B operand of the
+// step's k-block (lanes g = 0 hold columns 0..7, the others zeros).
+__device__ __forceinline__ void comp_grad_block(const Ctx& c, int gen, const float* coef, const int (&sample)[SB],
+                                                const bool (&row_ok)[SB], bf16x8 (&h)[SB], bf16x8 (&lo)[SB]) {
+#pragma clang fp contract(off)
+    const unsigned S = (unsigned)CF(int32_t, samples_per_ray);
+    const float* grgb = CF(cfptr_t, grad_rgb);
+    const bool dens_head = CF(int32_t, sigma_layer) < 0;
+    float* out = gen == 3 ? CF(fptr_t, grad_head) : CF(fptr_t, grad_sigma);
+    const int64_t ldo = gen == 3 ? CF(int64_t, ld_head) : CF(int64_t, ld_sigma);
+#pragma unroll
+    for (int sb = 0; sb < SB; ++sb) {
+        f4 x0 = {0.f, 0.f, 0.f, 0.f};
+        if ((c.lane >> 4) == 0 && row_ok[sb]) {
+            const unsigned m = (unsigned)sample[sb];
+            const unsigned ray = m / S;
+            const f4 q0 = *reinterpret_cast<const f4*>(coef + (size_t)m * 8);
+            const f4 q1 = *reinterpret_cast<const f4*>(coef + (size_t)m * 8 + 4);
+            const float g0 = grgb[ray * 3 + 0], g1 = grgb[ray * 3 + 1], g2 = grgb[ray * 3 + 2];
+            const float ds = (g0 * q1[0] + g1 * q1[1]) + g2 * q1[2];
+            if (gen == 3)
+                x0 = f4{g0 * q0[0], g1 * q0[1], g2 * q0[2], dens_head ? ds : 0.f};
+            else
+                x0 = f4{ds, 0.f, 0.f, 0.f};
+            // nontemporal, as the layer outputs: the first chunk's vmcnt(0) waits for its acknowledgement
+            if (out != nullptr) __builtin_nontemporal_store(x0, reinterpret_cast<f4*>(out + (size_t)m * ldo));
+        }
+        split8(__builtin_shufflevector(x0, f4{0.f, 0.f, 0.f, 0.f}, 0, 1, 2, 3, 4, 5, 6, 7), h[sb], lo[sb]);
+    }
+}
+
 struct LayerState {
     int floor_i;          // ReLU as an integer max on the fp32 bits: 0, or INT_MIN for no ReLU
     int col_chunk;        // 16-row chunk holding the column output (-1: none)
@@ -487,6 +532,7 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 v[r] = __builtin_bit_cast(float, max(__builtin_bit_cast(int, v[r] + b[r]), st.floor_i));
+            if (ch >= 0 && ch == st.col_chunk) c.sig[sb] = v[0];   // (the raw density, for fused compositing)
 #if NERF_FUSED_PAIR >= 2
             if (!pair_odd(ch)) {
                 // even chunk: held for the pair (alone if it is the layer's last); the column output
@@ -771,8 +817,13 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
         for (int kh = 0; kh < KBH; ++kh) {
             const int sg = kh < kb0 ? 0 : 1;            // segment of this block
             const int khl = sg ? kh - kb0 : kh;
-            const int gen = MODE != MODE_FWD ? 0 : sg ? LFI(int, seg_gen, 1, l) : LFI(int, seg_gen, 0, l);
-            if (gen != 0) {                             // generated at the tile start, still in LDS
+            const int gen = sg ? LFI(int, seg_gen, 1, l) : LFI(int, seg_gen, 0, l);
+            if (MODE == MODE_DGRAD && gen >= 3) {       // the fused composite's head / density gradient
+                comp_grad_block(c, gen, sg ? LFI(cfptr_t, seg_ptr, 1, l) : LFI(cfptr_t, seg_ptr, 0, l), sample,
+                                row_ok, hh[kh], hl[kh]);
+                continue;
+            }
+            if (MODE == MODE_FWD && gen != 0) {         // generated at the tile start, still in LDS
 #pragma unroll
                 for (int sb = 0; sb < SB; ++sb) gen_block(c, 16 * sb + (c.lane & 15), 32 * khl + 8 * g, hh[kh][sb], hl[kh][sb]);
                 continue;
@@ -881,6 +932,11 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
         for (int sb = 0; sb < SB; ++sb)
             __builtin_amdgcn_raw_buffer_store_b64(u2{st.mw[sb][0], st.mw[sb][1]}, st.rm, st.mrow_off[sb], 0, 0);
     }
+    if constexpr (MODE == MODE_FWD) {
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb) c.head[sb] = pv[sb];
+    }
+    if (l + 1 == c.n_layers) return;     // (no next layer: the image region may hold the tile's heads)
     // the next layer's operand: the wave's LDS image back into registers (same wave: LDS ops in order)
 #pragma unroll
     for (int kb = 0; kb < KBMAX; ++kb)
@@ -889,6 +945,88 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
             c.xh[kb][sb] = *reinterpret_cast<const bf16x8*>(c.ximg + ((kb * SB + sb) * 2) * 1024 + c.lane * 16);
             c.xl[kb][sb] = *reinterpret_cast<const bf16x8*>(c.ximg + ((kb * SB + sb) * 2 + 1) * 1024 + c.lane * 16);
         }
+}
+
+// ---- compositing fused into the forward (nerf_mlp_fused_render): at the end of a tile the waves
+// hand their samples' raw heads and interval lengths to the wave compositing each ray, through that
+// wave's operand-image region at COMP_OFF.  The last layer (one 16-row chunk) writes only the first
+// 2 SB KB of its image and its image is not read back; every wave passed that layer's chunk barrier
+// after reading back its previous image, and a region is next written by its own wave (the next
+// tile's generated rows, then its first layer) after it has composited: one barrier suffices.
+constexpr int COMP_OFF = 8192;
+static_assert(COMP_OFF >= SB * 2048 && COMP_OFF + TILE * 20 <= XIMG_BYTES, "composite scratch");
+
+template <int R>
+__device__ __forceinline__ void composite_wave(Ctx& c, int64_t ray, int S) {
+    const char* reg = c.ximg + COMP_OFF;
+    float rd[R], del[R], rc[R][3];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int s = r * 64 + c.lane;
+        rd[r] = 0.f; del[r] = 0.f;
+        rc[r][0] = rc[r][1] = rc[r][2] = 0.f;
+        if (s < S) {
+            const f4 h = *reinterpret_cast<const f4*>(reg + s * 16);
+            rc[r][0] = h[0]; rc[r][1] = h[1]; rc[r][2] = h[2]; rd[r] = h[3];
+            del[r] = *reinterpret_cast<const float*>(reg + TILE * 16 + s * 4);
+        }
+    }
+    float w[R], rgb[3], cc[R][3], cs[R][3];
+    composite_ray<R, true>(S, CF(float, scale_a), CF(float, scale_b), 1, CF(float, density_shift), c.lane, rd, del,
+                           rc, w, rgb, cc, cs);
+    const int64_t base = ray * S;
+    float* wo = CF(fptr_t, weights);
+    float* co = CF(fptr_t, coef);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int s = r * 64 + c.lane;
+        if (s < S) {
+            // nontemporal (the next tile's first chunk waits for every store's acknowledgement)
+            if (wo != nullptr) __builtin_nontemporal_store(w[r], wo + base + s);
+            if (co != nullptr) {
+                f4* q = reinterpret_cast<f4*>(co + (base + s) * 8);
+                __builtin_nontemporal_store(f4{cc[r][0], cc[r][1], cc[r][2], 0.f}, q);
+                __builtin_nontemporal_store(f4{cs[r][0], cs[r][1], cs[r][2], 0.f}, q + 1);
+            }
+        }
+    }
+    if (c.lane == 0) {
+        float* o = CF(fptr_t, rgb) + ray * 3;
+        __builtin_nontemporal_store(rgb[0], o);
+        __builtin_nontemporal_store(rgb[1], o + 1);
+        __builtin_nontemporal_store(rgb[2], o + 2);
+    }
+}
+
+__device__ __forceinline__ void composite_tile(Ctx& c, int tile) {
+    const int S = CF(int32_t, samples_per_ray);
+    const bool col_sigma = CF(int32_t, sigma_layer) >= 0;
+    if (c.lane < 16) {
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb) {
+            const int j = c.wave * SPW + 16 * sb + c.lane;       // sample of the tile
+            if (tile * TILE + j < c.M) {
+                const int r = j / S, o = j - r * S;
+                char* reg = c.smem + NSLOT * SLOT_BYTES + r * XIMG_BYTES + COMP_OFF;
+                f4 h = c.head[sb];
+                if (col_sigma) h[3] = c.sig[sb];
+                *reinterpret_cast<f4*>(reg + o * 16) = h;
+                *reinterpret_cast<float*>(reg + TILE * 16 + o * 4) = c.cdist[sb];
+            }
+        }
+    }
+    barrier();
+    // (s_barrier is no memory operation to the compiler: without this clobber the scratch reads
+    // below may be hoisted above it, before the other waves' writes have landed)
+    asm volatile("" ::: "memory");
+    const int rpt = TILE / S;
+    const int64_t ray = (int64_t)tile * rpt + c.wave;
+    if (c.wave < rpt && ray * S < c.M) {
+        if (S > 64)
+            composite_wave<2>(c, ray, S);
+        else
+            composite_wave<1>(c, ray, S);
+    }
 }
 
 template <int MODE>
@@ -935,6 +1073,15 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
         }
     for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
         const int base = tile * TILE + c.wave * SPW;
+        if (MODE == MODE_FWD && a.comp_on) {
+            // the samples' interval lengths for the tile-end compositing (long landed by then)
+            const float* dist = CF(cfptr_t, dist);
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) {
+                const int m = base + 16 * sb + (c.lane & 15);
+                c.cdist[sb] = c.lane < 16 && m < c.M ? dist[m] : 0.f;
+            }
+        }
         if (MODE == MODE_FWD && a.gen_mask != 0) {
             // the tile's in-kernel encodings (one code copy for every layer type): the inputs of both
             // loaded together, then each into the wave's LDS scratch and out to its HBM rows; the one
@@ -965,6 +1112,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
                 default: break;                          // rejected on the host
             }
         }
+        if (MODE == MODE_FWD && a.comp_on) composite_tile(c, tile);
     }
 #ifdef NERF_FUSED_DIAG_MFMAONLY
     if (c.dsink == 1234.5f) LF(fptr_t, out, 0)[threadIdx.x] = c.dsink;   // keeps the MFMAs live
@@ -973,6 +1121,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
 #undef LF
 #undef LFI
 #undef EF
+#undef CF
 
 struct PackArgs {
     const float* src[NERF_FUSED_MAX_SRCS];
@@ -1042,8 +1191,9 @@ bool encoding_ok(const nerf_fused_encoding& e, int64_t M) {
 }
 }  // namespace
 
-extern "C" int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_layers, const void* image, int64_t M,
-                                  const nerf_fused_encoding* encodings, void* stream) {
+namespace {
+int fused_launch(const nerf_fused_layer* layers, int32_t n_layers, const void* image, int64_t M,
+                 const nerf_fused_encoding* encodings, const nerf_fused_composite* comp, void* stream) {
     NERF_REQUIRE(layers != nullptr && image != nullptr);
     NERF_REQUIRE(n_layers >= 1 && n_layers <= NERF_FUSED_MAX_LAYERS);
     NERF_REQUIRE(M >= 1 && M <= (int64_t)1 << 30);
@@ -1090,6 +1240,19 @@ extern "C" int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_laye
             const int gen = s < L.nseg ? L.seg_gen[s] : 0;
             NERF_REQUIRE(s < L.nseg || L.seg_gen[s] == 0);
             if (gen == 0) continue;
+            if (gen >= 3) {
+                // the fused composite's gradient rows (input-gradient chain): one coefficient block
+                NERF_REQUIRE(dgrad && gen <= 4 && comp != nullptr && comp->grad_rgb != nullptr && L.nseg == 1);
+                NERF_REQUIRE(L.seg_kb[0] == 1 && L.seg_k[0] == 8 && L.seg_ld[0] == 8 && L.seg_rd[0] == 1);
+                NERF_REQUIRE(L.seg_ptr[0] != nullptr && aligned16(L.seg_ptr[0]) && L.seg_rows[0] >= M);
+                NERF_REQUIRE((int64_t)L.seg_rows[0] * 32 < ((int64_t)1 << 31));
+                float* o = gen == 3 ? comp->grad_head : comp->grad_sigma;
+                const int64_t ld = gen == 3 ? comp->ld_head : comp->ld_sigma;
+                NERF_REQUIRE(o == nullptr || (aligned16(o) && ld % 4 == 0 && ld >= 4));
+                const int S = comp->samples_per_ray;
+                NERF_REQUIRE(S >= 1 && M % S == 0);
+                continue;
+            }
             // read from the rows generated at the tile start: the first layer only, one segment
             NERF_REQUIRE(!dgrad && l == 0 && encodings != nullptr && (gen == 1 || gen == 2) && gen_lds < 0);
             const nerf_fused_encoding& e = encodings[gen - 1];
@@ -1139,6 +1302,25 @@ extern "C" int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_laye
     a.n_layers = n_layers;
     a.M = (int)M;
     a.ntiles = (int)((M + TILE - 1) / TILE);
+    // compositing fused into the forward (include/nerf_amd.h nerf_fused_composite)
+    a.comp_on = 0;
+    memset(&a.comp, 0, sizeof(a.comp));
+    if (comp != nullptr) {
+        a.comp = *comp;
+        const int S = comp->samples_per_ray;
+        if (!dgrad) {
+            NERF_REQUIRE(S >= 16 && S <= 128 && TILE % S == 0 && TILE / S <= NWAVE && M % S == 0);
+            NERF_REQUIRE(comp->dist != nullptr && comp->rgb != nullptr);
+            NERF_REQUIRE(comp->coef == nullptr || (aligned16(comp->coef) && M * 32 < ((int64_t)1 << 31)));
+            // the heads: the last layer, one 16-row chunk with a barrier (a register-fed part)
+            const nerf_fused_layer& H = layers[n_layers - 1];
+            NERF_REQUIRE(comp->head_layer == n_layers - 1 && H.type >= 3 && H.N <= 16);
+            NERF_REQUIRE(H.N >= (comp->sigma_layer < 0 ? 4 : 3));
+            NERF_REQUIRE(comp->sigma_layer < n_layers - 1);
+            if (comp->sigma_layer >= 0) NERF_REQUIRE(layers[comp->sigma_layer].col_out != nullptr);
+            a.comp_on = 1;
+        }
+    }
     const int grid = a.ntiles < num_cus() ? a.ntiles : num_cus();
     if (dgrad)
         hipLaunchKernelGGL(mlp_fused_kernel<MODE_DGRAD>, dim3(grid), dim3(WG), 0, as_stream(stream), a);
@@ -1146,6 +1328,18 @@ extern "C" int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_laye
         hipLaunchKernelGGL(mlp_fused_kernel<MODE_FWD>, dim3(grid), dim3(WG), 0, as_stream(stream), a);
     NERF_CHECK_LAUNCH();
     return NERF_OK;
+}
+}  // namespace
+
+extern "C" int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_layers, const void* image, int64_t M,
+                                  const nerf_fused_encoding* encodings, void* stream) {
+    return fused_launch(layers, n_layers, image, M, encodings, nullptr, stream);
+}
+
+extern "C" int nerf_mlp_fused_render(const nerf_fused_layer* layers, int32_t n_layers, const void* image, int64_t M,
+                                     const nerf_fused_encoding* encodings, const nerf_fused_composite* composite,
+                                     void* stream) {
+    return fused_launch(layers, n_layers, image, M, encodings, composite, stream);
 }
 
 extern "C" int nerf_fused_pack(const float* const* srcs, int32_t n_srcs, const int32_t* map_src,

@@ -134,6 +134,27 @@ class NerfFusedEncoding(ctypes.Structure):
     ]
 
 
+class NerfFusedComposite(ctypes.Structure):
+    _fields_ = [
+        ("dist", c_vp),
+        ("rgb", c_vp),
+        ("weights", c_vp),
+        ("coef", c_vp),
+        ("grad_rgb", c_vp),
+        ("grad_head", c_vp),
+        ("ld_head", c_i64),
+        ("grad_sigma", c_vp),
+        ("ld_sigma", c_i64),
+        ("samples_per_ray", c_i32),
+        ("head_layer", c_i32),
+        ("sigma_layer", c_i32),
+        ("scale_a", c_f),
+        ("scale_b", c_f),
+        ("density_shift", c_f),
+        ("reserved", c_i32),
+    ]
+
+
 NERF_HASHGRID_MAX_LEVELS = 32
 NERF_HASHGRID_MAX_FEATURES = 8
 
@@ -193,6 +214,8 @@ _SIGNATURES = {
     "nerf_pack_weight_x3": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
     "nerf_mlp_fused_fwd": (c_i32, [ctypes.POINTER(NerfFusedLayer), c_i32, c_vp, c_i64,
                                    ctypes.POINTER(NerfFusedEncoding), c_vp]),
+    "nerf_mlp_fused_render": (c_i32, [ctypes.POINTER(NerfFusedLayer), c_i32, c_vp, c_i64,
+                                      ctypes.POINTER(NerfFusedEncoding), ctypes.POINTER(NerfFusedComposite), c_vp]),
     "nerf_struct_size": (c_i64, [c_i32]),
     "nerf_fused_pack": (c_i32, [ctypes.POINTER(c_vp), c_i32, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "nerf_hashgrid_fwd": (c_i32, [ctypes.POINTER(NerfHashgridParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
@@ -214,7 +237,8 @@ _SIGNATURES = {
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES.keys())
 # argument structs in nerf_struct_size's order (their sizes are checked against the library at load)
-STRUCTS = (NerfPEParams, NerfFusedLayer, NerfFusedEncoding, NerfHashgridParams, NerfAdamBatch, NerfSeg)
+STRUCTS = (NerfPEParams, NerfFusedLayer, NerfFusedEncoding, NerfHashgridParams, NerfAdamBatch, NerfSeg,
+           NerfFusedComposite)
 
 _lib = None
 
@@ -234,7 +258,7 @@ def load(path: str | None = None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.nerf_abi_version() != 6:
+    if lib.nerf_abi_version() != 7:
         raise RuntimeError("nerf_amd: ABI version mismatch between Python binding and libnerf_amd.so")
     for which, st in enumerate(STRUCTS):
         if lib.nerf_struct_size(which) != ctypes.sizeof(st):

@@ -57,6 +57,52 @@ WGRAD_ROW257 = os.environ.get("NERF_WGRAD_257", "1") != "0"
 # reduce).  The result differs from the per-pass sum only in fp32 summation order.
 MERGE_PASSES = os.environ.get("NERF_MERGE_PASSES", "1") != "0"
 
+# Alpha compositing fused into the field MLP's launches (nerf_mlp_fused_render): the forward
+# composites each tile's rays at the tile end and the input-gradient chain takes the compositing's
+# gradient from per-sample coefficients (NERF_FUSE_COMPOSITE=0: nerf_composite_fwd/bwd launches).
+FUSE_COMPOSITE = os.environ.get("NERF_FUSE_COMPOSITE", "1") != "0"
+
+
+class CompositeSpec:
+    """The renderer's compositing of one field pass (barf/model_interpolation.py:316-353 with the
+    NerfModel head activations), run inside the field MLP's launches: interval lengths [M], samples
+    per ray, density factor and shift.  The forward stores its per-sample backward coefficients in
+    ``coef`` ([M, 8], include/nerf_amd.h nerf_fused_composite)."""
+
+    __slots__ = ("dist", "S", "sa", "sb", "shift", "coef")
+
+    def __init__(self, dist: torch.Tensor, S: int, sa: float, sb: float, shift: float = 0.0):
+        self.dist, self.S, self.sa, self.sb, self.shift = dist, int(S), float(sa), float(sb), float(shift)
+        self.coef = None
+
+
+def composite_sigma_layer(plan) -> int:
+    """The layer whose column output is the raw density, or -1 (row 3 of the head layer)."""
+    return plan.column_outputs[0][0] if plan.column_outputs else -1
+
+
+def composite_eligible(plan, M: int, S: int) -> bool:
+    """The fused forward runs this plan and its last layer can hand its heads to the compositing."""
+    if not FUSE_COMPOSITE or matmul_precision() != "x3" or not mlp_fused.eligible(plan, M):
+        return False
+    if not (16 <= S <= 128 and 128 % S == 0 and M % S == 0 and M * 32 < (1 << 31)):
+        return False
+    L = len(plan.layers)
+    if len(plan.column_outputs) > 1 or (plan.column_outputs and plan.column_outputs[0][0] == L - 1):
+        return False
+    kbr, _ = mlp_fused._layer_shape(plan, L - 1)
+    N = plan.layers[L - 1].module.out_features
+    return kbr > 0 and (4 if composite_sigma_layer(plan) < 0 else 3) <= N <= 16
+
+
+def composite_grads_torch(comp: CompositeSpec, g_rgb: torch.Tensor, sigma_col: bool):
+    """The compositing's gradient rows from its coefficients where the fused chain cannot take them:
+    d head [M, 3] (+ d sigma-raw [M]) = coef * grad_rgb of the sample's ray."""
+    gr = g_rgb.repeat_interleave(comp.S, dim=0)
+    gh = comp.coef[:, 0:3] * gr
+    gs = (comp.coef[:, 4:7] * gr).sum(dim=1)
+    return gh, gs
+
 
 def _wgrad_workspace(ws: torch.Tensor, M: int, N4: int, Kp: int) -> torch.Tensor:
     need = K.linear_wgrad_workspace_bytes(M, N4, Kp)
@@ -271,9 +317,12 @@ def _src_tensor(src: Source, pos, dirs, acts, dir_rd):
 
 class MLPFunction(torch.autograd.Function):
     @classmethod
-    def apply(cls, plan: MLPPlan, *args):
-        # grad mode is off inside forward (and needs_input_grad ignores it): note it for forward
+    def apply(cls, plan: MLPPlan, *args, composite: CompositeSpec | None = None):
+        # grad mode is off inside forward (and needs_input_grad ignores it): note it for forward.
+        # composite: the renderer's compositing run inside the fused launches (composite_eligible);
+        # the outputs then end with (rgb [B, 3], weights [B, S]) (weights non-differentiable)
         plan.infer = not torch.is_grad_enabled()
+        plan.composite = composite
         return super().apply(plan, *args)
 
     @staticmethod
@@ -283,7 +332,13 @@ class MLPFunction(torch.autograd.Function):
         # (NerfModel with delayed density never reads z_last: a 268 MB memset + clone per step)
         ctx.set_materialize_grads(False)
         ctx.fused_forward = False
+        comp = getattr(plan, "composite", None)
+        plan.composite = None
+        ctx.comp = None
+        rgb = w = None
         prec = matmul_precision()
+        if comp is not None and not composite_eligible(plan, M, comp.S):
+            raise RuntimeError("MLPFunction: fused compositing requested for a plan / size it does not fit")
         acts: list[torch.Tensor] = []
         masks: list[torch.Tensor | None] = []
         pre: list[torch.Tensor] = []
@@ -306,7 +361,14 @@ class MLPFunction(torch.autograd.Function):
             col_t = {li: torch.empty(M, device=pos.device, dtype=torch.float32) for li, _ in plan.column_outputs}
             # deferred encodings (render_raw) are generated by the kernel itself, their rows stored by
             # the first layer that reads them
-            fused.run(M, pos, dirs, dir_rd, acts, masks, col_t, (K.deferred(pos), K.deferred(dirs)))
+            if comp is not None:
+                B = M // comp.S
+                rgb = torch.empty(B, 3, device=pos.device, dtype=torch.float32)
+                w = torch.empty(B, comp.S, device=pos.device, dtype=torch.float32)
+                comp.coef = (torch.empty(M, 8, device=pos.device, dtype=torch.float32)
+                             if keep_all else None)
+            fused.run(M, pos, dirs, dir_rd, acts, masks, col_t, (K.deferred(pos), K.deferred(dirs)),
+                      comp=(comp, rgb, w, composite_sigma_layer(plan)) if comp is not None else None)
             K.mark_filled(pos)
             K.mark_filled(dirs)
             cols = tuple(col_t[li] for li, _ in plan.column_outputs)
@@ -371,6 +433,10 @@ class MLPFunction(torch.autograd.Function):
             ctx.save_for_backward(pos, dirs if dirs is not None else pos, *acts, *pre)
         if cols is None:
             cols = tuple(acts[li][:, c].contiguous() for li, c in plan.column_outputs)
+        if comp is not None:
+            ctx.comp = comp
+            ctx.mark_non_differentiable(w)
+            return tuple(acts[i] for i in plan.outputs) + cols + (rgb, w)
         return tuple(acts[i] for i in plan.outputs) + cols
 
     @staticmethod
@@ -387,6 +453,14 @@ class MLPFunction(torch.autograd.Function):
         dev = pos.device
         dY: list[torch.Tensor | None] = [None] * L
         owned = [True] * L       # False: dY[i] is autograd's incoming tensor (never written in place)
+        comp = ctx.comp
+        g_rgb = None
+        if comp is not None:
+            n_out = len(plan.outputs) + len(plan.column_outputs)
+            g_rgb = grads[n_out]
+            grads = grads[:n_out]
+            if g_rgb is not None:
+                g_rgb = g_rgb.contiguous()
         col_grads: list[list[tuple[int, torch.Tensor]]] = [[] for _ in range(L)]
         for (li, c), g in zip(plan.column_outputs, grads[len(plan.outputs):]):
             if g is not None:
@@ -410,32 +484,63 @@ class MLPFunction(torch.autograd.Function):
         # the head gradient through the stored ReLU bits, when nothing else feeds the backward
         # (a column output's gradient joins the chain as one more k-block and is added to its
         # layer's stored gradient below, as in the layer-by-layer path)
-        chain = (ctx.fused_forward
-                 and all(dY[i] is None for i in range(L - 1)) and dY[L - 1] is not None
-                 and all(len(col_grads[li]) == 1 for li, _ in plan.column_outputs)
-                 and mlp_fused.dgrad_eligible(plan, M)
-                 and mlp_fused.FusedInputGrad.layout(plan, need_pos, need_dir) is not None)
+        chain_ok = (ctx.fused_forward and mlp_fused.dgrad_eligible(plan, M)
+                    and mlp_fused.FusedInputGrad.layout(plan, need_pos, need_dir) is not None)
+        # fused compositing: the chain forms the head / density gradient rows itself from the
+        # forward's coefficients and grad_rgb (and stores them for the weight gradients) when they
+        # are the only gradients; otherwise they are formed here and join the others
+        comp_chain = (g_rgb is not None and chain_ok and all(d is None for d in dY)
+                      and not any(col_grads))
+        if g_rgb is not None and not comp_chain:
+            sl = composite_sigma_layer(plan)
+            gh, gs = composite_grads_torch(comp, g_rgb, sl >= 0)
+            head = plan.layers[L - 1]
+            if dY[L - 1] is None:
+                dY[L - 1] = torch.zeros(M, head.out_ld, device=dev, dtype=torch.float32)
+            elif not owned[L - 1]:
+                dY[L - 1] = dY[L - 1].clone()
+            owned[L - 1] = True
+            dY[L - 1][:, 0:3] += gh
+            if sl < 0:
+                dY[L - 1][:, 3] += gs
+            else:
+                col_grads[sl].append((dict(plan.column_outputs)[sl], gs))
+        chain = chain_ok and (comp_chain or (
+            all(dY[i] is None for i in range(L - 1)) and dY[L - 1] is not None
+            and all(len(col_grads[li]) == 1 for li, _ in plan.column_outputs)))
         if chain:
             key = (dev, bool(need_pos), bool(need_dir))
             fd = plan.fused_dgrad.get(key)
             if fd is None:
                 fd = plan.fused_dgrad[key] = mlp_fused.FusedInputGrad(plan, dev, need_pos, need_dir)
-            g_head = dY[L - 1]
             g_cols = {}
-            for li, _ in plan.column_outputs:
-                g4 = torch.zeros(M, 4, device=dev, dtype=torch.float32)
-                g4[:, 0] = col_grads[li][0][1].reshape(-1)
-                g_cols[li] = g4
+            comp_rt = None
+            if comp_chain:
+                g_head = None
+                dY[L - 1] = torch.empty(M, plan.layers[L - 1].out_ld, device=dev, dtype=torch.float32)
+                if plan.layers[L - 1].out_ld > 4:
+                    dY[L - 1][:, 4:].zero_()
+            else:
+                g_head = dY[L - 1]
+                for li, _ in plan.column_outputs:
+                    g4 = torch.zeros(M, 4, device=dev, dtype=torch.float32)
+                    g4[:, 0] = col_grads[li][0][1].reshape(-1)
+                    g_cols[li] = g4
+            sl = composite_sigma_layer(plan)
             for l in range(L - 1):
                 dY[l] = torch.empty(M, plan.layers[l].out_ld, device=dev, dtype=torch.float32)
                 if plan.layers[l].out_ld > 256 and plan.layers[l].N > 256:
+                    if comp_chain and l == sl and plan.layers[l].out_ld == 260:
+                        continue              # the chain writes the density column 256 (+ zeros to 259)
                     dY[l][:, 256:].zero_()    # the chain fills the register-fed 256 columns
+            if comp_chain:
+                comp_rt = (comp, g_rgb, dY[L - 1], dY[sl][:, 256:] if sl >= 0 else None, sl)
             # encoding-input gradients (pose refinement): one buffer per step that produces them
             x_out = {}
             for (l, _, _, _, x, *_rest) in fd.steps:
                 if x is not None:
                     x_out[l] = torch.empty(M, x.k_pad, device=dev, dtype=torch.float32)
-            fd.run(M, g_head, dY, ctx.masks, g_cols, x_out)
+            fd.run(M, g_head, dY, ctx.masks, g_cols, x_out, comp=comp_rt)
             for (l, _, _, _, x, *_rest) in fd.steps:
                 if x is None:
                     continue

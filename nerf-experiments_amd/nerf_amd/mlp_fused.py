@@ -203,11 +203,13 @@ class FusedForward:
         _pack_image(self)
 
     def run(self, M: int, pos: torch.Tensor, dirs: torch.Tensor | None, dir_rd: int, acts, masks, col_outs,
-            gens=(None, None)):
+            gens=(None, None), comp=None):
         """Launch on the current stream.  acts[l]: [M, out_ld] fp32 or None (not stored),
         masks[l]: [M, 32] uint8 or None, col_outs: {layer: [M] fp32}.  gens: the DeferredEncoding
         of pos / dirs or None: generated in-kernel at every tile start (kernels.encode_fwd(defer=True))
-        and stored into the tensor, which later layers read; the first layer reads them from LDS."""
+        and stored into the tensor, which later layers read; the first layer reads them from LDS.
+        comp: (CompositeSpec, rgb [B, 3], weights [B, S], sigma layer) — the rays composited at the
+        end of every tile (nerf_mlp_fused_render), coefficients into spec.coef when it is set."""
         self.pack()
         L = len(self.plan.layers)
         descs = (_lib.NerfFusedLayer * L)()
@@ -269,11 +271,30 @@ class FusedForward:
             # algorithmic bytes: stored outputs / mask bits / columns written
             nbytes += (4.0 * M * acts[idx].shape[1] if acts[idx] is not None else 0.0) \
                 + (32.0 * M if masks[idx] is not None else 0.0) + (4.0 * M if idx in col_outs else 0.0)
+        cdesc = None
+        if comp is not None:
+            spec, rgb, w, sl = comp
+            cdesc = _lib.NerfFusedComposite()
+            cdesc.dist = spec.dist.data_ptr()
+            cdesc.rgb = rgb.data_ptr()
+            cdesc.weights = w.data_ptr() if w is not None else None
+            cdesc.coef = spec.coef.data_ptr() if spec.coef is not None else None
+            cdesc.samples_per_ray = spec.S
+            cdesc.head_layer = L - 1
+            cdesc.sigma_layer = sl
+            cdesc.scale_a, cdesc.scale_b, cdesc.density_shift = spec.sa, spec.sb, spec.shift
+            # algorithmic bytes: interval lengths in; rgb, weights, coefficients out
+            nbytes += 4.0 * M + 12.0 * (M // spec.S) + (4.0 * M if w is not None else 0.0) \
+                + (32.0 * M if spec.coef is not None else 0.0)
         end = K.TIMER.bracket("mlp_fused_fwd", flops, nbytes + self.image.numel() * self.image.element_size(),
                               fn="mlp_fused_kernel<0>") \
             if K.TIMER is not None else None
-        st = _lib.load().nerf_mlp_fused_fwd(descs, L, self.image.data_ptr(), M, encs if gen_of else None,
-                                            K._stream(self.device))
+        if cdesc is not None:
+            st = _lib.load().nerf_mlp_fused_render(descs, L, self.image.data_ptr(), M, encs if gen_of else None,
+                                                   ctypes.byref(cdesc), K._stream(self.device))
+        else:
+            st = _lib.load().nerf_mlp_fused_fwd(descs, L, self.image.data_ptr(), M, encs if gen_of else None,
+                                                K._stream(self.device))
         if end is not None:
             end.record()
         _lib.check(st, "nerf_mlp_fused_fwd")
@@ -408,11 +429,14 @@ class FusedInputGrad:
     def pack(self):
         _pack_image(self)
 
-    def run(self, M: int, g_head: torch.Tensor, dY, masks, g_cols=None, x_out=None):
+    def run(self, M: int, g_head: torch.Tensor | None, dY, masks, g_cols=None, x_out=None, comp=None):
         """g_head: [M, ld] gradient of the last layer's output; g_cols: {layer: [M, 4] buffer whose
         column 0 is the gradient of the layer's column output}; x_out: {layer: [M, k_pad] buffer for
         the gradient of the layer's encoding input}.  Fills dY[l] ([M, out_ld] fp32, the columns of
-        the register-fed chain) for l = L-2 .. 0 on the current stream."""
+        the register-fed chain) for l = L-2 .. 0 on the current stream.  comp: (CompositeSpec,
+        grad_rgb [B, 3], head-gradient rows [M, >=4], density-gradient rows (a [M, >=4] view) or
+        None, sigma layer) — the head and density blocks are formed in-kernel from the fused
+        compositing's coefficients (seg_gen 3 / 4) and stored to those rows."""
         g_cols = g_cols or {}
         x_out = x_out or {}
         self.pack()
@@ -428,7 +452,17 @@ class FusedInputGrad:
             d.nb = nb
             d.relu = 0
             d.nseg = 1 if kbh else 0
-            if kbh:
+            if kbh and comp is not None:
+                # the composite's head (first step) / density (the density layer's step) gradient
+                coef = comp[0].coef
+                d.seg_kb[0] = 1
+                d.seg_k[0] = 8
+                d.seg_rd[0] = 1
+                d.seg_rows[0] = coef.shape[0]
+                d.seg_ld[0] = 8
+                d.seg_ptr[0] = coef.data_ptr()
+                d.seg_gen[0] = 3 if kbr == 0 else 4
+            elif kbh:
                 src = g_head if kbr == 0 else g_cols[l]
                 d.seg_kb[0] = 1
                 d.seg_k[0] = (lp.N + 3) // 4 * 4 if kbr == 0 else 4
@@ -460,10 +494,28 @@ class FusedInputGrad:
             # algorithmic bytes: HBM-fed gradients and ReLU bits read, dY / encoding gradients written
             nbytes += (4.0 * d.seg_k[0] * d.seg_rows[0] if kbh else 0.0) + (32.0 * M if d.mask_in else 0.0)
             nbytes += 4.0 * M * min(d.ldo, n_out) + (4.0 * M * d.ldo2 if x is not None else 0.0)
+        cdesc = None
+        if comp is not None:
+            spec, g_rgb, gh, gsig, sl = comp
+            cdesc = _lib.NerfFusedComposite()
+            cdesc.grad_rgb = g_rgb.data_ptr()
+            cdesc.grad_head = gh.data_ptr()
+            cdesc.ld_head = gh.stride(0)
+            cdesc.grad_sigma = gsig.data_ptr() if gsig is not None else None
+            cdesc.ld_sigma = gsig.stride(0) if gsig is not None else 0
+            cdesc.samples_per_ray = spec.S
+            cdesc.head_layer = len(self.plan.layers) - 1
+            cdesc.sigma_layer = sl
+            # algorithmic bytes beyond the coefficient rows counted above: grad_rgb, the rows stored
+            nbytes += 12.0 * (M // spec.S) + 16.0 * M * (2 if gsig is not None else 1)
         end = K.TIMER.bracket("mlp_fused_dgrad", flops, nbytes + self.image.numel() * self.image.element_size(),
                               fn="mlp_fused_kernel<1>") \
             if K.TIMER is not None else None
-        st = _lib.load().nerf_mlp_fused_fwd(descs, S, self.image.data_ptr(), M, None, K._stream(self.device))
+        if cdesc is not None:
+            st = _lib.load().nerf_mlp_fused_render(descs, S, self.image.data_ptr(), M, None, ctypes.byref(cdesc),
+                                                   K._stream(self.device))
+        else:
+            st = _lib.load().nerf_mlp_fused_fwd(descs, S, self.image.data_ptr(), M, None, K._stream(self.device))
         if end is not None:
             end.record()
         _lib.check(st, "nerf_mlp_fused_fwd (input-gradient chain)")

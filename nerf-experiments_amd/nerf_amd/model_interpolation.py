@@ -9,7 +9,8 @@ _compute_color, forward, compute_psnr, configure_optimizers) and same outputs.
 Kernels used:
   t sampling        nerf_sample_uniform  (Philox stream seeded from torch's CPU generator)
   encodings + MLP   NerfModel.render_raw (encode + fp32 MFMA linear chain)
-  compositing       nerf_composite_fwd/bwd (heads' softplus/sigmoid fused)
+  compositing       inside the field MLP's launches (nerf_mlp_fused_render) where the rays fill
+                    whole 128-sample tiles, else nerf_composite_fwd/bwd (heads' activations fused)
   resampling        nerf_resample_pdf (batch fallback decided on device)
 No step of ``forward`` synchronises the host with the device (the reference's
 isnan prints, int(alpha) and the resample validity check all did).
@@ -214,6 +215,12 @@ class NerfInterpolation(nn.Module):
                 raise ValueError(f"strategy must be one of ('left', 'middle'), was '{self.integration_strategy}'")
             # (B,) pixel widths hit the reference's .repeat(1, S).view(N, 1) quirk -> pw[n % B]
             pw_mode = 0 if (pixel_width is not None and pixel_width.dim() == 2) else 1
+            if model.fused_composite_ok(batch_size * samples_per_ray, samples_per_ray):
+                # compositing inside the field MLP's launches (nerf_mlp_fused_render)
+                rgb, weights = model.render_composite(ray_origs, ray_dirs, pixel_width, t_start, t_end,
+                                                      samples_per_ray, query, pw_mode, sample_dist,
+                                                      *self.density_factor)
+                return rgb, weights, sample_dist
             heads = model.render_raw(ray_origs, ray_dirs, pixel_width, t_start, t_end, samples_per_ray, query,
                                      pw_mode)
             rgb, weights = composite_raw(heads, sample_dist, batch_size, samples_per_ray, *self.density_factor)

@@ -21,7 +21,7 @@ from typing import Iterator, Literal
 import torch as th
 import torch.nn as nn
 import torch.nn.functional as F
-from .mlp import MLPFunction, nerf_model_plan
+from .mlp import CompositeSpec, MLPFunction, composite_eligible, nerf_model_plan
 from .positional_encodings import PositionalEncoding
 
 # encodings generated inside the fused field-MLP kernel (NERF_FUSE_ENC=0: stand-alone encoding
@@ -157,3 +157,23 @@ class NerfModel(NerfBaseModel):
         dir_pe = self.direction_encoder.encode_padded(ray_dirs, defer=FUSE_ENCODINGS)
         z_last, head, dens = self._run_mlp(pos_pe, dir_pe, samples_per_ray)
         return self._heads(z_last, head, dens)
+
+    def fused_composite_ok(self, n_samples: int, samples_per_ray: int) -> bool:
+        """render_composite can run these rays (nerf_mlp_fused_render: split precision, whole rays
+        per 128-sample tile)."""
+        return composite_eligible(self._get_plan(), n_samples, samples_per_ray)
+
+    def render_composite(self, ray_origs: th.Tensor, ray_dirs: th.Tensor, pixel_width: th.Tensor | None,
+                         t_start: th.Tensor, t_end: th.Tensor, samples_per_ray: int, query: int, pw_mode: int,
+                         distances: th.Tensor, scale_a: float, scale_b: float) -> tuple[th.Tensor, th.Tensor]:
+        """render_raw followed by the renderer's compositing (_render_rays on the activated heads,
+        barf/model_interpolation.py:316-353), both inside the field MLP's launches: (rgb [B, 3],
+        weights [B, S]); rgb and weights bitwise those of composite_raw, weights non-differentiable."""
+        pos_pe = self.position_encoder.encode_rays(ray_origs, ray_dirs, t_start, t_end, pixel_width,
+                                                   samples_per_ray, query, pw_mode, defer=FUSE_ENCODINGS)
+        dir_pe = self.direction_encoder.encode_padded(ray_dirs, defer=FUSE_ENCODINGS)
+        plan = self._get_plan()
+        comp = CompositeSpec(distances.contiguous().view(-1), samples_per_ray, scale_a, scale_b)
+        outs = MLPFunction.apply(plan, pos_pe.shape[0], pos_pe, dir_pe, samples_per_ray, *plan.params(),
+                                 composite=comp)
+        return outs[-2], outs[-1]
