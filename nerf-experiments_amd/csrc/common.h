@@ -38,6 +38,34 @@ __device__ __forceinline__ double wave_inclusive_scan(double v) {
     return v;
 }
 
+// The same inclusive scan on DPP lane shifts, no LDS round trip per step (the __shfl_up form is a
+// ds_bpermute per 32-bit half and step): row_shr 1, 2, 4, 8 inside each 16-lane row, then row_bcast
+// 15 / 31 carry the row totals (lanes without a source add 0).  A different summation tree than
+// wave_inclusive_scan: use one or the other consistently.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_shift_d(double v) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, ROW_MASK, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, ROW_MASK, 0xf, false);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double wave_inclusive_scan_dpp(double v) {
+    v += dpp_shift_d<0x111, 0xf>(v);     // row_shr:1
+    v += dpp_shift_d<0x112, 0xf>(v);     // row_shr:2
+    v += dpp_shift_d<0x114, 0xf>(v);     // row_shr:4
+    v += dpp_shift_d<0x118, 0xf>(v);     // row_shr:8
+    v += dpp_shift_d<0x142, 0xa>(v);     // row_bcast:15 into rows 1, 3
+    v += dpp_shift_d<0x143, 0xc>(v);     // row_bcast:31 into rows 2, 3
+    return v;
+}
+// lane 63's value in every lane (two readlanes: scalar registers, no LDS)
+__device__ __forceinline__ double wave_last_d(double v) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, 63);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), 63);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
 __device__ __forceinline__ int wave_inclusive_scan_int(int v) {
     const int lane = lane_id();
 #pragma unroll

@@ -5,7 +5,7 @@
 // Reference: NerfInterpolation._render_rays, barf/model_interpolation.py:316-353
 //   b_s = ((-sigma_s * delta_s) * scale_a) * scale_b,  T_s = exp(sum_{j<s} b_j) (fp64 prefix),
 //   w_s = T_s * (1 - exp(b_s)),  rgb = sum_s w_s c_s.
-// One wavefront per ray; lane l owns the R samples s = 64 r + l.
+// One wavefront per ray; lane l owns the R samples s = 64 r + l.  Prefix sums: fp64 DPP wave scans.
 #pragma once
 #include "common.h"
 
@@ -39,9 +39,9 @@ __device__ __forceinline__ void composite_ray(int S, float sa, float sb, int act
         float bb = ((-sig) * del[r]) * sa;
         bb = bb * sb;
         if (s >= S) bb = 0.f;
-        const double incl = wave_inclusive_scan((double)bb);
+        const double incl = wave_inclusive_scan_dpp((double)bb);
         const double ex = carry + (incl - (double)bb);      // exclusive prefix
-        carry += __shfl(incl, NERF_WAVE - 1, NERF_WAVE);
+        carry += wave_last_d(incl);
         T[r] = (s == 0) ? 1.0f : expf((float)ex);
         e[r] = expf(bb);
         w[r] = T[r] * (1.0f - e[r]);
@@ -65,9 +65,9 @@ __device__ __forceinline__ void composite_ray(int S, float sa, float sb, int act
             for (int r = 0; r < R; ++r) {
                 const int s = r * NERF_WAVE + lane;
                 const double q = s < S ? (double)c[r][ch] * (double)w[r] : 0.0;
-                const double qi = wave_inclusive_scan(q);
+                const double qi = wave_inclusive_scan_dpp(q);
                 qincl[r] = qcarry + qi;
-                qcarry += __shfl(qi, NERF_WAVE - 1, NERF_WAVE);
+                qcarry += wave_last_d(qi);
             }
 #pragma unroll
             for (int r = 0; r < R; ++r) {
