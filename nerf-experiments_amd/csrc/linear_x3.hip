@@ -1226,6 +1226,100 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     }
 }
 
+// ------------------------------------------------------------------- TN small N
+// Weight gradient of a layer with few outputs (N <= 16: the colour head's last Linear(128, 3 or 4),
+// barf/model_interpolation_architecture.py:88-92), where the tile kernels would run a 128-row MFMA
+// tile for 4 rows.  One workgroup per M split streams the split's rows once (dY: 4 N4 bytes, X:
+// 4 ktot bytes per row); thread (row group g, column quad q) accumulates exact fp32 products of the
+// rows m = mbeg + g, g + RG, ... in sample order (SN_U rows' loads in flight per thread), and the RG
+// row groups' partial sums are added in a fixed order through LDS: deterministic, and finer than the
+// 3 x bf16 products of the tile kernels.  Same slab / bias-slab layout and reduce.
+constexpr int SN_T = 512;
+constexpr int SN_U = 8;
+template <int N4>
+__global__ __launch_bounds__(SN_T) void linear_wgrad_smalln_kernel(TNArgs a, int kpad) {
+    extern __shared__ __attribute__((aligned(16))) float sn_part[];     // [RG][N4][ktot] + [RG][N4]
+    const int split = blockIdx.x;
+    const int mbeg = split * a.m_per_split;
+    const int mend = min(mbeg + a.m_per_split, a.M);
+    const int ktot = a.X.ktot;
+    const int qw = ktot >> 2;                       // column quads per row
+    const int rg = SN_T / qw;                       // row groups
+    const int t = threadIdx.x;
+    const int g = t / qw, q = t - g * qw;
+    const bool live = g < rg;
+    // this thread's four packed columns 4 q .. 4 q + 3: one segment (segments span multiples of 32)
+    int xs = 0, xoff = 0;
+#pragma unroll
+    for (int i = 0; i < MAX_SEGS; ++i)
+        if (i < a.X.n && 4 * q >= a.X.koff[i] && 4 * q < a.X.koff[i] + a.X.kp[i]) { xs = i; xoff = 4 * q - a.X.koff[i]; }
+    const bool col_ok = live && xoff < pick4(a.X.k, xs);
+    const float* xp0 = pick4(a.X.ptr, xs) + xoff;
+    const int64_t xld0 = pick4(a.X.ld, xs);
+    const unsigned xrd0 = (unsigned)pick4(a.X.row_div, xs);
+    const float* xp1 = pick4(a.x1ptr, xs) + xoff;
+    const int64_t xld1 = pick4(a.x1ld, xs);
+    const unsigned xrd1 = (unsigned)pick4(a.x1rd, xs);
+    f4 acc[N4];
+    f4 dbs[N4 / 4];
+#pragma unroll
+    for (int n = 0; n < N4; ++n) acc[n] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < N4 / 4; ++j) dbs[j] = f4{0.f, 0.f, 0.f, 0.f};
+    if (live) {
+        for (int m0 = mbeg + g; m0 < mend; m0 += SN_U * rg) {
+            f4 y[SN_U][N4 / 4], x[SN_U];
+#pragma unroll
+            for (int u = 0; u < SN_U; ++u) {
+                const int m = m0 + u * rg;
+                const bool ok = m < mend;
+                const bool b1 = m >= a.M0;
+                const int mr = ok ? (b1 ? m - a.M0 : m) : 0;
+                const float* yr = (b1 ? a.dY1 : a.dY) + (int64_t)mr * (b1 ? a.lddy1 : a.lddy);
+#pragma unroll
+                for (int j = 0; j < N4 / 4; ++j)
+                    y[u][j] = ok ? *reinterpret_cast<const f4*>(yr + 4 * j) : f4{0.f, 0.f, 0.f, 0.f};
+                const unsigned rd = b1 ? xrd1 : xrd0;
+                const unsigned xr = rd == 1u ? (unsigned)mr : (unsigned)mr / rd;
+                const float* xr_p = (b1 ? xp1 : xp0) + (int64_t)xr * (b1 ? xld1 : xld0);
+                x[u] = ok && col_ok ? *reinterpret_cast<const f4*>(xr_p) : f4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int u = 0; u < SN_U; ++u) {
+#pragma unroll
+                for (int n = 0; n < N4; ++n) {
+                    const float yn = y[u][n >> 2][n & 3];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) acc[n][c] = __builtin_fmaf(yn, x[u][c], acc[n][c]);
+                }
+#pragma unroll
+                for (int j = 0; j < N4 / 4; ++j) dbs[j] += y[u][j];
+            }
+        }
+        float* p = sn_part + (size_t)g * N4 * ktot;
+#pragma unroll
+        for (int n = 0; n < N4; ++n) *reinterpret_cast<f4*>(p + (size_t)n * ktot + 4 * q) = acc[n];
+        if (q == 0) {
+            float* d = sn_part + (size_t)rg * N4 * ktot + g * N4;
+#pragma unroll
+            for (int j = 0; j < N4 / 4; ++j) *reinterpret_cast<f4*>(d + 4 * j) = dbs[j];
+        }
+    }
+    __syncthreads();
+    float* slab = a.slab + (size_t)split * (size_t)((a.N + TB - 1) / TB * TB) * kpad;
+    for (int o = t; o < N4 * ktot; o += SN_T) {
+        float v = 0.f;
+        for (int gg = 0; gg < rg; ++gg) v += sn_part[(size_t)gg * N4 * ktot + o];
+        const int n = o / ktot, k = o - n * ktot;
+        slab[(size_t)n * kpad + k] = v;
+    }
+    if (t < N4) {
+        float v = 0.f;
+        for (int gg = 0; gg < rg; ++gg) v += sn_part[(size_t)rg * N4 * ktot + gg * N4 + t];
+        a.db_slab[(size_t)split * ((a.N + TB - 1) / TB * TB) + t] = v;
+    }
+}
+
 // Interleaved split weights: element (r, c) of a [rows][ld] matrix goes to
 // Wx[r][c / 32][c % 32] (hi) and Wx[r][c / 32][32 + c % 32] (lo), i.e. each 32-column
 // chunk of a row is 128 contiguous bytes: 32 hi then 32 lo.
@@ -1420,6 +1514,12 @@ extern "C" int nerf_linear_gauss_x3(const nerf_seg* segs, int32_t n_segs, int64_
     return nerf::gauss_reduce(part, slabs, N, inv_std, grad_inv_std, accumulate, part + slabs * N, st);
 }
 
+// NERF_WGRAD_SMALLN=0: layers with N <= 16 on the 128-tile kernel (A/B switch, read once)
+static const bool SMALLN_ON = [] {
+    const char* e = getenv("NERF_WGRAD_SMALLN");
+    return !(e && e[0] == '0');
+}();
+
 extern "C" int nerf_linear_wgrad_x3_rows(const float* dY, int64_t ld_dy, const nerf_seg* segs, int64_t M0,
                                          const float* dY1, int64_t ld_dy1, const nerf_seg* segs1, int64_t M1,
                                          int32_t n_segs, int32_t N, void* workspace, size_t workspace_bytes,
@@ -1462,6 +1562,22 @@ extern "C" int nerf_linear_wgrad_x3_rows(const float* dY, int64_t ld_dy, const n
         a.M0 = (int)M;
     }
     // (M = 0 still launches: every split writes its zero slab, which the reduce reads)
+    if (N <= 16 && L.ktot <= 4 * SN_T && SMALLN_ON) {                  // few output rows: vector-ALU stream
+        const int n4 = (N + 3) / 4 * 4;
+        const int rg = SN_T / (L.ktot / 4);
+        const size_t lds = ((size_t)rg * n4 * L.ktot + (size_t)rg * n4) * sizeof(float);
+        if (lds <= 160 * 1024) {
+            const dim3 grid((unsigned)splits), block(SN_T);
+            switch (n4) {
+                case 4: hipLaunchKernelGGL(linear_wgrad_smalln_kernel<4>, grid, block, lds, as_stream(stream), a, ntk * TB); break;
+                case 8: hipLaunchKernelGGL(linear_wgrad_smalln_kernel<8>, grid, block, lds, as_stream(stream), a, ntk * TB); break;
+                case 12: hipLaunchKernelGGL(linear_wgrad_smalln_kernel<12>, grid, block, lds, as_stream(stream), a, ntk * TB); break;
+                default: hipLaunchKernelGGL(linear_wgrad_smalln_kernel<16>, grid, block, lds, as_stream(stream), a, ntk * TB); break;
+            }
+            NERF_CHECK_LAUNCH();
+            return NERF_OK;
+        }
+    }
     if ((N > 128 || L.ktot > 128) && N <= 257 && L.ktot <= 256) {   // one 256 x 256 tile (+ row 256)
         const int64_t blocks = splits;
         hipLaunchKernelGGL((linear_wgrad_x3_stream_kernel<3, 2>), dim3((unsigned)blocks), dim3(512), 0,

@@ -347,7 +347,11 @@ def _split_bf16(W):
                                        (5003, 256, (200, 24), (1, 7)), (777, 200, (128, 60), (1, 3)),
                                        (50, 256, (256,), (1,)), (10, 160, (64,), (1,)),
                                        # 257 rows by their true count: the 256 x 256 tile + row 256
-                                       (70000, 257, (256,), (1,)), (40, 257, (200,), (3,))])
+                                       (70000, 257, (256,), (1,)), (40, 257, (200,), (3,)),
+                                       # N <= 16: the vector-ALU small-N weight gradient (exact fp32
+                                       # products, well inside the split-precision bound)
+                                       (100003, 4, (128,), (1,)), (999, 16, (64, 32), (1, 5)),
+                                       (77, 12, (512, 32), (1, 7)), (5000, 8, (1024,), (1,))])
 def test_linear_x3_fwd_wgrad(M, N, ks, rd):
     """3 x bf16 split-precision GEMMs (hi*hi + hi*lo + lo*hi, fp32 accumulate).
 
@@ -436,7 +440,9 @@ def test_linear_x3_fwd_wgrad(M, N, ks, rd):
                                                 (70000, 33333, 257, (256,), (1,), (1,)),
                                                 (2000, 1500, 256, (256, 64), (1, 1), (1, 1)),
                                                 (4096, 2048, 128, (256, 32), (1, 64), (1, 32)),
-                                                (1000, 37, 260, (200,), (1,), (3,))])
+                                                (1000, 37, 260, (200,), (1,), (3,)),
+                                                (131072, 65536, 3, (128,), (1,), (1,)),
+                                                (3000, 77, 16, (64, 32), (1, 1), (1, 64))])
 def test_linear_x3_wgrad_two_row_blocks(M0, M1, N, ks, rd0, rd1):
     """nerf_linear_wgrad_x3_rows: the weight gradient of two passes' rows (own dY / X pointers,
     row strides and row divisors) in one launch and one reduce, against fp64 over the
