@@ -716,7 +716,10 @@ def main():
             "config": {"workload": wl["config"], "workload_key": args.workload,
                        "rays_per_gpu": wl["rays"], "samples_per_ray": wl["coarse"] + wl["fine"],
                        "coarse_samples": wl["coarse"], "fine_samples": wl["fine"], "global_rays": wl["rays"] * world,
-                       "parallelism": f"ray-batch dp{world}" + (" (RCCL bucketed all-reduce from post-accumulate-grad hooks)" if world > 1 else "")},
+                       "parallelism": f"ray-batch dp{world}" + ((" (RCCL bucketed all-reduce from post-accumulate-grad hooks)"
+                                                          if backend == "nccl" else
+                                                          f" ({backend} bucketed all-reduce: a multi-process rehearsal)")
+                                                         if world > 1 else "")},
             "roofline": roofline,
             "roofline_hbm": (_hbm_roofline(ks, hbm_bytes, hbm_ms, hbm_gbs, args.steps) if hbm_ms > 0 else
                              {"kernel": "none: the positional encodings and the alpha compositing have no launch "
