@@ -682,6 +682,11 @@ __host__ __device__ constexpr int epi_placed() {                 // parts placed
     return KBR - EPI0 < EPI_NP ? (KBR - EPI0 > 0 ? KBR - EPI0 : 0) : EPI_NP;
 }
 
+// pin the split HBM-fed operand blocks in registers across a layer's chunk loop (0: hipcc's choice)
+#ifndef NERF_FUSED_PIN_HBM
+#define NERF_FUSED_PIN_HBM 1
+#endif
+
 // k-steps of weight fragments read ahead of the step being multiplied
 #ifndef NERF_FUSED_FA
 #define NERF_FUSED_FA 2
@@ -847,6 +852,17 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
             }
         }
     }
+#if NERF_FUSED_PIN_HBM
+    // the split HBM-fed operand stays in registers for the whole chunk loop: hipcc otherwise keeps
+    // the fp32 rows and redoes the split in every chunk (8 conversions + 4 subtracts + 4 shifts per
+    // block and chunk: 32-64 VALU per chunk of the skip / head layers)
+    if constexpr (KBH > 0) {
+#pragma unroll
+        for (int kh = 0; kh < KBH; ++kh)
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) asm volatile("" : "+v"(hh[kh][sb]), "+v"(hl[kh][sb]));
+    }
+#endif
     const unsigned hbm_frag = (unsigned)LF(int, hbm_off, l) + (unsigned)c.lane * 16u;
 
     // the previous chunk's accumulators (its epilogue runs during the current chunk)
