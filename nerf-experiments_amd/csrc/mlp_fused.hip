@@ -682,6 +682,11 @@ __host__ __device__ constexpr int epi_placed() {                 // parts placed
     return KBR - EPI0 < EPI_NP ? (KBR - EPI0 > 0 ? KBR - EPI0 : 0) : EPI_NP;
 }
 
+// the first layer's weight fragments one chunk ahead by builtin loads (0: the asm loads + vmcnt(0))
+#ifndef NERF_FUSED_L0_PREFETCH
+#define NERF_FUSED_L0_PREFETCH 1
+#endif
+
 // pin the split HBM-fed operand blocks in registers across a layer's chunk loop (0: hipcc's choice)
 #ifndef NERF_FUSED_PIN_HBM
 #define NERF_FUSED_PIN_HBM 1
@@ -867,6 +872,60 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
 
     // the previous chunk's accumulators (its epilogue runs during the current chunk)
     f4 pv[SB] = {};
+#if NERF_FUSED_L0_PREFETCH
+    if constexpr (KBR == 0) {
+        // The first layer has no register-fed part and no DMA.  Its weight fragments (and biases)
+        // come from L2 one chunk ahead through builtin buffer loads whose waits hipcc counts, so a
+        // chunk's MFMAs do not wait for an L2 round trip and the previous chunk's stores are not
+        // drained in every chunk (the form below — asm loads waited with vmcnt(0) — paid both in
+        // each of the layer's 8-16 chunks).
+        typedef bf16x8 fragk_t[KBH > 0 ? KBH : 1][2];
+        auto frag_load = [&](fragk_t& f, int ch) __attribute__((always_inline)) {
+#pragma unroll
+            for (int kh = 0; kh < KBH; ++kh)
+#pragma unroll
+                for (int hl_ = 0; hl_ < 2; ++hl_)
+                    f[kh][hl_] = __builtin_bit_cast(
+                        bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                    c.rimg, hbm_frag + (unsigned)(((ch * KBH + kh) * 2 + hl_) * 1024), 0, 0));
+        };
+        auto bias_load = [&](int ch) __attribute__((always_inline)) {
+            return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              c.rimg, st.bias_off + (MODE == MODE_FWD ? 64u * (unsigned)ch : 0u), 0, 0));
+        };
+        // two fragment / bias buffers used alternately (a register copy of a just-issued load would
+        // wait for it): chunk ch multiplies `cur` while chunk ch + 1's loads land in `nxt`
+        fragk_t hA, hB;
+        f4 bA, bB = f4{0.f, 0.f, 0.f, 0.f};
+        frag_load(hA, 0);
+        auto step = [&](int ch, fragk_t& cur, fragk_t& nxt, f4& bthis, const f4& bprev) __attribute__((always_inline)) {
+            frag_load(nxt, ch + 1 < NC ? ch + 1 : ch);    // (past the end: a harmless repeat)
+            bthis = bias_load(ch);
+            f4 a[SB];
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) a[sb] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kh = 0; kh < KBH; ++kh) {
+#pragma unroll
+                for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(cur[kh][1], hh[kh][sb], a[sb]);
+#pragma unroll
+                for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(cur[kh][0], hl[kh][sb], a[sb]);
+#pragma unroll
+                for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(cur[kh][0], hh[kh][sb], a[sb]);
+            }
+            // the previous chunk's epilogue (all parts: no register-fed stages to place them in)
+#pragma unroll
+            for (int i = 0; i < EPI_NP; ++i) epi_part<MODE>(c, st, epi_part_of(i), ch - 1, pv, bprev);
+            if constexpr (!NERF_FUSED_P3S) epi_part<MODE>(c, st, 3, ch - 1, pv, bprev);
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) pv[sb] = a[sb];
+        };
+        for (int ch = 0; ch < NC; ch += 2) {
+            step(ch, hA, hB, bA, bB);
+            if (ch + 1 < NC) step(ch + 1, hB, hA, bB, bA);
+        }
+    } else
+#endif
     for (int ch = 0; ch < NC; ++ch) {
         // the previous chunk's biases (rows 4 g .. 4 g + 3), for its epilogue in this chunk, issued
         // before this chunk's DMA so that waiting for it does not wait for the DMA
