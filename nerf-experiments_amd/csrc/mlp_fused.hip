@@ -83,14 +83,16 @@ constexpr int ST_AUX_DG = NERF_FUSED_STORE_AUX_DG;
 // bias load at the start of the chunk itself
 constexpr int AFTER_DMA_VM = 1 + 2 * SB;
 // Layer-output stores in chunk pairs: a 16-row chunk is 64 B of each sample row, half a 128-B line.
-// The even chunk's values wait in registers for the odd one's, and the pair leaves as two stores
-// each covering whole lines of 8 samples (lanes s and s ^ 8 trade halves by a DPP row rotate), not
-// two half-line stores per sample a chunk apart.  Every chunk still issues 2 stores per column
-// block (counted waits assume at least that many).  NERF_FUSED_PAIR: 0 none, 1 the input-gradient
-// chain only (default: chain 3.73 -> 3.55 ms per mip step, while the forward ran 3.55 -> 3.69),
-// 2 both.
+// The even chunk's values wait in registers for the odd one's.  NERF_FUSED_PAIR: 0 none; 1 the
+// input-gradient chain only, as two stores each covering whole lines of 8 samples (lanes s and s ^ 8
+// trade halves by a DPP row rotate: chain 3.73 -> 3.55 ms per mip step); 2 that in the forward too
+// (WRITE_SIZE 1.0x, but the DPP / select work costs the forward ~0.2 ms); 3 (default) the chain as 1
+// and the forward's pair as its two half-line stores back to back, no lane exchange: forward
+// WRITE_SIZE 7.25 -> 6.47 GB per fine launch, forward +0.13 ms, chain -0.12 ms and weight gradients
+// -0.08 ms (fewer half-written lines left dirty for them): step -0.08 ms (profiles/r03m).  Every
+// chunk still issues 2 stores per column block (counted waits assume at least that many).
 #ifndef NERF_FUSED_PAIR
-#define NERF_FUSED_PAIR 1
+#define NERF_FUSED_PAIR 3
 #endif
 
 struct FusedArgs {
@@ -544,11 +546,20 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
                 const unsigned coff = ch == st.col_chunk ? st.sample_off[sb] : OOB;
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), st.rc, coff, 0, 0);
             } else {
+#if NERF_FUSED_PAIR == 3
+                // the pair's two half lines of every sample back to back (the even chunk's from the stash):
+                // no lane exchange, the halves reach L2 together
+                const unsigned oa = 16 * (ch - 1) < st.colok ? st.row_off[sb] + 64u * (unsigned)(ch - 1) : OOB;
+                const unsigned ob = 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
+                __builtin_amdgcn_raw_buffer_store_b128(st.stash[sb], st.ro, oa, 0, ST_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, ob, 0, ST_AUX);
+#else
                 f4 va, vb;
                 unsigned oa, ob;
                 pair_stores(c, st, sb, ch, st.colok, st.pa[sb], st.pb[sb], v, va, vb, oa, ob);
                 __builtin_amdgcn_raw_buffer_store_b128(va, st.ro, oa, 0, ST_AUX);
                 __builtin_amdgcn_raw_buffer_store_b128(vb, st.ro, ob, 0, ST_AUX);
+#endif
             }
 #else
             const unsigned off = ch >= 0 && 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
