@@ -450,13 +450,30 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(int splits, int n_val
             off = (size_t)n * kpad + k;
             stride = (size_t)npad * kpad;
         }
-        const float* base = is_db ? db_slab : slab;
+        const float* base = (is_db ? db_slab : slab) + off;
+#ifndef NERF_REDUCE_ILP2
+        // eight slabs' loads in flight per thread (the slabs were just written: the sum runs at the
+        // cache's bandwidth only with enough loads outstanding), summed in a fixed order
+        double q[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        int sp = g;
+        for (; sp + 28 < splits; sp += 32) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = base[(size_t)(sp + 4 * j) * stride];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) q[j] += (double)v[j];
+        }
+        for (int j = 0; sp < splits; sp += 4, ++j) q[j & 7] += (double)base[(size_t)sp * stride];
+        s0 = ((q[0] + q[1]) + (q[2] + q[3]));
+        s1 = ((q[4] + q[5]) + (q[6] + q[7]));
+#else
         int sp = g;
         for (; sp + 4 < splits; sp += 8) {
-            s0 += (double)base[(size_t)sp * stride + off];
-            s1 += (double)base[(size_t)(sp + 4) * stride + off];
+            s0 += (double)base[(size_t)sp * stride];
+            s1 += (double)base[(size_t)(sp + 4) * stride];
         }
-        if (sp < splits) s0 += (double)base[(size_t)sp * stride + off];
+        if (sp < splits) s0 += (double)base[(size_t)sp * stride];
+#endif
     }
     part[g][o] = s0 + s1;
     __syncthreads();
