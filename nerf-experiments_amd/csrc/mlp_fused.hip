@@ -89,7 +89,8 @@ constexpr int AFTER_DMA_VM = 1 + 2 * SB;
 // (WRITE_SIZE 1.0x, but the DPP / select work costs the forward ~0.2 ms); 3 (default) the chain as 1
 // and the forward's pair as its two half-line stores back to back, no lane exchange: forward
 // WRITE_SIZE 7.25 -> 6.47 GB per fine launch, forward +0.13 ms, chain -0.12 ms and weight gradients
-// -0.08 ms (fewer half-written lines left dirty for them): step -0.08 ms (profiles/r03m).  Every
+// -0.08 ms (fewer half-written lines left dirty for them): step -0.08 ms (profiles/r03m); 4 the
+// chain's pairs back to back as well (measured +0.1 ms in the chain, profiles/r03s).  Every
 // chunk still issues 2 stores per column block (counted waits assume at least that many).
 #ifndef NERF_FUSED_PAIR
 #define NERF_FUSED_PAIR 3
@@ -546,7 +547,7 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
                 const unsigned coff = ch == st.col_chunk ? st.sample_off[sb] : OOB;
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), st.rc, coff, 0, 0);
             } else {
-#if NERF_FUSED_PAIR == 3
+#if NERF_FUSED_PAIR >= 3
                 // the pair's two half lines of every sample back to back (the even chunk's from the stash):
                 // no lane exchange, the halves reach L2 together
                 const unsigned oa = 16 * (ch - 1) < st.colok ? st.row_off[sb] + 64u * (unsigned)(ch - 1) : OOB;
@@ -613,11 +614,19 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
                 __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, off1, 0, ST_AUX_DG);
                 __builtin_amdgcn_raw_buffer_store_b128(v, st.ro2, off2, 0, ST_AUX_DG);
             } else if (!sec) {
+#if NERF_FUSED_PAIR >= 4
+                // the pair's two half lines back to back (no lane exchange)
+                const unsigned oa = 16 * (ch - 1) < st.colok ? st.row_off[sb] + 64u * (unsigned)(ch - 1) : OOB;
+                const unsigned ob = 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
+                __builtin_amdgcn_raw_buffer_store_b128(st.stash[sb], st.ro, oa, 0, ST_AUX_DG);
+                __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, ob, 0, ST_AUX_DG);
+#else
                 f4 va, vb;
                 unsigned oa, ob;
                 pair_stores(c, st, sb, ch, st.colok, st.pa[sb], st.pb[sb], v, va, vb, oa, ob);
                 __builtin_amdgcn_raw_buffer_store_b128(va, st.ro, oa, 0, ST_AUX_DG);
                 __builtin_amdgcn_raw_buffer_store_b128(vb, st.ro, ob, 0, ST_AUX_DG);
+#endif
             } else {
                 f4 va, vb;
                 unsigned oa, ob;
