@@ -298,6 +298,17 @@ int nerf_linear_wgrad_x3_rows(const float* dY, int64_t ld_dy, const nerf_seg* se
                               const float* dY1, int64_t ld_dy1, const nerf_seg* segs1, int64_t M1,
                               int32_t n_segs, int32_t N, void* workspace, size_t workspace_bytes,
                               void* stream);
+/* nerf_linear_wgrad_x3_rows that also writes the per-ray sums of dY, raysum[ray][n] (n < N; rays of
+ * samples_per_ray0 rows in block 0, then of samples_per_ray1 rows in block 1), from the streamed
+ * single-tile kernel (N <= 256, 128 < N or 128 < K <= 256; 16 <= S <= 128 with S | 128, M0 % 128 = 0).
+ * A layer input that is per ray (the direction encoding of NerfModel's colour layer, row divisor S)
+ * then takes its weight gradient from the B rays instead of the M samples: sum_m dY[m] x[ray(m)] =
+ * sum_ray raysum[ray] x[ray] (barf/model_interpolation_architecture.py:88-92, 132-135). */
+int nerf_linear_wgrad_x3_rays(const float* dY, int64_t ld_dy, const nerf_seg* segs, int64_t M0,
+                              const float* dY1, int64_t ld_dy1, const nerf_seg* segs1, int64_t M1,
+                              int32_t n_segs, int32_t N, void* workspace, size_t workspace_bytes,
+                              float* raysum, int32_t samples_per_ray0, int32_t samples_per_ray1,
+                              void* stream);
 int nerf_pack_weight_x3(const float* W, int32_t N, int32_t K_orig, const int32_t* col_map,
                         int32_t Kp, void* Wp_x, void* Wt_x, int32_t ldwt, void* stream);
 

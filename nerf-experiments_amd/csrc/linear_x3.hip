@@ -751,6 +751,9 @@ struct TNArgs {
     int M0;
     const float* dY1; int64_t lddy1;
     const float* x1ptr[MAX_SEGS]; int64_t x1ld[MAX_SEGS]; int x1rd[MAX_SEGS];
+    // streamed kernel only: per-ray sums of dY (raysum[ray][n], rays of rs_S0 / rs_S1 samples in the
+    // two blocks, block 1's rays after block 0's rs_B0) for a per-ray input's weight gradient, or null
+    float* raysum; int rs_S0, rs_S1, rs_B0;
 };
 
 __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
@@ -1050,6 +1053,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         c_ok = xs >= 0 && xoff < pick4(a.X.k, xs);
     }
     float db = 0.f;
+    float ray_acc = 0.f;      // raysum: this dY column's sum over the current ray's rows so far
     // N = 257 (NerfModel's density + feature layer): row 256 of dW / db on the X conversion threads,
     // dW[256][c] = sum over the split's samples (in order) of dY[m][256] * X[m][c] as fp32 FMAs; the
     // step's 16 dY[m][256] values by scalar loads (uniform addresses), issued with the ring reads
@@ -1091,6 +1095,22 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         if (op == 0) {                                      // wave-uniform: the dY threads
 #pragma unroll
             for (int r = 0; r < WS_T; ++r) db += v[r];
+            if (a.raysum != nullptr && valid > 0) {
+                // rays end at step ends (16 | S, ray starts and splits at multiples of 128 rows)
+                float sv = 0.f;
+#pragma unroll
+                for (int r = 0; r < WS_T; ++r) sv += v[r];
+                ray_acc += sv;
+                const int last = WS_ROW0(step) + (valid < WS_T ? valid : WS_T) - 1;
+                const bool b1 = last >= a.M0;
+                const int rel = b1 ? last - a.M0 : last;
+                const int S = b1 ? a.rs_S1 : a.rs_S0;
+                if ((rel + 1) % S == 0) {
+                    const int ray = (b1 ? a.rs_B0 : 0) + rel / S;
+                    if (c < a.N) a.raysum[(size_t)ray * a.N + c] = ray_acc;
+                    ray_acc = 0.f;
+                }
+            }
         }
         if (xrow) {                                         // wave-uniform: the X threads of N = 257
 #pragma unroll
@@ -1520,10 +1540,10 @@ static const bool SMALLN_ON = [] {
     return !(e && e[0] == '0');
 }();
 
-extern "C" int nerf_linear_wgrad_x3_rows(const float* dY, int64_t ld_dy, const nerf_seg* segs, int64_t M0,
-                                         const float* dY1, int64_t ld_dy1, const nerf_seg* segs1, int64_t M1,
-                                         int32_t n_segs, int32_t N, void* workspace, size_t workspace_bytes,
-                                         void* stream) {
+static int wgrad_x3_rows_impl(const float* dY, int64_t ld_dy, const nerf_seg* segs, int64_t M0,
+                              const float* dY1, int64_t ld_dy1, const nerf_seg* segs1, int64_t M1,
+                              int32_t n_segs, int32_t N, void* workspace, size_t workspace_bytes,
+                              float* raysum, int32_t S0, int32_t S1, void* stream) {
     // N need not be a multiple of 4: the kernels read dY in 4-column pieces up to pad4(N) <= ld_dy;
     // slab rows past N are left unspecified (nerf_linear_wgrad_reduce's n_valid <= N)
     const int64_t M = M0 + M1;
@@ -1539,7 +1559,16 @@ extern "C" int nerf_linear_wgrad_x3_rows(const float* dY, int64_t ld_dy, const n
     float* db_slab = slab + (size_t)splits * ntn * TB * (size_t)ntk * TB;
     int64_t mps = (M + splits - 1) / splits;
     mps = ((mps + TBM - 1) / TBM) * TBM;
-    TNArgs a{dY, ld_dy, N, L, (int)M, (int)mps, splits, slab, db_slab, (int)M0, dY, ld_dy, {}, {}, {}};
+    if (raysum != nullptr) {
+        // per-ray sums of dY from the streamed kernel: rays of 16..128 samples (S | 128) that no step or
+        // split cuts (splits and block 1 start at multiples of 128 rows)
+        auto s_ok = [](int S) { return S >= 16 && S <= 128 && 128 % S == 0; };
+        NERF_REQUIRE(s_ok(S0) && (M1 == 0 || s_ok(S1)) && M0 % 128 == 0 && M0 % S0 == 0 && M1 % (M1 ? S1 : 1) == 0);
+        NERF_REQUIRE((N > 128 || L.ktot > 128) && N <= 256 && L.ktot <= 256);
+        mps = ((mps + 127) / 128) * 128;
+    }
+    TNArgs a{dY, ld_dy, N, L, (int)M, (int)mps, splits, slab, db_slab, (int)M0, dY, ld_dy, {}, {}, {},
+             raysum, S0 > 0 ? S0 : 1, S1 > 0 ? S1 : 1, S0 > 0 ? (int)(M0 / S0) : 0};
     for (int i = 0; i < MAX_SEGS; ++i) {
         a.x1ptr[i] = L.ptr[i];
         a.x1ld[i] = L.ld[i];
@@ -1589,6 +1618,24 @@ extern "C" int nerf_linear_wgrad_x3_rows(const float* dY, int64_t ld_dy, const n
     hipLaunchKernelGGL(linear_wgrad_x3_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
     NERF_CHECK_LAUNCH();
     return NERF_OK;
+}
+
+extern "C" int nerf_linear_wgrad_x3_rows(const float* dY, int64_t ld_dy, const nerf_seg* segs, int64_t M0,
+                                         const float* dY1, int64_t ld_dy1, const nerf_seg* segs1, int64_t M1,
+                                         int32_t n_segs, int32_t N, void* workspace, size_t workspace_bytes,
+                                         void* stream) {
+    return wgrad_x3_rows_impl(dY, ld_dy, segs, M0, dY1, ld_dy1, segs1, M1, n_segs, N, workspace, workspace_bytes,
+                              nullptr, 0, 0, stream);
+}
+
+extern "C" int nerf_linear_wgrad_x3_rays(const float* dY, int64_t ld_dy, const nerf_seg* segs, int64_t M0,
+                                         const float* dY1, int64_t ld_dy1, const nerf_seg* segs1, int64_t M1,
+                                         int32_t n_segs, int32_t N, void* workspace, size_t workspace_bytes,
+                                         float* raysum, int32_t samples_per_ray0, int32_t samples_per_ray1,
+                                         void* stream) {
+    NERF_REQUIRE(raysum != nullptr);
+    return wgrad_x3_rows_impl(dY, ld_dy, segs, M0, dY1, ld_dy1, segs1, M1, n_segs, N, workspace, workspace_bytes,
+                              raysum, samples_per_ray0, samples_per_ray1, stream);
 }
 
 extern "C" int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N, const nerf_seg* segs, int32_t n_segs,

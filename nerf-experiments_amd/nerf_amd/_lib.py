@@ -211,6 +211,9 @@ _SIGNATURES = {
     "nerf_linear_wgrad_x3": (c_i32, [c_vp, c_i64, c_i32, ctypes.POINTER(NerfSeg), c_i32, c_i64, c_vp, c_sz, c_vp]),
     "nerf_linear_wgrad_x3_rows": (c_i32, [c_vp, c_i64, ctypes.POINTER(NerfSeg), c_i64, c_vp, c_i64,
                                           ctypes.POINTER(NerfSeg), c_i64, c_i32, c_i32, c_vp, c_sz, c_vp]),
+    "nerf_linear_wgrad_x3_rays": (c_i32, [c_vp, c_i64, ctypes.POINTER(NerfSeg), c_i64, c_vp, c_i64,
+                                          ctypes.POINTER(NerfSeg), c_i64, c_i32, c_i32, c_vp, c_sz, c_vp, c_i32,
+                                          c_i32, c_vp]),
     "nerf_pack_weight_x3": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
     "nerf_mlp_fused_fwd": (c_i32, [ctypes.POINTER(NerfFusedLayer), c_i32, c_vp, c_i64,
                                    ctypes.POINTER(NerfFusedEncoding), c_vp]),

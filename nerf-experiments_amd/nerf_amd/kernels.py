@@ -514,7 +514,8 @@ def linear_wgrad_x3(dY: torch.Tensor, N4: int, segs, M: int, workspace: torch.Te
     kpad = sum(pad32(k) for _, k, _ in segs)
     wide = (N4 > 128 or kpad > 128) and N4 <= 257 and kpad <= 256
     end = TIMER.bracket("linear_wgrad_x3", 2.0 * M * N4 * kt, 4.0 * M * N4 + _segs_bytes(segs, M) + 4.0 * N4 * kt,
-                        fn="linear_wgrad_x3_stream_kernel" if wide else "linear_wgrad_x3_kernel") \
+                        fn="linear_wgrad_x3_stream_kernel" if wide else
+                        ("linear_wgrad_smalln_kernel" if N4 <= 16 else "linear_wgrad_x3_kernel")) \
         if TIMER is not None else None
     st = _lib.load().nerf_linear_wgrad_x3(_ptr(dY), dY.stride(0), N4, arr, len(segs), M, _ptr(workspace),
                                           workspace.numel() * workspace.element_size(), _stream(dY.device))
@@ -536,7 +537,8 @@ def linear_wgrad_x3_rows(blocks, N4: int, workspace: torch.Tensor) -> None:
     wide = (N4 > 128 or kpad > 128) and N4 <= 257 and kpad <= 256
     end = TIMER.bracket("linear_wgrad_x3", 2.0 * (M + M1) * N4 * kt,
                         4.0 * (M + M1) * N4 + _segs_bytes(segs, M) + _segs_bytes(segs1, M1) + 4.0 * N4 * kt,
-                        fn="linear_wgrad_x3_stream_kernel" if wide else "linear_wgrad_x3_kernel") \
+                        fn="linear_wgrad_x3_stream_kernel" if wide else
+                        ("linear_wgrad_smalln_kernel" if N4 <= 16 else "linear_wgrad_x3_kernel")) \
         if TIMER is not None else None
     st = _lib.load().nerf_linear_wgrad_x3_rows(_ptr(dY), dY.stride(0), a0, M, _ptr(dY1), dY1.stride(0), a1, M1,
                                                len(segs), N4, _ptr(workspace),
@@ -544,6 +546,27 @@ def linear_wgrad_x3_rows(blocks, N4: int, workspace: torch.Tensor) -> None:
     if end is not None:
         end.record()
     _lib.check(st, "nerf_linear_wgrad_x3_rows")
+
+
+def linear_wgrad_x3_rays(blocks, N4: int, workspace: torch.Tensor, raysum: torch.Tensor, S0: int, S1: int) -> None:
+    """linear_wgrad_x3_rows (streamed single-tile kernel) that also writes the per-ray sums of dY into
+    raysum [B0 + B1, N4] (nerf_linear_wgrad_x3_rays); blocks as linear_wgrad_x3_rows, M1 may be 0."""
+    (dY, segs, M), (dY1, segs1, M1) = blocks
+    a0, a1 = make_segs(segs), make_segs(segs1)
+    kt = sum(k for _, k, _ in segs)
+    if raysum.shape[1] != N4 or not raysum.is_contiguous():
+        raise ValueError("linear_wgrad_x3_rays: raysum must be contiguous [rays, N4]")
+    end = TIMER.bracket("linear_wgrad_x3", 2.0 * (M + M1) * N4 * kt,
+                        4.0 * (M + M1) * N4 + _segs_bytes(segs, M) + _segs_bytes(segs1, M1) + 4.0 * N4 * kt
+                        + 4.0 * raysum.numel(), fn="linear_wgrad_x3_stream_kernel") \
+        if TIMER is not None else None
+    st = _lib.load().nerf_linear_wgrad_x3_rays(_ptr(dY), dY.stride(0), a0, M, _ptr(dY1), dY1.stride(0), a1, M1,
+                                               len(segs), N4, _ptr(workspace),
+                                               workspace.numel() * workspace.element_size(), _ptr(raysum), S0, S1,
+                                               _stream(dY.device))
+    if end is not None:
+        end.record()
+    _lib.check(st, "nerf_linear_wgrad_x3_rays")
 
 
 def pack_weight_x3(W: torch.Tensor, col_map: torch.Tensor, Kp: int, Wpx: torch.Tensor | None,

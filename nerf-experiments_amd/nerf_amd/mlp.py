@@ -111,6 +111,58 @@ def _wgrad_workspace(ws: torch.Tensor, M: int, N4: int, Kp: int) -> torch.Tensor
     return torch.empty((need + 3) // 4, device=ws.device, dtype=torch.float32)
 
 
+# The weight gradient of a layer whose last input is per ray (NerfModel's colour layer reads the
+# direction encoding once per ray: row divisor S) as the streamed single-tile kernel over its other
+# inputs, which also sums dY over each ray's samples, then the per-ray input's part over the B rays:
+# sum_m dY[m] x[ray(m)] = sum_ray (sum_{m in ray} dY[m]) x[ray] (nerf_linear_wgrad_x3_rays;
+# NERF_WGRAD_RAYS=0: the 128-tile kernel over every sample's row, as before)
+WGRAD_RAYS = os.environ.get("NERF_WGRAD_RAYS", "1") != "0"
+
+
+def _ray_split(blocks, N4: int):
+    """(main segments per block, ray segment per block) when the layer's weight gradient can take
+    its last, per-ray input from per-ray dY sums; None otherwise."""
+    if not WGRAD_RAYS or N4 > 256:
+        return None
+    mains, rays = [], []
+    for dZ, segs, M in blocks:
+        if len(segs) < 2 or M == 0:
+            return None
+        t, k, S = segs[-1]
+        if not (16 <= S <= 128 and 128 % S == 0 and M % S == 0) or any(rd != 1 for _, _, rd in segs[:-1]):
+            return None
+        mains.append(segs[:-1])
+        rays.append((t, k, S))
+    kmain = sum(K.pad32(k) for _, k, _ in mains[0])
+    if kmain > 256 or not (N4 > 128 or kmain > 128) or blocks[0][2] % 128:
+        return None
+    return mains, rays
+
+
+def _wgrad_rays(blocks, N4: int, lp, workspace, gW, gb, acc, split) -> None:
+    """The weight gradient of `blocks` (one or two passes' rows) through the per-ray route (_ray_split)."""
+    mains, rays = split
+    Mt = sum(M for _, _, M in blocks)
+    kmain = sum(K.pad32(k) for _, k, _ in mains[0])
+    dev = blocks[0][0].device
+    Bs = [M // r[2] for (_, _, M), r in zip(blocks, rays)]
+    raysum = torch.empty(sum(Bs), N4, device=dev, dtype=torch.float32)
+    b0 = (blocks[0][0], mains[0], blocks[0][2])
+    b1 = (blocks[1][0], mains[1], blocks[1][2]) if len(blocks) > 1 else (blocks[0][0], mains[0], 0)
+    ws = _wgrad_workspace(workspace, Mt, N4, kmain)
+    K.linear_wgrad_x3_rays([b0, b1], N4, ws, raysum, rays[0][2], rays[1][2] if len(blocks) > 1 else 0)
+    K.linear_wgrad_reduce(Mt, N4, kmain, lp.N, ws, lp.col_map[:kmain], gW, gb, accumulate=acc)
+    kray = K.pad32(rays[0][1])
+    Bt = sum(Bs)
+    ws2 = _wgrad_workspace(workspace, Bt, N4, kray)
+    r0 = (raysum[:Bs[0]], [(rays[0][0], rays[0][1], 1)], Bs[0])
+    if len(blocks) > 1:
+        K.linear_wgrad_x3_rows([r0, (raysum[Bs[0]:], [(rays[1][0], rays[1][1], 1)], Bs[1])], N4, ws2)
+    else:
+        K.linear_wgrad_x3(r0[0], N4, r0[1], Bs[0], ws2)
+    K.linear_wgrad_reduce(Bt, N4, kray, lp.N, ws2, lp.col_map[kmain:kmain + kray], gW, None, accumulate=acc)
+
+
 def _flush_wgrad(entry, sink) -> None:
     """A stashed pass whose partner never ran its backward (BucketedGradAllReduce.finish()): its
     weight gradient alone, landed as the sink expects."""
@@ -119,8 +171,12 @@ def _flush_wgrad(entry, sink) -> None:
     gW, acc = sink.target(w)
     gb, _ = sink.target(b)
     ws = torch.empty((K.linear_wgrad_workspace_bytes(M, N4, lp.Kp) + 3) // 4, device=dZ.device, dtype=torch.float32)
-    K.linear_wgrad_x3(dZ, nrow, segs, M, ws)
-    K.linear_wgrad_reduce(M, N4, lp.Kp, lp.N, ws, lp.col_map, gW, gb, accumulate=acc)
+    rsplit = _ray_split([(dZ, segs, M)], N4) if nrow == N4 else None
+    if rsplit is not None:          # the route the unmerged backward takes: the same result, bitwise
+        _wgrad_rays([(dZ, segs, M)], N4, lp, ws, gW, gb, acc, rsplit)
+    else:
+        K.linear_wgrad_x3(dZ, nrow, segs, M, ws)
+        K.linear_wgrad_reduce(M, N4, lp.Kp, lp.N, ws, lp.col_map, gW, gb, accumulate=acc)
     sink.landed(w)
     sink.landed(b)
 
@@ -619,7 +675,14 @@ class MLPFunction(torch.autograd.Function):
                         raise RuntimeError("direct gradient sink: weight and bias of one layer out of step")
                 else:
                     gW, gb, acc = torch.empty_like(w), torch.empty_like(lp.module.bias), False
-                if prev is not None:
+                rsplit = None
+                if ctx.prec == "x3" and nrow == N4:
+                    rsplit = _ray_split([(prev[0], prev[1], prev[2]), (dZ, segs, M)] if prev is not None
+                                        else [(dZ, segs, M)], N4)
+                if rsplit is not None:
+                    _wgrad_rays([(prev[0], prev[1], prev[2]), (dZ, segs, M)] if prev is not None else [(dZ, segs, M)],
+                                N4, lp, workspace, gW, gb, acc, rsplit)
+                elif prev is not None:
                     pdZ, psegs, pM = prev[0], prev[1], prev[2]
                     ws = _wgrad_workspace(workspace, M + pM, N4, lp.Kp)
                     K.linear_wgrad_x3_rows([(pdZ, psegs, pM), (dZ, segs, M)], nrow, ws)
