@@ -148,3 +148,29 @@ def test_fused_composite_in_the_renderer():
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
     for a, b in zip(out[1][2], out[0][2]):
         _close(a, b)
+
+
+@pytest.mark.parametrize("S", [96, 200])
+def test_renderer_falls_back_for_rays_that_do_not_fill_a_tile(S):
+    """Samples per ray that do not divide the 128-sample tile (or exceed it) take render_raw + the
+    stand-alone compositing kernels: the renderer's output is the same with the fused switch on or off."""
+    from nerf_amd import NerfInterpolation, mlp
+    model = _model()
+    assert not model.fused_composite_ok(64 * S, S)
+    o, d, _, _, pw = _rays(64, 8, seed=31)
+    ren = NerfInterpolation(2.0, 8.0, model, S, "stratified_uniform", -1.0, "middle").to(DEV)
+    outs = []
+    for fuse in (True, False):
+        saved = mlp.FUSE_COMPOSITE
+        mlp.FUSE_COMPOSITE = fuse
+        try:
+            torch.manual_seed(3)
+            fine, _ = ren(o, d, pw)
+            model.zero_grad(set_to_none=True)
+            fine.square().sum().backward()
+        finally:
+            mlp.FUSE_COMPOSITE = saved
+        torch.cuda.synchronize()
+        outs.append((fine.detach(), [p.grad.clone() for p in model.parameters()]))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert all(torch.equal(a, b) for a, b in zip(outs[0][1], outs[1][1]))
