@@ -1065,6 +1065,9 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         for (int r = 0; r < WS_T; ++r) {
             int m = WS_ROW0(step) + r;
             m = m < mend && r < WS_VALID(step) ? m : mbeg;
+#ifdef NERF_WS_DIAG_YD_FIXED      // diagnostic builds only: every row-256 load from one row (cache hits)
+            m = mbeg;
+#endif
             const bool b1 = m >= a.M0;
             yd[r] = *(const __attribute__((address_space(4))) float*)((b1 ? a.dY1 : a.dY) +
                                                                        (int64_t)(b1 ? m - a.M0 : m) * (b1 ? a.lddy1 : a.lddy) + 256);
