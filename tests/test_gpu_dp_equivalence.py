@@ -1,0 +1,87 @@
+"""Ray-batch data parallelism on the real kernels: two processes, each with half of a batch, reduce
+their weight gradients through BucketedGradAllReduce(direct=True) — the field MLP's weight gradients
+land straight in the buckets from the slab reduce (per-ray, small-N and merged-pass routes included)
+and the buckets are all-reduced as they complete — and the result equals one process's gradient of
+the whole batch (rays are independent, the gradient mean is the only exchange).  The
+ranks share the one GPU over gloo (the driver's multi-GPU runs use RCCL, one GPU per rank; the CPU
+suite's tests/test_ddp_direct.py covers the same protocol on the oracle forward).  Equidistant
+samples and the deterministic resample, so both runs see the same samples per ray; tolerance 1e-5
+of each gradient's scale (summation order)."""
+import os
+import sys
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "nerf-experiments_amd")
+B = 512
+
+
+def _setup(dev):
+    from nerf_amd import BarfPositionalEncoding, IntegratedBarfFourierFeatures, NerfInterpolation, NerfModel
+    torch.manual_seed(0)
+    pos = IntegratedBarfFourierFeatures(10, 10, 1.28, 6.4, True, 1.0, True)
+    pos.pixel_width_sigma = 0.0
+    dirs = BarfPositionalEncoding(4, 4, 1.28, 6.4, True, 1.0)
+    model = NerfModel(4, 256, True, False, 2, pos, dirs, 5e-4, 1e-4, 200000)
+    ren = NerfInterpolation(2.0, 8.0, model, 128, "equidistant", 0.0, "middle", model, 64).to(dev)
+    g = torch.Generator().manual_seed(3)
+    o = (torch.randn(B, 3, generator=g) * 0.2 + torch.tensor([0.0, 0.0, 4.0])).to(dev)
+    d = torch.nn.functional.normalize(torch.randn(B, 3, generator=g) * 0.2 - torch.tensor([0.0, 0.0, 1.0]),
+                                      dim=1).to(dev)
+    pw = torch.full((B,), 1 / 1111.1, device=dev)
+    c = torch.rand(B, 3, generator=g).to(dev)
+    return ren, o, d, pw, c
+
+
+def _grads(ren, o, d, pw, c, sl):
+    from nerf_amd.ddp import BucketedGradAllReduce
+    ar = BucketedGradAllReduce(list(ren.parameters()), direct=True)
+    try:
+        loss, _ = ren.training_loss(o[sl], d[sl], pw[sl], c[sl])
+        loss.backward()
+        ar.finish()
+        torch.cuda.synchronize()
+        return {n: p.grad.detach().cpu().clone() for n, p in ren.named_parameters() if p.grad is not None}
+    finally:
+        ar.remove()
+
+
+def _worker(rank, world, init_file, out_file):
+    sys.path.insert(0, PKG)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method="file://" + init_file, rank=rank, world_size=world)
+    try:
+        torch.set_float32_matmul_precision("high")
+        dev = torch.device("cuda", 0)
+        ren, o, d, pw, c = _setup(dev)
+        n = B // world
+        g = _grads(ren, o, d, pw, c, slice(rank * n, (rank + 1) * n))
+        if rank == 0:
+            torch.save(g, out_file)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_equal_the_whole_batch():
+    with tempfile.TemporaryDirectory() as tmp:
+        init_file, out_file = os.path.join(tmp, "rdzv"), os.path.join(tmp, "g.pt")
+        mp.spawn(_worker, args=(2, init_file, out_file), nprocs=2, join=True)
+        dp = torch.load(out_file, weights_only=True)
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision("high")
+    try:
+        ren, o, d, pw, c = _setup(torch.device("cuda", 0))
+        ref = _grads(ren, o, d, pw, c, slice(0, B))
+    finally:
+        torch.set_float32_matmul_precision(prev)
+    assert dp.keys() == ref.keys() and len(ref) > 0
+    for n in ref:
+        scale = ref[n].abs().max().clamp_min(1e-30)
+        assert (dp[n] - ref[n]).abs().max() <= 1e-5 * scale, n
