@@ -24,8 +24,10 @@ Other BASELINE.json configs as extra workloads (same JSON line, their own `confi
                    64 coarse samples, fine pass of 64 + 192 (round/argmax), positions at the sample t,
                    Adam(0.9, 0.99, 1e-15); 5120 rays per GPU -> 64 + 256 ray-samples per ray
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload mip|n2v|barf|ingp]
-    (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload mip|n2v|barf|garf|ingp]
+    N>1: `python bench.py --gpus N` starts N rank processes itself (RANK / LOCAL_RANK / WORLD_SIZE,
+    MASTER_ADDR 127.0.0.1, a free MASTER_PORT; launch_ranks), or run it under
+    `python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N` (WORLD_SIZE must equal N).
 
 Prints ONE JSON line on rank 0 (schema: see DESIGN.md §Measurement).
 """
@@ -260,7 +262,9 @@ def build_workload(name: str, device, rank: int, feed: bool = False):
         from nerf_amd.model_ingp import INGPEncoding, NaiveINGP
         torch.manual_seed(0)
         # 3d-ingp/main.py:94-118 with the hash-grid position encoder of its commented config (:98-104)
-        ren = NaiveINGP(2, 7, 64, 192, INGPEncoding(1600, 16, 2 ** 16, 2, 16), IngpFourier(4), 8, 256,
+        ren = NaiveINGP(near_sphere_normalized=2, far_sphere_normalized=7, samples_per_ray_fine=192,
+                        samples_per_ray_coarse=64, position_encoder=INGPEncoding(1600, 16, 2 ** 16, 2, 16),
+                        direction_encoder=IngpFourier(4), n_hidden=8, hidden_dim=256,
                         learning_rate=1e-5, learning_rate_decay=1, weight_decay=0).to(device)
         o, d, pw, target, _ = synthetic_batch_lego(w["rays"], 1000 + rank, device, 400)
         opt = ren.configure_optimizers()["optimizer"]
@@ -614,6 +618,57 @@ def teardown(dist) -> None:
         dist.destroy_process_group()
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, cmd: list[str], env: dict | None = None, poll_s: float = 0.2) -> int:
+    """Start ``cmd`` as N rank processes of one node (RANK / LOCAL_RANK / WORLD_SIZE /
+    LOCAL_WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set as torch.distributed.run sets them)
+    and wait for them.  The caller has touched no GPU (the ranks initialise their own devices) and
+    is not replaced (no exec): rank 0's stdout — the JSON line — passes straight through, the other
+    ranks' stdout goes to stderr.  If a rank fails, the others (this launcher's own children, by
+    PID) are terminated, so a rank blocked in a collective cannot hang the job; returns the first
+    non-zero exit status, else 0."""
+    import signal
+    import subprocess
+    base = dict(os.environ if env is None else env)
+    base.update({"WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
+                 "MASTER_PORT": base.get("MASTER_PORT") or str(_free_port()),
+                 "GROUP_RANK": "0", "ROLE_RANK": "0"})
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), ROLE_WORLD_SIZE=str(n))
+        procs.append(subprocess.Popen(cmd, env=e, stdout=None if r == 0 else sys.stderr))
+    status = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]          # every rank polled (no short-circuit)
+            if all(c is not None for c in codes):
+                break
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                status = bad[0]
+                break
+            time.sleep(poll_s)
+    finally:
+        live = [p for p in procs if p.poll() is None]
+        for p in live:
+            p.send_signal(signal.SIGTERM)
+        for p in live:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    if status == 0:
+        status = next((p.returncode for p in procs if p.returncode != 0), 0)
+    return status
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -635,12 +690,24 @@ def main():
                          "high/medium = 3 x bf16 split MFMA (fp32-accurate to ~2^-16); the reference's "
                          "naive-to-vanilla run uses medium + 16-mixed (main.py:53)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` without a launcher: start N rank processes of this same
+        # command (one per GPU) and relay rank 0's line.  Nothing above has touched the GPU, and
+        # this process is not replaced (no exec): it only waits for its children.
+        sys.exit(launch_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
     torch.set_float32_matmul_precision(args.matmul_precision)
 
     # NERF_DIST_BACKEND=gloo rehearses the multi-process step on fewer GPUs than ranks (ranks share
     # devices round-robin); the driver's runs use RCCL ("nccl"), one GPU per rank
     backend = os.environ.get("NERF_DIST_BACKEND", "nccl")
     world, rank, local_rank, dist = init_distributed(backend)
+    if world != args.gpus:
+        # under torch.distributed.run the world is the launcher's; a different --gpus would make
+        # the line's n_gpus disagree with the ranks that ran
+        teardown(dist)
+        ap.error(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     device = torch.device("cuda", local_rank if backend == "nccl" else local_rank % torch.cuda.device_count())
     torch.cuda.set_device(device)
 
@@ -699,7 +766,7 @@ def main():
                        else "ray-samples/sec (coarse+fine), training step"),
             "value": value,
             "unit": "ray-samples/s",
-            "n_gpus": world,
+            "n_gpus": dist.get_world_size() if dist is not None else 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
@@ -755,4 +822,18 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        # a rank that fails must exit at once: left to the interpreter's shutdown it can block in
+        # the process group's teardown while its peers wait in a collective, and the job hangs
+        try:
+            main()
+        except SystemExit:
+            raise
+        except BaseException:       # noqa: BLE001
+            import traceback
+            traceback.print_exc()
+            sys.stderr.flush()
+            sys.stdout.flush()
+            os._exit(1)
+    else:
+        main()

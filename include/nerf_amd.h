@@ -53,6 +53,14 @@ const char* nerf_status_string(int status);
  * 0 nerf_pe_params, 1 nerf_fused_layer, 2 nerf_fused_encoding, 3 nerf_hashgrid_params,
  * 4 nerf_adam_batch, 5 nerf_seg, 6 nerf_fused_composite; -1 for an unknown index. */
 int64_t nerf_struct_size(int32_t which);
+/* Build flags of the loaded library: 0 for a product build.  Bit 0 (NERF_BUILD_DIAG_FUSED): the
+ * fused field-MLP kernels were compiled with a NERF_FUSED_DIAG_* switch; bit 1
+ * (NERF_BUILD_DIAG_WGRAD): the streamed weight gradient with a NERF_WS_DIAG_* switch.  Those
+ * switches drop work for profiling ablations and give wrong results by construction; bindings
+ * refuse a library with any bit set (nerf_amd/_lib.py load()). */
+#define NERF_BUILD_DIAG_FUSED 1
+#define NERF_BUILD_DIAG_WGRAD 2
+int32_t nerf_build_flags(void);
 
 /* ---------------------------------------------------------------------------
  * Alpha compositing (a4).  One wavefront per ray, exclusive prefix sum of

@@ -16,6 +16,15 @@ extern "C" int64_t nerf_struct_size(int32_t which) {
     }
 }
 
+// each translation unit that holds diagnostic switches reports its own compile flags (a variant
+// build recompiles only that unit: tools/build_variant.sh)
+extern "C" int32_t nerf_tu_build_flags_mlp_fused(void);
+extern "C" int32_t nerf_tu_build_flags_linear_x3(void);
+
+extern "C" int32_t nerf_build_flags(void) {
+    return NERF_TU_BUILD_FLAGS | nerf_tu_build_flags_mlp_fused() | nerf_tu_build_flags_linear_x3();
+}
+
 extern "C" const char* nerf_status_string(int status) {
     switch (status) {
         case NERF_OK: return "ok";

@@ -17,6 +17,23 @@
         if (!(cond)) return NERF_ERR_INVALID_ARG;             \
     } while (0)
 
+// Diagnostic ablation switches (profiling builds only, wrong results by construction).  Every
+// NERF_*_DIAG_* macro tested in csrc/ must be listed here (tests/test_capi.py checks the list): a
+// translation unit compiled with one reports it through nerf_build_flags(), which load() refuses.
+#if defined(NERF_FUSED_DIAG_NOFRAG) || defined(NERF_FUSED_DIAG_MFMAONLY) || defined(NERF_FUSED_DIAG_NOMASK) || \
+    defined(NERF_FUSED_DIAG_NOSPLIT) || defined(NERF_FUSED_DIAG_NOSTORE) || defined(NERF_FUSED_DIAG_NOMASKIN) || \
+    defined(NERF_FUSED_DIAG_DROPSTORE)
+#define NERF_TU_DIAG_FUSED NERF_BUILD_DIAG_FUSED
+#else
+#define NERF_TU_DIAG_FUSED 0
+#endif
+#if defined(NERF_WS_DIAG_YD_FIXED) || defined(NERF_WS_DIAG_NOCONV) || defined(NERF_WS_DIAG_NOMFMA)
+#define NERF_TU_DIAG_WGRAD NERF_BUILD_DIAG_WGRAD
+#else
+#define NERF_TU_DIAG_WGRAD 0
+#endif
+#define NERF_TU_BUILD_FLAGS (NERF_TU_DIAG_FUSED | NERF_TU_DIAG_WGRAD)
+
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 static inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }

@@ -1664,3 +1664,7 @@ extern "C" int nerf_pack_weight_x3(const float* W, int32_t N, int32_t K_orig, co
     NERF_CHECK_LAUNCH();
     return NERF_OK;
 }
+
+extern "C" __attribute__((visibility("hidden"))) int32_t nerf_tu_build_flags_linear_x3(void) {
+    return NERF_TU_BUILD_FLAGS;
+}

@@ -1450,3 +1450,7 @@ extern "C" int nerf_fused_pack(const float* const* srcs, int32_t n_srcs, const i
     NERF_CHECK_LAUNCH();
     return NERF_OK;
 }
+
+extern "C" __attribute__((visibility("hidden"))) int32_t nerf_tu_build_flags_mlp_fused(void) {
+    return NERF_TU_BUILD_FLAGS;
+}

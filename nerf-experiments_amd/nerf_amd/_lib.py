@@ -220,6 +220,7 @@ _SIGNATURES = {
     "nerf_mlp_fused_render": (c_i32, [ctypes.POINTER(NerfFusedLayer), c_i32, c_vp, c_i64,
                                       ctypes.POINTER(NerfFusedEncoding), ctypes.POINTER(NerfFusedComposite), c_vp]),
     "nerf_struct_size": (c_i64, [c_i32]),
+    "nerf_build_flags": (c_i32, []),
     "nerf_fused_pack": (c_i32, [ctypes.POINTER(c_vp), c_i32, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "nerf_hashgrid_fwd": (c_i32, [ctypes.POINTER(NerfHashgridParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
                                   c_vp, c_vp, c_i64, c_vp]),
@@ -266,6 +267,12 @@ def load(path: str | None = None):
     for which, st in enumerate(STRUCTS):
         if lib.nerf_struct_size(which) != ctypes.sizeof(st):
             raise RuntimeError(f"nerf_amd: {st.__name__} layout differs from libnerf_amd.so's")
+    flags = lib.nerf_build_flags()
+    if flags != 0 and os.environ.get("NERF_ALLOW_DIAG_BUILD") != "1":
+        # NERF_*_DIAG_* ablation builds drop work and return wrong results by construction; only
+        # the profiling tools opt in (NERF_ALLOW_DIAG_BUILD=1), never the product path or a test
+        raise RuntimeError(f"nerf_amd: {p} is a diagnostic build (nerf_build_flags = {flags:#x}); "
+                           "rebuild with `make -C nerf-experiments_amd`")
     if path is None:
         _lib = lib
     return lib

@@ -96,7 +96,8 @@ class BucketedGradAllReduce:
     a parameter that NO rank produced a gradient for ends with ``.grad = None`` on every rank, as
     with one process (the reduced flags are read on the host only by a rank that itself lacked a
     gradient).  Gradients are pre-scaled by 1/world and summed.  One backward per ``finish()``.
-    With world size 1 (or no process group) every method is a no-op and ``.grad`` is untouched.
+    With world size 1 (or no process group) and ``direct=False`` every method is a no-op and
+    ``.grad`` is untouched.
 
     ``direct=True`` also installs this object as the field MLPs' gradient sink
     (``nerf_amd.mlp.GRAD_SINK``): every MLP forward recorded for autograd ``claim``s its layers'
@@ -106,7 +107,11 @@ class BucketedGradAllReduce:
     ``landed(p)``; the last expected landing marks the parameter ready, so its bucket can start its
     all-reduce while the MLP's remaining weight-gradient kernels run.  Those parameters never pass
     through autograd's accumulation (the backward returns None for them), and a field used twice
-    per step costs no extra add."""
+    per step costs no extra add.  This holds at world size 1 too: the sink is installed, the MLP
+    weight gradients bypass autograd accumulation and any user gradient hooks on those
+    parameters, and ``finish()`` must still be called after every backward (it flushes held-back
+    weight gradients and resets the per-step claims).  A forward that claims parameters after
+    gradients of the previous backward have landed, without a ``finish()`` in between, raises."""
 
     def __init__(self, params, bucket_bytes: int = 1 << 20, group=None, direct: bool = False):
         seen, plist = set(), []
@@ -156,6 +161,9 @@ class BucketedGradAllReduce:
         """One more expected contribution for each of ``params`` this step (all must be ours)."""
         if not all(id(p) in self._owned for p in params):
             return False
+        if self._arrived:
+            raise RuntimeError("BucketedGradAllReduce: a forward claimed parameters after the previous "
+                               "backward's gradients landed; call finish() after every backward()")
         for p in params:
             self._expected[id(p)] = self._expected.get(id(p), 0) + 1
         return True
@@ -180,6 +188,9 @@ class BucketedGradAllReduce:
         if first and p.grad is None:
             p.grad = torch.empty_like(p)
             return p.grad, False
+        if p.grad is None:
+            raise RuntimeError("BucketedGradAllReduce: .grad was cleared between two contributions of one "
+                               "step (zero_grad inside a step, or a skipped finish())")
         return p.grad, True
 
     def remaining(self, p) -> int:
@@ -217,10 +228,13 @@ class BucketedGradAllReduce:
         self._launch_ready()
 
     def _launch(self, b: _Bucket) -> None:
-        b.flat[b.flags_at:].fill_(1.0)
-        for j, r in enumerate(b.ready):
-            if not r:
-                b.flat[b.flags_at + j].fill_(0.0)
+        # the "has a gradient" flags: one fill when every parameter is ready, else one host->device
+        # copy of the whole flag row (not a launch per missing parameter)
+        if all(b.ready):
+            b.flat[b.flags_at:].fill_(1.0)
+        else:
+            flags = torch.tensor([1.0 if r else 0.0 for r in b.ready], dtype=b.flat.dtype)
+            b.flat[b.flags_at:].copy_(flags.to(b.flat.device, non_blocking=True))
         if self.world > 1:
             b.flat.mul_(1.0 / self.world)
         b.handle = dist.all_reduce(b.flat, group=self.group, async_op=True)

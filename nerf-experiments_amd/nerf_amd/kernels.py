@@ -227,7 +227,7 @@ def encode_fwd(params: NerfPEParams, out_dim: int, *, x=None, xdir=None, ray_o=N
                 raise ValueError(f"{name} must be contiguous")
     out = torch.empty(n_samples, ld, device=device, dtype=torch.float32)
 
-    def fill():
+    def fill(out):
         end = None
         if TIMER is not None:
             # algorithmic bytes: the encoding's out_dim columns written, its inputs read once
@@ -260,16 +260,21 @@ def encode_fwd(params: NerfPEParams, out_dim: int, *, x=None, xdir=None, ray_o=N
             e.ray_d = _ptr(x)
             e.samples_per_ray, e.n_rays, e.per_ray = 1, n_samples, 1
         e.out, e.ld, e.out_dim = _ptr(out), ld, out_dim
-        out._nerf_deferred = DeferredEncoding(e, (x, ray_o, ray_d, t_start, t_end, pixel_width, out), fill)
+        # keep holds the inputs whose pointers the spec carries; NOT out itself (the tensor owns the
+        # spec: a reference back to it would be a cycle holding the rows' HBM until the cycle GC)
+        out._nerf_deferred = DeferredEncoding(e, (x, ray_o, ray_d, t_start, t_end, pixel_width), fill)
         return out
-    fill()
+    fill(out)
     return out
 
 
 class DeferredEncoding:
     """The pending rows of an encoding output: ``spec`` (nerf_fused_encoding: what the fused field
-    MLP needs to generate them in-kernel; its pointers stay valid through ``keep``) and ``fill`` (the
-    stand-alone encoding launch, for any other consumer)."""
+    MLP needs to generate them in-kernel; its input pointers stay valid through ``keep``, its output
+    pointer through the tensor that owns this object) and ``fill(out)`` (the stand-alone encoding
+    launch, for any other consumer).  Deferral is internal to NerfModel.render_raw /
+    render_composite → MLPFunction, which either hands the spec to the fused kernel or materializes
+    the rows first; any other reader must call ``materialize`` before touching the rows."""
 
     __slots__ = ("spec", "keep", "fill")
 
@@ -286,7 +291,7 @@ def materialize(t) -> None:
     d = deferred(t)
     if d is not None:
         t._nerf_deferred = None
-        d.fill()
+        d.fill(t)
 
 
 def mark_filled(t) -> None:

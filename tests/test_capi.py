@@ -50,6 +50,53 @@ def test_abi_version_and_status_strings():
     assert b"workspace" in lib.nerf_status_string(-4)
 
 
+def test_product_build_has_no_diagnostic_flags():
+    """VERDICT r3 #8: the shipped library was built with no NERF_*_DIAG_* ablation switch."""
+    from nerf_amd import _lib
+    assert _lib.load().nerf_build_flags() == 0
+
+
+def test_every_diagnostic_switch_is_reported():
+    """Every NERF_*_DIAG_* macro a kernel source tests is in common.h's list that feeds
+    nerf_build_flags (a new switch not listed there would ship unnoticed)."""
+    csrc = os.path.join(ROOT, "nerf-experiments_amd", "csrc")
+    common = open(os.path.join(csrc, "common.h")).read()
+    listed = set(re.findall(r"defined\((NERF_\w*DIAG\w*)\)", common))
+    used = set()
+    for f in os.listdir(csrc):
+        if f.endswith(".hip"):
+            used |= set(re.findall(r"\b(NERF_\w*_DIAG_\w+)\b", open(os.path.join(csrc, f)).read()))
+    assert used and used <= listed, sorted(used - listed)
+
+
+def test_load_refuses_a_diagnostic_build(tmp_path):
+    """A library with a unit compiled under a diagnostic switch (here capi.hip, the cheapest unit to
+    recompile, with NERF_FUSED_DIAG_NOSTORE; every unit reports through the same common.h macro)
+    returns bit 0 from nerf_build_flags and load() refuses it unless NERF_ALLOW_DIAG_BUILD=1."""
+    import subprocess
+    from nerf_amd import _lib
+    pkg = os.path.join(ROOT, "nerf-experiments_amd")
+    objs = [os.path.join(pkg, "build", f) for f in sorted(os.listdir(os.path.join(pkg, "build")))
+            if f.endswith(".o") and f != "capi.o"]
+    capi = tmp_path / "capi_diag.o"
+    base = ["/opt/rocm/bin/hipcc", "-O1", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
+            "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(pkg, "csrc")]
+    r = subprocess.run(base + ["-DNERF_FUSED_DIAG_NOSTORE", "-c", os.path.join(pkg, "csrc", "capi.hip"),
+                               "-o", str(capi)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lib = tmp_path / "libnerf_amd_diag.so"
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "-fPIC", "--offload-arch=gfx950", "-o", str(lib),
+                        *objs, str(capi)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    with pytest.raises(RuntimeError, match="diagnostic build"):
+        _lib.load(str(lib))
+    os.environ["NERF_ALLOW_DIAG_BUILD"] = "1"
+    try:
+        assert _lib.load(str(lib)).nerf_build_flags() == 1
+    finally:
+        del os.environ["NERF_ALLOW_DIAG_BUILD"]
+
+
 def test_struct_layouts_match_the_library():
     """Every argument struct of the binding has the C struct's size (load() checks it too)."""
     import ctypes
