@@ -6,7 +6,11 @@ the whole batch (rays are independent, the gradient mean is the onl
 ranks share the one GPU over gloo (the driver's multi-GPU runs use RCCL, one GPU per rank; the CPU
 suite's tests/test_ddp_direct.py covers the same protocol on the oracle forward).  Equidistant
 samples and the deterministic resample, so both runs see the same samples per ray; tolerance 1e-5
-of each gradient's scale (summation order)."""
+of each gradient's scale (summation order).  Two workloads: mip (C3's shared coarse / fine field)
+and barf (C4: per-image CameraExtrinsics refining the rays, whose rotation / translation
+gradients come back through the ray-mode encoding backward and pose_rays_bwd and are all-reduced
+through the post-accumulate-grad hooks beside the MLP's direct buckets;
+barf/model_camera_extrinsics.py:77-85, barf/model_barf.py:29-92)."""
 import os
 import sys
 import tempfile
@@ -22,46 +26,71 @@ PKG = os.path.join(ROOT, "nerf-experiments_amd")
 B = 512
 
 
-def _setup(dev):
+def _setup(dev, workload="mip"):
+    """(modules whose parameters are reduced, loss of a ray slice)."""
     from nerf_amd import BarfPositionalEncoding, IntegratedBarfFourierFeatures, NerfInterpolation, NerfModel
     torch.manual_seed(0)
-    pos = IntegratedBarfFourierFeatures(10, 10, 1.28, 6.4, True, 1.0, True)
-    pos.pixel_width_sigma = 0.0
-    dirs = BarfPositionalEncoding(4, 4, 1.28, 6.4, True, 1.0)
-    model = NerfModel(4, 256, True, False, 2, pos, dirs, 5e-4, 1e-4, 200000)
-    ren = NerfInterpolation(2.0, 8.0, model, 128, "equidistant", 0.0, "middle", model, 64).to(dev)
     g = torch.Generator().manual_seed(3)
     o = (torch.randn(B, 3, generator=g) * 0.2 + torch.tensor([0.0, 0.0, 4.0])).to(dev)
     d = torch.nn.functional.normalize(torch.randn(B, 3, generator=g) * 0.2 - torch.tensor([0.0, 0.0, 1.0]),
                                       dim=1).to(dev)
     pw = torch.full((B,), 1 / 1111.1, device=dev)
     c = torch.rand(B, 3, generator=g).to(dev)
-    return ren, o, d, pw, c
+    if workload == "mip":
+        pos = IntegratedBarfFourierFeatures(10, 10, 1.28, 6.4, True, 1.0, True)
+        pos.pixel_width_sigma = 0.0
+        dirs = BarfPositionalEncoding(4, 4, 1.28, 6.4, True, 1.0)
+        model = NerfModel(4, 256, True, False, 2, pos, dirs, 5e-4, 1e-4, 200000)
+        ren = NerfInterpolation(2.0, 8.0, model, 128, "equidistant", 0.0, "middle", model, 64).to(dev)
+
+        def loss(sl):
+            return ren.training_loss(o[sl], d[sl], pw[sl], c[sl])[0]
+        return [ren], loss
+    # barf (bench.py --workload barf): coarse-to-fine masked PE mid-schedule, 128 equidistant
+    # samples, rays refined by the per-image extrinsics of 16 views
+    from nerf_amd.model_camera_extrinsics import CameraExtrinsics
+    pos = BarfPositionalEncoding(10, 10.0, 0, 1, True, 1.0)
+    dirs = BarfPositionalEncoding(4, 4.0, 0, 1, True, 1.0)
+    pos.update_alpha(0.55)
+    dirs.update_alpha(0.55)
+    model = NerfModel(4, 256, True, False, 2, pos, dirs, 5e-4, 1e-5, 200000)
+    ren = NerfInterpolation(2.0, 8.0, model, 128, "equidistant", 0.0, "middle").to(dev)
+    extr = CameraExtrinsics(16, 1e-3, 1e-5, 200000).to(dev)
+    with torch.no_grad():
+        extr.rotation.copy_(torch.randn(extr.rotation.shape, generator=g) * 0.02)
+        extr.translation.copy_(torch.randn(extr.translation.shape, generator=g) * 0.02)
+    img = torch.randint(0, 16, (B,), generator=g).to(dev)
+
+    def loss(sl):
+        o2, d2, _, _ = extr(img[sl], o[sl], d[sl])
+        return ren.training_loss(o2, d2, pw[sl], c[sl])[0]
+    return [ren, extr], loss
 
 
-def _grads(ren, o, d, pw, c, sl):
+def _grads(modules, loss, sl):
     from nerf_amd.ddp import BucketedGradAllReduce
-    ar = BucketedGradAllReduce(list(ren.parameters()), direct=True)
+    params = [p for m in modules for p in m.parameters()]
+    ar = BucketedGradAllReduce(params, direct=True)
     try:
-        loss, _ = ren.training_loss(o[sl], d[sl], pw[sl], c[sl])
-        loss.backward()
+        loss(sl).backward()
         ar.finish()
         torch.cuda.synchronize()
-        return {n: p.grad.detach().cpu().clone() for n, p in ren.named_parameters() if p.grad is not None}
+        return {f"{i}.{n}": p.grad.detach().cpu().clone() for i, m in enumerate(modules)
+                for n, p in m.named_parameters() if p.grad is not None}
     finally:
         ar.remove()
 
 
-def _worker(rank, world, init_file, out_file):
+def _worker(rank, world, init_file, out_file, workload):
     sys.path.insert(0, PKG)
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method="file://" + init_file, rank=rank, world_size=world)
     try:
         torch.set_float32_matmul_precision("high")
         dev = torch.device("cuda", 0)
-        ren, o, d, pw, c = _setup(dev)
+        modules, loss = _setup(dev, workload)
         n = B // world
-        g = _grads(ren, o, d, pw, c, slice(rank * n, (rank + 1) * n))
+        g = _grads(modules, loss, slice(rank * n, (rank + 1) * n))
         if rank == 0:
             torch.save(g, out_file)
         dist.barrier()
@@ -69,19 +98,22 @@ def _worker(rank, world, init_file, out_file):
         dist.destroy_process_group()
 
 
-def test_two_ranks_equal_the_whole_batch():
+@pytest.mark.parametrize("workload", ["mip", "barf"])
+def test_two_ranks_equal_the_whole_batch(workload):
     with tempfile.TemporaryDirectory() as tmp:
         init_file, out_file = os.path.join(tmp, "rdzv"), os.path.join(tmp, "g.pt")
-        mp.spawn(_worker, args=(2, init_file, out_file), nprocs=2, join=True)
+        mp.spawn(_worker, args=(2, init_file, out_file, workload), nprocs=2, join=True)
         dp = torch.load(out_file, weights_only=True)
     prev = torch.get_float32_matmul_precision()
     torch.set_float32_matmul_precision("high")
     try:
-        ren, o, d, pw, c = _setup(torch.device("cuda", 0))
-        ref = _grads(ren, o, d, pw, c, slice(0, B))
+        modules, loss = _setup(torch.device("cuda", 0), workload)
+        ref = _grads(modules, loss, slice(0, B))
     finally:
         torch.set_float32_matmul_precision(prev)
     assert dp.keys() == ref.keys() and len(ref) > 0
+    if workload == "barf":
+        assert any(k.startswith("1.") for k in ref)          # the camera extrinsics were reduced
     for n in ref:
         scale = ref[n].abs().max().clamp_min(1e-30)
         assert (dp[n] - ref[n]).abs().max() <= 1e-5 * scale, n
