@@ -463,7 +463,8 @@ def _roofline(ks_fn: dict, x3: bool, steps: int, workload: str):
     # HIP kernel functions as rocprofv3 names them (template instantiations separately: the fused
     # kernel's forward is mlp_fused_kernel<0>, its input-gradient chain mlp_fused_kernel<1>)
     mfma_fns = ("mlp_fused_kernel<0>", "mlp_fused_kernel<1>", "linear_nt_x3_glds_kernel", "linear_nt_x3_kernel",
-                "linear_wgrad_x3_stream_kernel", "linear_wgrad_x3_kernel", "linear_nt_kernel", "linear_wgrad_kernel")
+                "linear_wgrad_x3_tr_kernel", "linear_wgrad_x3_stream_kernel", "linear_wgrad_x3_kernel", "linear_nt_kernel",
+                "linear_wgrad_kernel")
     cands = [k for k in mfma_fns if k in ks_fn]
     if not cands:
         return None

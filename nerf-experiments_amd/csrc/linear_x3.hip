@@ -1249,6 +1249,331 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     }
 }
 
+// ------------------------------------------------------------------- TN register-staged, transposed reads
+// The same 256 x 256 weight-gradient tile as linear_wgrad_x3_stream_kernel (one workgroup per M
+// split, dY and X read from HBM once, 16-sample MFMA steps in sample order, lo*hi + hi*lo + hi*hi on
+// v_mfma_f32_32x32x16_bf16: slabs bitwise equal), with the operand stream rebuilt around what the
+// hardware does fastest (tools/stream_bench.hip, profiles/r04b): plain nontemporal
+// global_load_dwordx4 rows into VGPRs stream 1 GB at 6.45-6.6 TB/s after the forward's writes,
+// where the LDS-DMA ring of the stream kernel reads the same rows at 4.2-4.4 TB/s.
+//
+// Waves 0-3 load dY rows 4w .. 4w + 3 of a step, waves 4-7 the X rows; lane l holds columns
+// 4l .. 4l + 3 of each (one coalesced 1 KB row per wave-instruction), two steps ahead of the step
+// being converted.  Each lane splits its own 16 values into bf16 hi / lo and writes them ROW-major
+// ([op][hi|lo][16 samples][256 columns], 64-byte blocks XOR-permuted by row & 3) with ds_write_b64;
+// the MFMA operands, which need 8 consecutive SAMPLES per lane, come back through
+// ds_read_b64_tr_b16 (the gfx950 transposed read; MI355X guide T10) — no raw ring, no column reads,
+// no DMA.  Per step: 32 KB of image, two stages (64 KB of LDS); both conflict-free.
+// Bias gradients, the 257th row (NerfModel's density + feature layer) and the per-ray dY sums of the
+// colour layer come from per-wave partials over the wave's rows, added in a fixed order (same values
+// as the stream kernel up to fp32 summation order).
+constexpr int WT_T = 16;                          // samples per step
+constexpr int WT_IMG = 4 * WT_T * 512;            // image stage: [op][hi | lo][16 rows][256 cols] bf16
+constexpr int WT_RS = 4 * 256 * 4;                // per-ray partials of the 4 dY waves
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4_t;
+
+// byte offset of columns col .. col + 3 (8-byte aligned) of image row `row` of plane (op, pl)
+__device__ __forceinline__ unsigned wt_off(int op, int pl, int row, int col) {
+    return (unsigned)(((op * 2 + pl) * WT_T + row) * 512 + ((2 * col) ^ ((row & 3) << 6)));
+}
+
+typedef const __attribute__((address_space(1))) float* wt_gfp;
+// source of relative row `rel` of the split (rows past its end read its first row): block 1 (rows
+// >= M0) from s1 / ld1 / rd1, block 0 from s0 / ld0 / rd0
+__device__ __forceinline__ wt_gfp wt_src_row(wt_gfp s0, wt_gfp s1, int64_t ld0, int64_t ld1, unsigned rd0,
+                                             unsigned rd1, bool rd_one, int M0, int mbeg, int mend, int rel) {
+    int m = mbeg + rel;
+    m = m < mend ? m : mbeg;
+    const bool b1 = m >= M0;                                // wave-uniform
+    const unsigned r = (unsigned)(b1 ? m - M0 : m);
+    const unsigned rr = rd_one ? r : r / (b1 ? rd1 : rd0);
+    return (b1 ? s1 : s0) + (int64_t)rr * (b1 ? ld1 : ld0);
+}
+
+template <bool ROW257, bool RAYS>
+__global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void linear_wgrad_x3_tr_kernel(
+    TNArgs a, int npad, int kpad) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * WT_IMG + (RAYS ? 2 * WT_RS : 0)];
+    // every argument the loop uses in registers (a lambda reading the by-value argument through a
+    // reference puts it in scratch), global pointers in the global address space (flat loads would
+    // share lgkmcnt with the LDS traffic)
+    typedef wt_gfp gfp;
+    typedef const __attribute__((address_space(1))) f4* gf4p;
+    const int split = blockIdx.x;
+    const int mbeg = split * a.m_per_split;
+    const int mend = min(mbeg + a.m_per_split, a.M);
+    const int M0 = a.M0, N = a.N;
+    const gfp dY0 = (gfp)a.dY, dY1 = (gfp)a.dY1;
+    const int64_t lddy0 = a.lddy, lddy1 = a.lddy1;
+    const int rs_S0 = a.rs_S0, rs_S1 = a.rs_S1, rs_B0 = a.rs_B0;
+    float* const raysum = a.raysum;
+    const int steps = mbeg < mend ? (mend - mbeg + WT_T - 1) / WT_T : 0;
+    const int t = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
+    const int op = wave >> 2;                 // this wave loads and converts 0: dY rows, 1: X rows
+    const int lr = 4 * (wave & 3);            // its first row of each step
+
+    // ---- this lane's source columns 4 lane .. 4 lane + 3 (segments span multiples of 32 columns);
+    // invalid columns read column 0 of the operand (finite data) and are zeroed when converted
+    gfp s0, s1;
+    int64_t ld0, ld1;
+    unsigned rd0 = 1, rd1 = 1, cmask = 0;
+    if (op == 0) {
+        const int nval = N < 256 ? N : 256;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cmask |= (4 * lane + e < nval ? 1u : 0u) << e;
+        const int col = 4 * lane < nval ? 4 * lane : 0;
+        s0 = dY0 + col;
+        s1 = dY1 + col;
+        ld0 = lddy0;
+        ld1 = lddy1;
+    } else {
+        int xs = -1, xoff = 0;
+#pragma unroll
+        for (int q = 0; q < MAX_SEGS; ++q)
+            if (q < a.X.n && 4 * lane >= a.X.koff[q] && 4 * lane < a.X.koff[q] + a.X.kp[q]) {
+                xs = q;
+                xoff = 4 * lane - a.X.koff[q];
+            }
+        const int kk = xs >= 0 ? pick4(a.X.k, xs) : 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cmask |= (xoff + e < kk ? 1u : 0u) << e;
+        const bool ok = cmask != 0;
+        s0 = (gfp)(ok ? pick4(a.X.ptr, xs) + xoff : a.X.ptr[0]);
+        ld0 = ok ? pick4(a.X.ld, xs) : a.X.ld[0];
+        rd0 = ok ? (unsigned)pick4(a.X.row_div, xs) : (unsigned)a.X.row_div[0];
+        s1 = (gfp)(ok ? pick4(a.x1ptr, xs) + xoff : a.x1ptr[0]);
+        ld1 = ok ? pick4(a.x1ld, xs) : a.x1ld[0];
+        rd1 = ok ? (unsigned)pick4(a.x1rd, xs) : (unsigned)a.x1rd[0];
+    }
+    // one source row per sample in every lane of the wave (the row divisor is the per-ray input's,
+    // absent from this kernel's layers in practice): no per-lane division
+    const bool rd_one = __ballot(rd0 != 1u || rd1 != 1u) == 0;
+    // (rows are computed by free functions of values: through a lambda's captures `b1 ? x : y`
+    // becomes a select of the captured variables' addresses, which keeps them in scratch)
+#define WT_SRC_ROW(i, q) wt_src_row(s0, s1, ld0, ld1, rd0, rd1, rd_one, M0, mbeg, mend, (i) * WT_T + lr + (q))
+#define WT_YD_ROW(i, q) wt_src_row(dY0 + 256, dY1 + 256, lddy0, lddy1, 1u, 1u, true, M0, mbeg, mend, (i) * WT_T + lr + (q))
+    f4 ra[4], rb[4];                          // the two register stages: steps in flight
+    float ya[4], yb[4];
+    auto issue = [&](int i, f4 (&r)[4], float (&y)[4]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) r[q] = __builtin_nontemporal_load((gf4p)WT_SRC_ROW(i, q));
+        if constexpr (ROW257) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) y[q] = *WT_YD_ROW(i, q);
+        }
+    };
+
+    // ---- per-wave partial sums (fixed order: rows of the wave in sample order)
+    f4 dbp = {0.f, 0.f, 0.f, 0.f};            // dY waves: bias gradient of columns 4 lane ..
+    f4 rp = {0.f, 0.f, 0.f, 0.f};             // dY waves: the current ray's dY sums
+    f4 dacc = {0.f, 0.f, 0.f, 0.f};           // X waves (ROW257): dW[256][4 lane ..]
+    float dbx = 0.f;                          // X waves (ROW257): db[256]
+    int pend_ray = -1;                        // a ray whose partials wait in rs[pend_ray & 1]
+    char* const rs = smem + 2 * WT_IMG;
+
+    // image offsets of this lane's row writes
+    unsigned woff[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) woff[q] = wt_off(op, 0, lr + q, 4 * lane);
+
+    const bool cols_full = __ballot(cmask != 0xfu) == 0;   // wave-uniform: no padded column in the wave
+    auto convert = [&](int i, const f4 (&r)[4], const float (&y)[4]) __attribute__((always_inline)) {
+        const int valid = mend - (mbeg + i * WT_T);          // rows of step i inside the split
+        char* const img = smem + (i & 1) * WT_IMG;
+        f4 rv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rv[q] = r[q];
+        if (!(cols_full && valid >= WT_T)) {                 // padded columns or the split's last rows
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const unsigned rm = lr + q < valid ? cmask : 0u;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    rv[q][e] = __builtin_bit_cast(float, __builtin_bit_cast(int, rv[q][e]) &
+                                                             __builtin_amdgcn_sbfe((int)rm, (unsigned)e, 1u));
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const f4 v = rv[q];
+            if (op == 0) {
+                dbp += v;
+                if constexpr (RAYS) rp += v;
+            } else if constexpr (ROW257) {
+                const float yq = lr + q < valid ? y[q] : 0.f;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) dacc[e] = __builtin_fmaf(yq, v[e], dacc[e]);
+                dbx += yq;
+            }
+            typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            typedef unsigned u2 __attribute__((ext_vector_type(2)));
+            u2 h, l;
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp) {
+                const f2 x2 = {v[2 * pp], v[2 * pp + 1]};
+                const unsigned hp = __builtin_bit_cast(unsigned, __builtin_convertvector(x2, bf16x2));
+                const f2 hv = {__builtin_bit_cast(float, hp << 16), __builtin_bit_cast(float, hp & 0xffff0000u)};
+                h[pp] = hp;
+                l[pp] = __builtin_bit_cast(unsigned, __builtin_convertvector(x2 - hv, bf16x2));
+            }
+            *reinterpret_cast<u2*>(img + woff[q]) = h;
+            *reinterpret_cast<u2*>(img + woff[q] + WT_T * 512) = l;
+        }
+        if constexpr (RAYS) {
+            if (op == 0 && valid > 0) {
+                // rays end at step ends (16 | S; ray starts and splits at multiples of 128 rows)
+                const int last = mbeg + i * WT_T + (valid < WT_T ? valid : WT_T) - 1;
+                const bool b1 = last >= M0;
+                const int rel = b1 ? last - M0 : last;
+                const int S = b1 ? rs_S1 : rs_S0;
+                if ((rel + 1) % S == 0) {
+                    const int ray = (b1 ? rs_B0 : 0) + rel / S;
+                    *reinterpret_cast<f4*>(rs + (ray & 1) * WT_RS + ((wave & 3) * 256 + 4 * lane) * 4) = rp;
+                    rp = f4{0.f, 0.f, 0.f, 0.f};
+                }
+            }
+        }
+    };
+    // the ray completed in the previous step: its 4 wave partials, added in wave order, to raysum
+    auto flush_ray = [&]() __attribute__((always_inline)) {
+        if constexpr (RAYS) {
+            if (pend_ray >= 0 && op == 0) {
+                const int c = 64 * (wave & 3) + lane;
+                const float* p = reinterpret_cast<const float*>(rs + (pend_ray & 1) * WT_RS);
+                const float s = ((p[c] + p[256 + c]) + p[512 + c]) + p[768 + c];
+                if (c < N) raysum[(size_t)pend_ray * N + c] = s;
+            }
+        }
+    };
+    // the ray (if any) whose last rows are in step i
+    auto ray_of_step = [=](int i) __attribute__((always_inline)) {
+        const int valid = mend - (mbeg + i * WT_T);
+        if (valid <= 0) return -1;
+        const int last = mbeg + i * WT_T + (valid < WT_T ? valid : WT_T) - 1;
+        const bool b1 = last >= M0;
+        const int rel = b1 ? last - M0 : last;
+        const int S = b1 ? rs_S1 : rs_S0;
+        return (rel + 1) % S == 0 ? (b1 ? rs_B0 : 0) + rel / S : -1;
+    };
+
+    // ---- MFMA role: wave (wr, wc) owns dW rows wr*128 .. +127 (4 x 32) and columns wc*64 .. +63 (2 x 32)
+    const int wr = wave >> 2, wc = wave & 3;
+    const bool active = wc * 64 < a.X.ktot && wr * 128 < N;
+    // transposed-read addresses: lane 4q + p of 16-lane group G supplies row 8 (G >> 1) + q (+ 4 for
+    // the fragment's second half), columns c0 + 16 (G & 1) + 4 p of the 32-column block c0
+    const int G = lane >> 4, qq = (lane & 15) >> 2, pq = lane & 3;
+    unsigned ya_off[4], xa_off[2];
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) ya_off[ii] = wt_off(0, 0, 8 * (G >> 1) + qq, wr * 128 + 32 * ii + 16 * (G & 1) + 4 * pq);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) xa_off[j] = wt_off(1, 0, 8 * (G >> 1) + qq, wc * 64 + 32 * j + 16 * (G & 1) + 4 * pq);
+    auto frag = [&](const char* img, unsigned off) __attribute__((always_inline)) {
+        const s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(img + off));
+        const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(img + off + 4 * 512));
+        return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    auto mfma_step = [&](int i) __attribute__((always_inline)) {
+        const char* img = smem + (i & 1) * WT_IMG;
+        bf16x8 xh[2], xl[2], yh[4], yl[4];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            xh[j] = frag(img, xa_off[j]);
+            xl[j] = frag(img, xa_off[j] + WT_T * 512);
+        }
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+            yh[ii] = frag(img, ya_off[ii]);
+            yl[ii] = frag(img, ya_off[ii] + WT_T * 512);
+        }
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[ii][j] = mfma_x3(yh[ii], yl[ii], xh[j], xl[j], acc[ii][j]);
+    };
+    auto barrier = []() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS writes / reads done
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    if (steps > 0) {
+        // prologue: steps 0 and 1 in flight, step 0 converted, step 2 issued
+        issue(0, ra, ya);
+        issue(1, rb, yb);
+        convert(0, ra, ya);
+        issue(2, ra, ya);
+        if constexpr (RAYS) pend_ray = op == 0 ? ray_of_step(0) : -1;
+        barrier();
+        // iteration i: convert step i + 1 (landed: issued two iterations ago), refill its registers
+        // with step i + 3, multiply step i; unrolled by two so the register stages are compile-time
+        // (loads past the last step re-read the split's first rows and conversions past it fill a
+        // stage nobody reads, masked to zero: no branch around them, so the counted waits are exact)
+        int i = 0;
+        for (; i + 1 < steps; i += 2) {
+            convert(i + 1, rb, yb);
+            issue(i + 3, rb, yb);
+            flush_ray();
+            if constexpr (RAYS) pend_ray = op == 0 ? ray_of_step(i + 1) : -1;
+            if (active) mfma_step(i);
+            barrier();
+            convert(i + 2, ra, ya);
+            issue(i + 4, ra, ya);
+            flush_ray();
+            if constexpr (RAYS) pend_ray = i + 2 < steps && op == 0 ? ray_of_step(i + 2) : -1;
+            if (active) mfma_step(i + 1);
+            barrier();
+        }
+        if (i < steps) {                       // odd step count: the last step, converted already
+            flush_ray();
+            if constexpr (RAYS) pend_ray = -1;
+            if (active) mfma_step(i);
+            barrier();
+        }
+        flush_ray();
+    }
+
+    float* slab = a.slab + (size_t)split * npad * kpad;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int k = wc * 64 + j * 32 + (lane & 31);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int n = wr * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                if (n < npad && k < kpad) slab[(size_t)n * kpad + k] = acc[i][j][r];
+            }
+        }
+    // per-wave partials through LDS (the image stages are free: the loop ended on a barrier), added
+    // in wave order
+    float* red = reinterpret_cast<float*>(smem);          // [4 dY waves][256] | [4 X waves][256]
+    *reinterpret_cast<f4*>(red + (op * 4 + (wave & 3)) * 256 + 4 * lane) = op == 0 ? dbp : dacc;
+    if (ROW257 && op == 1 && lane == 0) red[2048 + (wave & 3)] = dbx;
+    __syncthreads();
+    if (t < 256) {
+        const float s = ((red[t] + red[256 + t]) + red[512 + t]) + red[768 + t];
+        if (t < npad) a.db_slab[(size_t)split * npad + t] = s;
+    } else if (ROW257) {
+        const int c = t - 256;
+        const float* x = red + 1024;
+        slab[(size_t)256 * kpad + c] = ((x[c] + x[256 + c]) + x[512 + c]) + x[768 + c];
+        if (c == 0)
+            a.db_slab[(size_t)split * npad + 256] = ((red[2048] + red[2049]) + red[2050]) + red[2051];
+    }
+#undef WT_SRC_ROW
+#undef WT_YD_ROW
+}
+
 // ------------------------------------------------------------------- TN small N
 // Weight gradient of a layer with few outputs (N <= 16: the colour head's last Linear(128, 3 or 4),
 // barf/model_interpolation_architecture.py:88-92), where the tile kernels would run a 128-row MFMA
@@ -1543,6 +1868,12 @@ static const bool SMALLN_ON = [] {
     return !(e && e[0] == '0');
 }();
 
+// NERF_WGRAD_TR=0: the single-tile layers on the LDS-DMA stream kernel (A/B switch, read once)
+static const bool WGRAD_TR = [] {
+    const char* e = getenv("NERF_WGRAD_TR");
+    return !(e && e[0] == '0');
+}();
+
 static int wgrad_x3_rows_impl(const float* dY, int64_t ld_dy, const nerf_seg* segs, int64_t M0,
                               const float* dY1, int64_t ld_dy1, const nerf_seg* segs1, int64_t M1,
                               int32_t n_segs, int32_t N, void* workspace, size_t workspace_bytes,
@@ -1611,9 +1942,16 @@ static int wgrad_x3_rows_impl(const float* dY, int64_t ld_dy, const nerf_seg* se
         }
     }
     if ((N > 128 || L.ktot > 128) && N <= 257 && L.ktot <= 256) {   // one 256 x 256 tile (+ row 256)
-        const int64_t blocks = splits;
-        hipLaunchKernelGGL((linear_wgrad_x3_stream_kernel<3, 2>), dim3((unsigned)blocks), dim3(512), 0,
-                           as_stream(stream), a, ntn * TB, ntk * TB);
+        const dim3 grid((unsigned)splits), block(512);
+        hipStream_t st = as_stream(stream);
+        if (WGRAD_TR) {
+            // register-staged rows, transposed LDS reads (linear_wgrad_x3_tr_kernel)
+            if (N > 256) hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<true, false>), grid, block, 0, st, a, ntn * TB, ntk * TB);
+            else if (raysum) hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<false, true>), grid, block, 0, st, a, ntn * TB, ntk * TB);
+            else hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<false, false>), grid, block, 0, st, a, ntn * TB, ntk * TB);
+        } else {
+            hipLaunchKernelGGL((linear_wgrad_x3_stream_kernel<3, 2>), grid, block, 0, st, a, ntn * TB, ntk * TB);
+        }
         NERF_CHECK_LAUNCH();
         return NERF_OK;
     }

@@ -9,6 +9,7 @@ synchronisation happens anywhere in this module.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Sequence
 
 import torch
@@ -508,6 +509,12 @@ def linear_gauss_x3(segs, M: int, Wx: torch.Tensor, ldw: int, N: int, out: torch
     return True
 
 
+# the single-tile layers' weight-gradient kernel the library runs (NERF_WGRAD_TR=0: the LDS-DMA stream
+# kernel; the same switch is read by the library), for the timer's per-function grouping
+WGRAD_TILE_FN = ("linear_wgrad_x3_stream_kernel" if os.environ.get("NERF_WGRAD_TR", "1") == "0"
+                 else "linear_wgrad_x3_tr_kernel")
+
+
 def linear_wgrad_x3(dY: torch.Tensor, N4: int, segs, M: int, workspace: torch.Tensor) -> None:
     """Split-precision weight-gradient slabs (nerf_linear_wgrad_x3).  N4 is the row count: rounded
     up to 4 over a padded dY, or the true count (257: one 256 x 256 tile + a vector-ALU row); the
@@ -519,7 +526,7 @@ def linear_wgrad_x3(dY: torch.Tensor, N4: int, segs, M: int, workspace: torch.Te
     kpad = sum(pad32(k) for _, k, _ in segs)
     wide = (N4 > 128 or kpad > 128) and N4 <= 257 and kpad <= 256
     end = TIMER.bracket("linear_wgrad_x3", 2.0 * M * N4 * kt, 4.0 * M * N4 + _segs_bytes(segs, M) + 4.0 * N4 * kt,
-                        fn="linear_wgrad_x3_stream_kernel" if wide else
+                        fn=WGRAD_TILE_FN if wide else
                         ("linear_wgrad_smalln_kernel" if N4 <= 16 else "linear_wgrad_x3_kernel")) \
         if TIMER is not None else None
     st = _lib.load().nerf_linear_wgrad_x3(_ptr(dY), dY.stride(0), N4, arr, len(segs), M, _ptr(workspace),
@@ -542,7 +549,7 @@ def linear_wgrad_x3_rows(blocks, N4: int, workspace: torch.Tensor) -> None:
     wide = (N4 > 128 or kpad > 128) and N4 <= 257 and kpad <= 256
     end = TIMER.bracket("linear_wgrad_x3", 2.0 * (M + M1) * N4 * kt,
                         4.0 * (M + M1) * N4 + _segs_bytes(segs, M) + _segs_bytes(segs1, M1) + 4.0 * N4 * kt,
-                        fn="linear_wgrad_x3_stream_kernel" if wide else
+                        fn=WGRAD_TILE_FN if wide else
                         ("linear_wgrad_smalln_kernel" if N4 <= 16 else "linear_wgrad_x3_kernel")) \
         if TIMER is not None else None
     st = _lib.load().nerf_linear_wgrad_x3_rows(_ptr(dY), dY.stride(0), a0, M, _ptr(dY1), dY1.stride(0), a1, M1,
@@ -563,7 +570,7 @@ def linear_wgrad_x3_rays(blocks, N4: int, workspace: torch.Tensor, raysum: torch
         raise ValueError("linear_wgrad_x3_rays: raysum must be contiguous [rays, N4]")
     end = TIMER.bracket("linear_wgrad_x3", 2.0 * (M + M1) * N4 * kt,
                         4.0 * (M + M1) * N4 + _segs_bytes(segs, M) + _segs_bytes(segs1, M1) + 4.0 * N4 * kt
-                        + 4.0 * raysum.numel(), fn="linear_wgrad_x3_stream_kernel") \
+                        + 4.0 * raysum.numel(), fn=WGRAD_TILE_FN) \
         if TIMER is not None else None
     st = _lib.load().nerf_linear_wgrad_x3_rays(_ptr(dY), dY.stride(0), a0, M, _ptr(dY1), dY1.stride(0), a1, M1,
                                                len(segs), N4, _ptr(workspace),

@@ -26,7 +26,8 @@ sys.path.insert(0, ROOT)
 from bench import evidence_tag  # noqa: E402
 
 FNS = ("mlp_fused_kernel<0>", "mlp_fused_kernel<1>", "linear_nt_x3_glds_kernel", "linear_nt_x3_kernel", "linear_wgrad_smalln_kernel",
-       "linear_wgrad_x3_stream_kernel", "linear_wgrad_x3_kernel", "linear_nt_kernel", "linear_wgrad_kernel",
+       "linear_wgrad_x3_tr_kernel", "linear_wgrad_x3_stream_kernel", "linear_wgrad_x3_kernel", "linear_nt_kernel",
+       "linear_wgrad_kernel",
        "hashgrid_bwd_kernel", "hashgrid_fwd_kernel")
 
 
