@@ -520,6 +520,35 @@ def _hbm_roofline(ks, hbm_bytes, hbm_ms, hbm_gbs, steps):
             "bytes_per_step": hbm_bytes / steps}
 
 
+MALL_GATHER_GBS = 8600.0   # MI355X_MICROARCH.md "Indexed rows": random rows of a 38 MB table (Infinity Cache)
+
+
+def _gather_roofline(ks_fn: dict, steps: int, workload: str):
+    """The hash-grid kernels (C5) against the rate of the cache level their 7.2 MB table lives in:
+    larger than one XCD's 4 MB L2, far smaller than the 256 MB Infinity Cache (MALL), whose random-row
+    gather rate the guide measures at 8.6 TB/s chip-wide.  achieved = algorithmic bytes per launch
+    (8 corners x F fp32 gathered + F fp32 written per (sample, level); the backward:
+    F fp32 read + 8 corners x F 8-byte fixed-point adds) / the launch's event-timed duration."""
+    out = {}
+    for fn in ("hashgrid_fwd_level_kernel", "hashgrid_fwd_kernel", "hashgrid_bwd_kernel"):
+        r = ks_fn.get(fn)
+        if not r or r["ms"] <= 0:
+            continue
+        gbs = r["bytes"] / (r["ms"] * 1e-3) / 1e9
+        entry = {"bound": "mall", "achieved": gbs, "peak": MALL_GATHER_GBS, "unit": "GB/s",
+                 "frac": gbs / MALL_GATHER_GBS, "avg_launch_us": r["ms"] * 1e3 / max(r["launches"], 1),
+                 "avg_bytes_per_launch": r["bytes"] / max(r["launches"], 1),
+                 "launches_per_step": r["launches"] / steps, "ms_per_step": r["ms"] / steps}
+        for kind in ("traffic", "pmc"):
+            f = os.path.join(ROOT, "profiles", f"{kind}_{evidence_tag(workload, fn)}.json")
+            if os.path.exists(f):
+                with open(f) as fh:
+                    d = json.load(fh)
+                entry[kind] = d.get("bytes_per_launch") if kind == "traffic" else d
+        out[fn] = entry
+    return out or None
+
+
 def frame_roofline(ren, wl: dict, device, H: int = 800, W: int = 800, reps: int = 3):
     """HBM roofline of the same positional-encoding and compositing kernels at ONE full-frame
     launch: H*W rays (800 x 800: the C3 view size) x the workload's coarse and fine sample counts,
@@ -568,6 +597,39 @@ def frame_roofline(ren, wl: dict, device, H: int = 800, W: int = 800, reps: int 
                       "(%d rays x %s samples; algorithmic bytes per launch)" % (H, W, B, "/".join(map(str, counts))),
             "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
             "per_kernel": per}
+
+
+def frame_render(ren, wl: dict, device, name: str, H: int = 800, W: int = 800):
+    """One full H x W view rendered the way the reference's image logger does it
+    (barf/image_logger.py:155-214 through NerfInterpolation.render_image: batches of 65 536 rays
+    through forward, clip to [0, 1]) — the C3 frame render.  Reports its rate and which kernels it
+    launched: with the fused compositing no positional-encoding or compositing kernel runs (the
+    encodings are generated and the rays composited inside nerf_mlp_fused_render)."""
+    from nerf_amd import kernels as K
+    if not hasattr(ren, "render_image"):
+        return None
+    B = H * W
+    o, d, pw, _, _ = synthetic_batch_lego(B, 4242, device, W)
+    pw = pw.view(B, 1)
+    ren.render_image(o[:65536], d[:65536], pw[:65536])      # warm-up
+    torch.cuda.synchronize()
+    timer, prev = K.KernelTimer(), K.TIMER
+    K.TIMER = timer
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    rgb = ren.render_image(o, d, pw)
+    e.record()
+    K.TIMER = prev
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e)
+    ks = timer.summary()
+    spr = wl["coarse"] + wl["fine"]
+    return {"view": f"{H}x{W} ({B} rays x {spr} samples), batches of 65536 rays through forward, clip to [0, 1]",
+            "ms": ms, "ray_samples_per_s": B * spr / (ms * 1e-3),
+            "launches": {k: v["launches"] for k, v in ks.items()},
+            "encode_launches": ks.get("encode_fwd", {}).get("launches", 0),
+            "composite_launches": ks.get("composite_fwd", {}).get("launches", 0),
+            "mean_rgb": float(rgb.mean().item())}
 
 
 def init_distributed(backend: str = "nccl"):
@@ -798,6 +860,7 @@ def main():
                               "encode_launches_per_step": 0.0, "composite_launches_per_step": 0.0,
                               "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": None, "us_per_step": 0.0, "bytes_per_step": 0.0}),
+            "roofline_gather": _gather_roofline(ks_fn, args.steps, args.workload),
             "kernels": {k: {"launches_per_step": v["launches"] / args.steps, "ms_per_step": v["ms"] / args.steps,
                             "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["ms"] > 0 else 0.0,
                             "gbs": (v["bytes"] / (v["ms"] * 1e-3) / 1e9) if v["ms"] > 0 else 0.0}
@@ -810,8 +873,18 @@ def main():
             ("mean_rgb" if render else "final_loss"): final_loss,
         }
         if world == 1 and not args.no_frame_roofline:
-            try:          # an auxiliary measurement: its failure must not cost the bench line
-                out["roofline_hbm_frame"] = frame_roofline(ren, wl, device)
+            try:          # auxiliary measurements: their failure must not cost the bench line
+                out["frame_render"] = frame_render(ren, wl, device, args.workload)
+            except Exception as e:      # noqa: BLE001
+                out["frame_render"] = {"error": f"{type(e).__name__}: {e}"}
+            try:
+                fr = frame_roofline(ren, wl, device)
+                if fr is not None:
+                    fr["scope"] = ("the stand-alone encoding / compositing kernels, which neither the C3 training "
+                                   "step nor its frame render (frame_render) launches: they serve samples-per-ray "
+                                   "counts that do not divide the fused tile (3d-ingp's 256-sample fine pass), "
+                                   "matmul precision 'highest' and GARF's nerfacc-style rendering")
+                out["roofline_hbm_frame"] = fr
             except Exception as e:      # noqa: BLE001
                 out["roofline_hbm_frame"] = {"error": f"{type(e).__name__}: {e}"}
         if world == 1 and not args.no_cpu_baseline and not render:

@@ -22,6 +22,8 @@
 // 64-bit fixed-point integer at a scale 2^s chosen from the batch's max |g| so that no table entry
 // can overflow, and added with integer atomics; integer addition is associative, so the result is
 // independent of the order in which the atomics land (deterministic, unlike float atomics).
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -135,6 +137,50 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(HashArgs a, const flo
         if (f < F) o[f] = acc[f];
 }
 
+// The same features with the threads of a wave on ONE level and 64 consecutive samples (grid y =
+// level): a wave's gathers all hit one level's table and, along a ray, neighbouring cells (at the
+// coarse levels the same rows), instead of 16 tables per 16 threads; each thread writes its F
+// features of one row (rows of a sample complete in L2 from the levels' waves).  Bitwise the
+// kernel above (same per-level arithmetic).
+__global__ __launch_bounds__(256) void hashgrid_fwd_level_kernel(HashArgs a, const float* __restrict__ table,
+                                                                 float* __restrict__ out, int64_t ld) {
+#pragma clang fp contract(off)
+    const int F = a.p.features, T = a.p.table_size;
+    const int l = blockIdx.y;
+    const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (n >= a.n) return;
+    float p[3];
+    sample_position(a, n, p);
+    const Corners c = level_corners(p, a.p, a.p.res[l], T);
+    const float* tab = table + a.off[l] * F;
+    float acc[NERF_HASHGRID_MAX_FEATURES];
+#pragma unroll
+    for (int f = 0; f < NERF_HASHGRID_MAX_FEATURES; ++f) acc[f] = 0.0f;
+    if (F == 2) {
+        // the 8 rows' feature pairs as 8-byte loads, all issued before the sums
+        float2 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float2*>(tab + (int64_t)c.idx[k] * 2);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            acc[0] = acc[0] + c.w[k] * v[k].x;
+            acc[1] = acc[1] + c.w[k] * v[k].y;
+        }
+        *reinterpret_cast<float2*>(out + n * ld + (int64_t)l * 2) = make_float2(acc[0], acc[1]);
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+#pragma unroll
+        for (int f = 0; f < NERF_HASHGRID_MAX_FEATURES; ++f)
+            if (f < F) acc[f] = acc[f] + c.w[k] * tab[(int64_t)c.idx[k] * F + f];
+    }
+    float* o = out + n * ld + (int64_t)l * F;
+#pragma unroll
+    for (int f = 0; f < NERF_HASHGRID_MAX_FEATURES; ++f)
+        if (f < F) o[f] = acc[f];
+}
+
 // max |grad_out| over the batch as the bits of a non-negative float (order-preserving as uint32);
 // non-finite values land above every finite one
 template <int V>
@@ -198,7 +244,12 @@ __device__ __forceinline__ int fixed_shift(unsigned gmax_bits, int64_t n) {
 // atomics.  Global atomics scattered one lane per row run ~17x below their contiguous rate (they
 // execute at the memory side, one request per lane), so the scattered adds stay on chip and only
 // coalesced ones leave it; positions and corners are recomputed per part (cheap VALU).
-constexpr int PART_ENTRIES = 16384;                 // 128 KiB of int64 per workgroup
+#ifndef NERF_HG_PART_ENTRIES
+#define NERF_HG_PART_ENTRIES 20480
+#endif
+// all 160 KiB of LDS as int64 accumulators (16384: 8 parts per hashed level of 2^16 rows x 2
+// features, 20480: 7 — every part re-walks its slab's samples, so fewer parts is less work)
+constexpr int PART_ENTRIES = NERF_HG_PART_ENTRIES;
 constexpr int BWD_THREADS = 1024;
 
 struct BwdPlan {
@@ -382,9 +433,20 @@ extern "C" int nerf_hashgrid_fwd(const nerf_hashgrid_params* params, const float
                                   (params->query == 0 || t_end)));
     if (n_samples == 0) return NERF_OK;
     const HashArgs a = make_args(params, x, ray_o, ray_d, t_start, t_end, n_samples, samples_per_ray);
-    const int64_t threads = n_samples * params->levels;
-    hipLaunchKernelGGL(hashgrid_fwd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
-                       as_stream(stream), a, table, out, out_ld);
+    static const bool by_level = [] {
+        const char* e = getenv("NERF_HG_FWD_LEVEL");
+        return !(e && e[0] == '0');
+    }();
+    const bool f2_aligned = params->features != 2 || ((reinterpret_cast<uintptr_t>(out) & 7) == 0 && out_ld % 2 == 0 &&
+                                                      (reinterpret_cast<uintptr_t>(table) & 7) == 0);
+    if (by_level && f2_aligned && (n_samples + 255) / 256 < (1ll << 31)) {
+        hipLaunchKernelGGL(hashgrid_fwd_level_kernel, dim3((unsigned)((n_samples + 255) / 256), (unsigned)params->levels),
+                           dim3(256), 0, as_stream(stream), a, table, out, out_ld);
+    } else {
+        const int64_t threads = n_samples * params->levels;
+        hipLaunchKernelGGL(hashgrid_fwd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                           as_stream(stream), a, table, out, out_ld);
+    }
     NERF_CHECK_LAUNCH();
     return NERF_OK;
 }

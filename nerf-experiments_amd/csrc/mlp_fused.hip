@@ -34,6 +34,8 @@
 #include <stddef.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "common.h"
 #include "encode_common.h"
 #include "composite_common.h"
@@ -248,6 +250,42 @@ __device__ __forceinline__ void dma_seek(Ctx& c, int l) {
 // ones repeat pieces, and past the end of the stream the last chunk is fetched again), so that the
 // count of vector-memory ops in a chunk is the same on every path
 constexpr int DMA_PER_WAVE = 2 * KBMAX / NWAVE;
+// NERF_FUSED_WREG (default 1): the same pieces by plain buffer loads into VGPRs at the chunk start
+// and ds_write_b128 into the ring slot at the chunk end, instead of LDS-DMA.  A DMA piece costs its
+// wave 60-185 issue cycles beside MFMAs and LDS reads (MI355X_MICROARCH.md, LDS-DMA issue cost), a
+// load + ds_write_b128 pair ~17; the 8 VGPRs fit under the two-waves-per-SIMD budget.
+#ifndef NERF_FUSED_WREG
+#define NERF_FUSED_WREG 1
+#endif
+__device__ __forceinline__ void dma_advance(Ctx& c) {
+    if (c.d_remaining > 1) {
+        c.d_off += c.d_units * 1024;
+        if (--c.d_left == 0) dma_seek(c, __builtin_amdgcn_readlane(c.t_next, c.d_layer));
+        --c.d_remaining;
+    }
+}
+#if NERF_FUSED_WREG
+// the next register-fed chunk's pieces of this wave into registers (unit u of piece i: the DMA's)
+__device__ __forceinline__ void wload(Ctx& c, bf16x8 (&w)[DMA_PER_WAVE], unsigned (&dst)[DMA_PER_WAVE]) {
+#pragma unroll
+    for (int i = 0; i < DMA_PER_WAVE; ++i) {
+        const int u = (c.wave + NWAVE * i) & (c.d_units - 1);
+        asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(w[i])
+                     : "v"((unsigned)(c.lane * 16 + c.d_off + u * 1024)), "s"(c.rimg));
+        dst[i] = (unsigned)(u * 1024 + c.lane * 16);
+    }
+    dma_advance(c);
+}
+// ... and into ring slot `slot` once landed (N younger vector-memory ops may still be in flight)
+template <int N>
+__device__ __forceinline__ void wwrite(Ctx& c, int slot, bf16x8 (&w)[DMA_PER_WAVE], const unsigned (&dst)[DMA_PER_WAVE]) {
+    static_assert(DMA_PER_WAVE == 2, "wwrite waits for two pieces");
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(w[0]), "+v"(w[1]) : "n"(N));
+    char* base = c.smem + slot * SLOT_BYTES;
+#pragma unroll
+    for (int i = 0; i < DMA_PER_WAVE; ++i) *reinterpret_cast<bf16x8*>(base + dst[i]) = w[i];
+}
+#endif
 __device__ __forceinline__ void issue_dma(Ctx& c, int slot) {
     char* dst = c.smem + slot * SLOT_BYTES;
 #ifndef NERF_FUSED_NODMA          // diagnostic builds only: time the kernel without its weight stream
@@ -260,11 +298,7 @@ __device__ __forceinline__ void issue_dma(Ctx& c, int slot) {
 #else
     (void)dst;
 #endif
-    if (c.d_remaining > 1) {
-        c.d_off += c.d_units * 1024;
-        if (--c.d_left == 0) dma_seek(c, __builtin_amdgcn_readlane(c.t_next, c.d_layer));
-        --c.d_remaining;
-    }
+    dma_advance(c);
 }
 
 // Arguments of the shared encoding math (encode_common.h) for a generated segment: the encoding's
@@ -501,7 +535,7 @@ __device__ __forceinline__ void pair_stores(const Ctx& c, const LayerState& st, 
     va = lo8 ? x : ry;
     vb = lo8 ? rx : y;
     const int cl = lo8 ? ch - 1 : ch;                 // the chunk this lane writes in both stores
-    const bool inr = 16 * cl < colok;
+    const bool inr = cl >= 0 && 16 * cl < colok;
     oa = inr ? pa + 64u * (unsigned)cl : OOB;
     ob = inr ? pb + 64u * (unsigned)cl : OOB;
 }
@@ -511,7 +545,10 @@ __device__ __forceinline__ void pair_stores(const Ctx& c, const LayerState& st, 
 // dropped), in four parts placed between the next chunk's MFMA stages: 0 / 1 = the values of column
 // block 0 / 1 (FWD: bias + ReLU; DGRAD: times the ReLU bits) and their fp32 stores; 2 = ReLU mask
 // bits (FWD); 3 = the hi/lo split into the LDS image of the next layer's operand.
-template <int MODE>
+// EPAR: the parity of chunk ch when the caller knows it at compile time (the chunk loop unrolled by
+// two: 0 even, 1 odd — ch = -1, the nonexistent predecessor of chunk 0, comes in the odd slot with
+// every store dropped), -1: decided at run time
+template <int MODE, int EPAR = -1>
 __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, f4 (&a)[SB], f4 b) {
 #ifdef NERF_FUSED_NOEPI           // diagnostic builds only (timing without the chunk epilogues)
     return;
@@ -537,7 +574,7 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
                 v[r] = __builtin_bit_cast(float, max(__builtin_bit_cast(int, v[r] + b[r]), st.floor_i));
             if (ch >= 0 && ch == st.col_chunk) c.sig[sb] = v[0];   // (the raw density, for fused compositing)
 #if NERF_FUSED_PAIR >= 2
-            if (!pair_odd(ch)) {
+            if (EPAR >= 0 ? EPAR == 0 : !pair_odd(ch)) {
                 // even chunk: held for the pair (alone if it is the layer's last); the column output
                 // (col_idx is a multiple of 32: always an even chunk)
                 st.stash[sb] = v;
@@ -550,8 +587,8 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
 #if NERF_FUSED_PAIR >= 3
                 // the pair's two half lines of every sample back to back (the even chunk's from the stash):
                 // no lane exchange, the halves reach L2 together
-                const unsigned oa = 16 * (ch - 1) < st.colok ? st.row_off[sb] + 64u * (unsigned)(ch - 1) : OOB;
-                const unsigned ob = 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
+                const unsigned oa = ch > 0 && 16 * (ch - 1) < st.colok ? st.row_off[sb] + 64u * (unsigned)(ch - 1) : OOB;
+                const unsigned ob = ch >= 0 && 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
                 __builtin_amdgcn_raw_buffer_store_b128(st.stash[sb], st.ro, oa, 0, ST_AUX);
                 __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, ob, 0, ST_AUX);
 #else
@@ -603,7 +640,7 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
             st.pa[sb] = st.pb[sb] = st.pa2[sb] = st.pb2[sb] = st.row_off[sb] = st.row_off2[sb] = OOB;
 #endif
 #if NERF_FUSED_PAIR
-            if (!pair_odd(ch)) {
+            if (EPAR >= 0 ? EPAR == 0 : !pair_odd(ch)) {
                 // even chunk: held for the pair (alone if it is the layer's last); n1 is even, so
                 // both chunks of a pair go to the same output
                 st.stash[sb] = v;
@@ -702,6 +739,11 @@ __host__ __device__ constexpr int epi_placed() {                 // parts placed
     return KBR - EPI0 < EPI_NP ? (KBR - EPI0 > 0 ? KBR - EPI0 : 0) : EPI_NP;
 }
 
+// the chunk loop of the layers with a register-fed part unrolled by two (compile-time pair parity)
+#ifndef NERF_FUSED_UNROLL2
+#define NERF_FUSED_UNROLL2 1
+#endif
+
 // the first layer's weight fragments one chunk ahead by builtin loads (0: the asm loads + vmcnt(0))
 #ifndef NERF_FUSED_L0_PREFETCH
 #define NERF_FUSED_L0_PREFETCH 1
@@ -730,7 +772,7 @@ __device__ __forceinline__ void first_reads(bf16x8 (&fr)[FA][2], unsigned sa) {
 
 // One 16-row chunk's register-fed k-blocks (compile-time KB_I: immediate LDS offsets), fragments
 // read FA steps ahead; the previous chunk's epilogue parts 0-2 at stages EPI0 .. EPI0 + 2.
-template <int MODE, int KBR, int KBH, int KB_I>
+template <int MODE, int KBR, int KBH, int KB_I, int EPAR = -1>
 __device__ __forceinline__ void reg_steps(Ctx& c, LayerState& st, unsigned sa, bf16x8 (&fr)[FA][2], f4 (&a)[SB],
                                           f4 (&pv)[SB], f4& pb, int ch) {
     constexpr int EPI0 = KBR >= 8 ? 4 : (KBR >= 4 ? 1 : 0);
@@ -757,9 +799,9 @@ __device__ __forceinline__ void reg_steps(Ctx& c, LayerState& st, unsigned sa, b
         // measured slower: chain 3.78 -> 4.03-4.09 ms, forward 3.86 -> 3.94-4.00 per mip step)
         if constexpr (KB_I == EPI0) bias_wait<(KBR > 0 ? DMA_PER_WAVE : 0) + 2 * KBH>(pb);
         if constexpr (KB_I >= EPI0 && KB_I < EPI0 + epi_placed<KBR, EPI0>())
-            epi_part<MODE>(c, st, epi_part_of(KB_I - EPI0), ch - 1, pv, pb);
+            epi_part<MODE, EPAR>(c, st, epi_part_of(KB_I - EPI0), ch - 1, pv, pb);
         __builtin_amdgcn_sched_barrier(0);
-        reg_steps<MODE, KBR, KBH, KB_I + 1>(c, st, sa, fr, a, pv, pb, ch);
+        reg_steps<MODE, KBR, KBH, KB_I + 1, EPAR>(c, st, sa, fr, a, pv, pb, ch);
     }
 }
 
@@ -946,7 +988,10 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
         }
     } else
 #endif
-    for (int ch = 0; ch < NC; ++ch) {
+    {
+    // one chunk; EP: the compile-time parity of its predecessor (whose epilogue it runs)
+    auto chunk = [&](int ch, auto ep_tag) __attribute__((always_inline)) {
+        constexpr int EP = decltype(ep_tag)::value;
         // the previous chunk's biases (rows 4 g .. 4 g + 3), for its epilogue in this chunk, issued
         // before this chunk's DMA so that waiting for it does not wait for the DMA
         f4 pb;
@@ -956,7 +1001,19 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
             buf_load16(pb, st.bias_off, c.rimg);     // (zero biases: the load only keeps the count)
         const unsigned sa = lds_addr(c.smem + c.cur * SLOT_BYTES + c.lane * 16);
         bf16x8 fr[FA][2];
+#if NERF_FUSED_WREG
+        bf16x8 wr[DMA_PER_WAVE];
+        unsigned wdst[DMA_PER_WAVE];
+#endif
         if constexpr (KBR > 0) {
+#if NERF_FUSED_WREG
+            // this chunk's pieces were written at the end of the previous register-fed chunk (LDS
+            // ops complete in order; the barrier's lgkmcnt(0) covers them); the other slot is free
+            barrier();
+            first_reads<KBR, 0>(fr, sa);
+            wload(c, wr, wdst);                      // the next register-fed chunk, a whole chunk ahead
+            __builtin_amdgcn_sched_barrier(0);      // keep the loads ahead of this chunk's vmem ops (vmcnt)
+#else
             // this chunk's DMA share has landed (issued at the start of the previous register-fed
             // chunk and followed by >= AFTER_DMA_VM vector-memory ops), then everyone else's; the
             // other slot is free
@@ -967,6 +1024,7 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
             first_reads<KBR, 0>(fr, sa);
             issue_dma(c, c.cur ^ 1);                 // the next register-fed chunk, a whole chunk ahead
             __builtin_amdgcn_sched_barrier(0);      // keep the DMA ahead of this chunk's vmem ops (vmcnt)
+#endif
         }
         // this chunk's HBM-fed weight fragments, from L2
         bf16x8 hf[KBH > 0 ? KBH : 1][2];
@@ -978,7 +1036,7 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
         f4 a[SB];
 #pragma unroll
         for (int sb = 0; sb < SB; ++sb) a[sb] = f4{0.f, 0.f, 0.f, 0.f};
-        reg_steps<MODE, KBR, KBH, 0>(c, st, sa, fr, a, pv, pb, ch);
+        reg_steps<MODE, KBR, KBH, 0, EP>(c, st, sa, fr, a, pv, pb, ch);
         // the HBM-fed fragments have landed: with a register-fed part the 4 epilogue stores of parts
         // 0-1 were issued after them
 #pragma unroll
@@ -996,11 +1054,28 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
         if constexpr (KBR == 0) bias_wait<0>(pb);
         // the parts the stages did not take (all of them for the first layer)
 #pragma unroll
-        for (int i = epi_placed<KBR, EPI0>(); i < EPI_NP; ++i) epi_part<MODE>(c, st, epi_part_of(i), ch - 1, pv, pb);
-        if constexpr (!NERF_FUSED_P3S) epi_part<MODE>(c, st, 3, ch - 1, pv, pb);
+        for (int i = epi_placed<KBR, EPI0>(); i < EPI_NP; ++i) epi_part<MODE, EP>(c, st, epi_part_of(i), ch - 1, pv, pb);
+        if constexpr (!NERF_FUSED_P3S) epi_part<MODE, EP>(c, st, 3, ch - 1, pv, pb);
+#if NERF_FUSED_WREG
+        // the next chunk's pieces into the free slot (younger than their loads: the HBM-fed fragment
+        // loads, waited above, and the 2 SB epilogue stores of parts 0-1)
+        if constexpr (KBR > 0) wwrite<2 * SB>(c, c.cur ^ 1, wr, wdst);
+#endif
         if constexpr (KBR > 0) c.cur ^= 1;
 #pragma unroll
         for (int sb = 0; sb < SB; ++sb) pv[sb] = a[sb];
+    };
+#if NERF_FUSED_UNROLL2
+    // unrolled by two: chunk ch (even) runs the epilogue of the odd chunk ch - 1 (none for ch = 0:
+    // its stores are dropped), chunk ch + 1 that of the even chunk ch — the pair-store parity, the
+    // stash and the accumulator hand-over are compile-time, with no branch or register copy per chunk
+    for (int ch = 0; ch < NC; ch += 2) {
+        chunk(ch, std::integral_constant<int, 1>{});
+        if (ch + 1 < NC) chunk(ch + 1, std::integral_constant<int, 0>{});
+    }
+#else
+    for (int ch = 0; ch < NC; ++ch) chunk(ch, std::integral_constant<int, -1>{});
+#endif
     }
     {
         f4 lb;
@@ -1156,7 +1231,16 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
     const int l0 = next_ring_layer(c, 0);
     if (l0 >= 0) dma_seek(c, l0);
     c.cur = 0;
+#if NERF_FUSED_WREG
+    if (l0 >= 0) {
+        bf16x8 wr[DMA_PER_WAVE];
+        unsigned wdst[DMA_PER_WAVE];
+        wload(c, wr, wdst);
+        wwrite<0>(c, 0, wr, wdst);
+    }
+#else
     if (l0 >= 0) issue_dma(c, 0);
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the first chunk (the steady-state wait assumes predecessors)
     __syncthreads();
 #pragma unroll

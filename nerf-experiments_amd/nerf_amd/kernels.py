@@ -672,6 +672,12 @@ def _hashgrid_table_check(name: str, params, table: torch.Tensor) -> None:
                          f"(got {tuple(table.shape)})")
 
 
+# the forward kernel the library runs (NERF_HG_FWD_LEVEL=0: one thread per (sample, level) in
+# sample-major order; the same switch is read by the library)
+HASHGRID_FWD_FN = ("hashgrid_fwd_kernel" if os.environ.get("NERF_HG_FWD_LEVEL", "1") == "0"
+                   else "hashgrid_fwd_level_kernel")
+
+
 def hashgrid_fwd(params, table: torch.Tensor, out: torch.Tensor, *, x=None, ray_o=None, ray_d=None, t_start=None,
                  t_end=None, n_samples: int, samples_per_ray: int = 1) -> None:
     _hashgrid_table_check("table", params, table)
@@ -679,8 +685,9 @@ def hashgrid_fwd(params, table: torch.Tensor, out: torch.Tensor, *, x=None, ray_
     if out.dim() != 2 or out.stride(1) != 1 or out.shape[0] < n_samples or out.shape[1] < params.levels * params.features:
         raise ValueError("out must be a row-major [n, >= levels * features] tensor")
     _hashgrid_inputs(params, n_samples, x, ray_o, ray_d, t_start, t_end, samples_per_ray)
-    end = TIMER.bracket("hashgrid_fwd", 0.0, 8.0 * n_samples * params.levels * params.features * 8
-                        + 4.0 * n_samples * params.levels * params.features, fn="hashgrid_fwd_kernel") \
+    # algorithmic bytes: 8 corners x F fp32 gathered + F fp32 written per (sample, level)
+    end = TIMER.bracket("hashgrid_fwd", 0.0, 8.0 * n_samples * params.levels * params.features * 4
+                        + 4.0 * n_samples * params.levels * params.features, fn=HASHGRID_FWD_FN) \
         if TIMER is not None else None
     st = _lib.load().nerf_hashgrid_fwd(ctypes.byref(params), _ptr(x), _ptr(ray_o), _ptr(ray_d), _ptr(t_start),
                                        _ptr(t_end), n_samples, samples_per_ray, table.data_ptr(), out.data_ptr(),
@@ -708,6 +715,7 @@ def hashgrid_bwd(params, grad_out: torch.Tensor, grad_table: torch.Tensor, works
     if workspace.device != grad_out.device or not workspace.is_contiguous() \
             or workspace.numel() * workspace.element_size() < need or workspace.data_ptr() % 256:
         raise ValueError(f"workspace must be a contiguous, 256-byte aligned device buffer of >= {need} bytes")
+    # algorithmic work: F fp32 gradients read and 8 corners x F 8-byte fixed-point adds per (sample, level)
     end = TIMER.bracket("hashgrid_bwd", 0.0, 8.0 * n_samples * params.levels * params.features * 8
                         + 4.0 * n_samples * params.levels * params.features, fn="hashgrid_bwd_kernel") \
         if TIMER is not None else None

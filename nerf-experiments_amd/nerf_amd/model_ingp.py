@@ -357,7 +357,13 @@ class NaiveINGP(nn.Module):
         sample_dist = t_end - t
         if isinstance(model, NerfModel):
             # fused: positions o + t d generated in the encoding kernel, direction encoding once per
-            # ray, softplus(z - 1) / sigmoid applied in the compositor
+            # ray, softplus(z - 1) / sigmoid applied in the compositor — inside the field MLP's
+            # launches when the rays fill its tiles (the 64-sample coarse pass; the 256-sample fine
+            # pass takes the stand-alone compositing kernels, 0.07 ms of the C5 step)
+            if model.fused_composite_ok(batch_size * samples_per_ray, samples_per_ray):
+                rgb, weights = model.render_composite(ray_origs, ray_dirs, None, t, t_end, samples_per_ray, 0, 1,
+                                                      sample_dist, 1.0, 1.0)
+                return rgb, weights.unsqueeze(-1), sample_dist
             heads = model.render_raw(ray_origs, ray_dirs, None, t, t_end, samples_per_ray, 0, 1)
             rgb, weights = composite_raw(heads, sample_dist, batch_size, samples_per_ray, 1.0, 1.0)
             return rgb, weights.unsqueeze(-1), sample_dist

@@ -286,6 +286,23 @@ class NerfInterpolation(nn.Module):
         return {"optimizer": optimizer, "lr_scheduler": {"scheduler": lr_scheduler, "interval": "step",
                                                          "frequency": 1, "name": "le_nice_lr_scheduler"}}
 
+    @th.no_grad()
+    def render_image(self, ray_origs: th.Tensor, ray_dirs: th.Tensor, pixel_width: th.Tensor | float,
+                     batch_size: int = 65536) -> th.Tensor:
+        """A full view's colours [n_rays, 3] the way the reference's image logger renders it
+        (barf/image_logger.py:155-206: batches of rays through ``forward``, the fine rgb clipped to
+        [0, 1]), without its DataLoader / host round trips: the rays stay on the GPU, and every
+        batch whose rays fill the fused kernel's tiles goes through nerf_mlp_fused_render (the
+        encodings generated and the rays composited inside the field-MLP launch)."""
+        n = ray_origs.shape[0]
+        if not isinstance(pixel_width, th.Tensor):
+            pixel_width = th.full((n, 1), float(pixel_width), device=ray_origs.device)
+        out = th.empty(n, 3, device=ray_origs.device, dtype=th.float32)
+        for i in range(0, n, batch_size):
+            j = min(n, i + batch_size)
+            out[i:j] = self.forward(ray_origs[i:j], ray_dirs[i:j], pixel_width[i:j])[0].clip(0, 1)
+        return out
+
     def compute_psnr(self, loss: th.Tensor) -> float:
         try:
             if loss <= 1e-7:

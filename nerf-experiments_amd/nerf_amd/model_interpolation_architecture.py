@@ -173,7 +173,9 @@ class NerfModel(NerfBaseModel):
                                                    samples_per_ray, query, pw_mode, defer=FUSE_ENCODINGS)
         dir_pe = self.direction_encoder.encode_padded(ray_dirs, defer=FUSE_ENCODINGS)
         plan = self._get_plan()
-        comp = CompositeSpec(distances.contiguous().view(-1), samples_per_ray, scale_a, scale_b)
+        # (NerfModelINGP's density is softplus(z - 1): its DENSITY_SHIFT, applied by the compositor)
+        comp = CompositeSpec(distances.contiguous().view(-1), samples_per_ray, scale_a, scale_b,
+                             getattr(self, "DENSITY_SHIFT", 0.0))
         outs = MLPFunction.apply(plan, pos_pe.shape[0], pos_pe, dir_pe, samples_per_ray, *plan.params(),
                                  composite=comp)
         return outs[-2], outs[-1]
