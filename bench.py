@@ -530,7 +530,8 @@ def _gather_roofline(ks_fn: dict, steps: int, workload: str):
     (8 corners x F fp32 gathered + F fp32 written per (sample, level); the backward:
     F fp32 read + 8 corners x F 8-byte fixed-point adds) / the launch's event-timed duration."""
     out = {}
-    for fn in ("hashgrid_fwd_level_kernel", "hashgrid_fwd_kernel", "hashgrid_bwd_kernel"):
+    for fn in ("hashgrid_fwd_tile_kernel", "hashgrid_fwd_level_kernel", "hashgrid_fwd_kernel", "hashgrid_bwd_walk_kernel",
+               "hashgrid_bwd_kernel"):
         r = ks_fn.get(fn)
         if not r or r["ms"] <= 0:
             continue

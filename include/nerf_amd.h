@@ -46,7 +46,8 @@ extern "C" {
 #define NERF_ERR_WORKSPACE (-4)
 
 /* Library / ABI version (bumped on any signature or data-layout change; 6: NERF_FUSED_MASK;
- * 7: nerf_fused_composite / nerf_mlp_fused_render). */
+ * 7: nerf_fused_composite / nerf_mlp_fused_render; 8: nerf_hashgrid_workspace_n, fused compositing
+ * of 256-sample rays). */
 int nerf_abi_version(void);
 const char* nerf_status_string(int status);
 /* sizeof of the argument structs, for bindings to check their layouts against:
@@ -407,7 +408,8 @@ int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_layers, const v
 /* Alpha compositing fused into the field MLP (a4 inside a7: barf/model_interpolation.py:316-353 on
  * the heads of model_interpolation_architecture.py:128-141, replacing nerf_composite_fwd/bwd with
  * act = 1 for rays whose samples fill whole 128-sample tiles: 128 % S == 0, 16 <= S <= 128, with
- * 128 / S rays per tile and M = n_rays * S).
+ * 128 / S rays per tile, or S == 256, one ray per two tiles that one workgroup runs back to back;
+ * M = n_rays * S).
  *
  * Forward (the forward launch): at the end of every tile the waves hand their samples' raw heads
  * (rgb = rows 0..2 of layer head_layer, which has one 16-row chunk; sigma = the column output of
@@ -586,6 +588,12 @@ int nerf_hashgrid_fwd(const nerf_hashgrid_params* params, const float* x, const 
  * NaN.  workspace: nerf_hashgrid_workspace(params) bytes, 256-byte aligned; zeroed by the call
  * itself (no state is carried between calls). */
 size_t nerf_hashgrid_workspace(const nerf_hashgrid_params* params);
+/* (ABI 8) workspace for n_samples with grad_out restaged level-major: nerf_hashgrid_workspace(params)
+ * rounded up to 256 bytes, plus n_samples * levels * features fp32.  With a workspace of at least
+ * this size the call first copies grad_out level-major (one pass, with the max |g|) and the part
+ * walks read each level's values contiguously; a workspace of only nerf_hashgrid_workspace(params)
+ * bytes reads the [n][g_ld] rows in place.  Same result either way (bitwise). */
+size_t nerf_hashgrid_workspace_n(const nerf_hashgrid_params* params, int64_t n_samples);
 int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float* x, const float* ray_o,
                       const float* ray_d, const float* t_start, const float* t_end, int64_t n_samples,
                       int32_t samples_per_ray, const float* grad_out, int64_t g_ld, float* grad_table,

@@ -181,6 +181,50 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_level_kernel(HashArgs a, con
         if (f < F) o[f] = acc[f];
 }
 
+// The same features, 64 samples per workgroup with one wave per level (64 L threads): a wave's
+// gathers hit one level's table (at the coarse levels neighbouring samples of a ray share rows),
+// and the workgroup's results are staged in LDS and written as whole [64][ld] output rows — the
+// kernel above writes each 128-B row as 16 scattered 8-B pieces from 16 waves of the level grid,
+// which the caches cannot hold together (write amplification).  Bitwise the kernels above.
+constexpr int TILE_SAMPLES = 64;
+template <int F>
+__global__ __launch_bounds__(1024) void hashgrid_fwd_tile_kernel(HashArgs a, const float* __restrict__ table,
+                                                                 float* __restrict__ out, int64_t ld) {
+#pragma clang fp contract(off)
+    __shared__ float rows[TILE_SAMPLES * (16 * F + 1)];
+    const int L = a.p.levels, T = a.p.table_size, cols = L * F, rld = cols + 1;
+    const int l = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+    const int64_t n0 = (int64_t)blockIdx.x * TILE_SAMPLES;
+    const int64_t n = n0 + lane;
+    if (n < a.n) {
+        float p[3];
+        sample_position(a, n, p);
+        const Corners c = level_corners(p, a.p, a.p.res[l], T);
+        const float* tab = table + a.off[l] * F;
+        float v[8][F];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+            for (int f = 0; f < F; ++f) v[k][f] = tab[(int64_t)c.idx[k] * F + f];   // all 8 F loads first
+        float acc[F];
+#pragma unroll
+        for (int f = 0; f < F; ++f) acc[f] = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+            for (int f = 0; f < F; ++f) acc[f] = acc[f] + c.w[k] * v[k][f];
+#pragma unroll
+        for (int f = 0; f < F; ++f) rows[lane * rld + l * F + f] = acc[f];
+    }
+    __syncthreads();
+    const int64_t left = a.n - n0;
+    const int nr = left < TILE_SAMPLES ? (int)left : TILE_SAMPLES;
+    for (int e = threadIdx.x; e < nr * cols; e += blockDim.x) {
+        const int r = e / cols, cc = e - r * cols;
+        out[(n0 + r) * ld + cc] = rows[r * rld + cc];
+    }
+}
+
 // max |grad_out| over the batch as the bits of a non-negative float (order-preserving as uint32);
 // non-finite values land above every finite one
 template <int V>
@@ -224,6 +268,46 @@ __global__ __launch_bounds__(256) void hashgrid_gmax_kernel(const float* __restr
     }
 }
 
+// The max as above, and grad_out restaged level-major, gt[l][n][f] (the backward's part walks read
+// one level's F values per sample: from the [n][ld] rows that is 4 F bytes out of every 128-B line,
+// re-read by every part of the level; level-major they are contiguous).  64 rows per workgroup:
+// coalesced row reads into LDS, coalesced level-run writes out of it.
+template <int F>
+__global__ __launch_bounds__(256) void hashgrid_gtr_kernel(const float* __restrict__ g, int64_t ld, int64_t n, int L,
+                                                           float* __restrict__ gt, unsigned* __restrict__ gmax) {
+    __shared__ float rows[TILE_SAMPLES * (NERF_HASHGRID_MAX_LEVELS * F + 1)];
+    __shared__ unsigned wm[4];
+    const int cols = L * F, rld = cols + 1;
+    const int64_t n0 = (int64_t)blockIdx.x * TILE_SAMPLES;
+    const int nr = n - n0 < TILE_SAMPLES ? (int)(n - n0) : TILE_SAMPLES;
+    unsigned m = 0;
+    for (int e = threadIdx.x; e < nr * cols; e += 256) {
+        const int r = e / cols, c = e - r * cols;
+        const float v = g[(n0 + r) * ld + c];
+        rows[r * rld + c] = v;
+        const unsigned b = __float_as_uint(fabsf(v));
+        m = b > m ? b : m;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned o = __shfl_xor(m, off, 64);
+        m = o > m ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = wm[0] > wm[1] ? wm[0] : wm[1];
+        m = m > wm[2] ? m : wm[2];
+        m = m > wm[3] ? m : wm[3];
+        if (m != 0) atomicMax(gmax, m);
+    }
+    const int run = nr * F;                       // one level's values of the workgroup's rows
+    for (int e = threadIdx.x; e < L * run; e += 256) {
+        const int l = e / run, q = e - l * run;
+        const int r = q / F, f = q - r * F;
+        gt[((int64_t)l * n + n0) * F + q] = rows[r * rld + l * F + f];
+    }
+}
+
 // fixed-point exponent s with 8 * n * gmax * 2^s < 2^62 (no entry can overflow); -1000 flags a
 // non-finite gradient
 __device__ __forceinline__ int fixed_shift(unsigned gmax_bits, int64_t n) {
@@ -257,6 +341,7 @@ struct BwdPlan {
     int rows_per_part;
     int parts;                                      // parts of all levels (workgroups per slab)
     int64_t slab;                                   // samples per slab
+    int64_t nslab;                                  // slabs (the persistent walk's items: parts x nslab)
 };
 
 __host__ __device__ inline int64_t level_rows(int r, int T) {
@@ -269,38 +354,26 @@ __host__ __device__ inline int64_t level_rows(int r, int T) {
 // memory round trip instead of one per load.
 constexpr int BWD_UNROLL = 4;
 
+// One part's walk over the samples [n_begin, n_end): every corner contribution whose row falls in
+// the part [row0, row0 + prow) of level l, added to the LDS accumulators.  g: the level's F values of
+// sample n at gt[n F + f] when restaged level-major (gt != null), else at g[n ld + l F + f].
 template <int F>
-__global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_kernel(HashArgs a, BwdPlan pl, const float* __restrict__ g,
-                                                                   int64_t ld, const unsigned* __restrict__ gmax,
-                                                                   unsigned long long* __restrict__ acc) {
+__device__ __forceinline__ void walk_part(const HashArgs& a, int l, int res, int64_t row0, int prow, double scale,
+                                          int64_t n_begin, int64_t n_end, const float* __restrict__ g, int64_t ld,
+                                          const float* __restrict__ gt, unsigned long long* part) {
 #pragma clang fp contract(off)
-    __shared__ unsigned long long part[PART_ENTRIES];
     const int T = a.p.table_size;
-    const int w = (int)(blockIdx.x % (unsigned)pl.parts);
-    const int64_t slab = blockIdx.x / (unsigned)pl.parts;
-    int l = 0;
-    while (w >= pl.start[l + 1]) ++l;
-    const int res = a.p.res[l];
-    const int64_t row0 = (int64_t)(w - pl.start[l]) * pl.rows_per_part;
-    const int64_t rows = level_rows(res, T) - row0;
-    const int prow = (int)(rows < pl.rows_per_part ? rows : pl.rows_per_part);
-    const int s = fixed_shift(*gmax, a.n);
-    if (s == -1000) return;                         // uniform: the finish pass writes NaN
-    const double scale = ldexp(1.0, s);
-    for (int e = threadIdx.x; e < prow * F; e += BWD_THREADS) part[e] = 0ull;
-    __syncthreads();
     const bool rays = a.x == nullptr, mid = a.p.query != 0, small = a.n < ((int64_t)1 << 31);
-    const int64_t n1 = (slab + 1) * pl.slab < a.n ? (slab + 1) * pl.slab : a.n;
-    // samples past the slab are masked, their loads clamped into it
-    for (int64_t base = slab * pl.slab; base < n1; base += BWD_UNROLL * BWD_THREADS) {
+    // samples past the range are masked, their loads clamped into it
+    for (int64_t base = n_begin; base < n_end; base += BWD_UNROLL * BWD_THREADS) {
         const int64_t nb = base + threadIdx.x;
         float p[BWD_UNROLL][3], gv[BWD_UNROLL][F];
-        // loads first (indices clamped into the slab, so every load is in bounds) ...
+        // loads first (indices clamped into the range, so every load is in bounds) ...
         if (rays) {
             float t0[BWD_UNROLL], t1[BWD_UNROLL], o[BWD_UNROLL][3], d[BWD_UNROLL][3];
 #pragma unroll
             for (int u = 0; u < BWD_UNROLL; ++u) {
-                const int64_t n = nb + u * BWD_THREADS < n1 ? nb + u * BWD_THREADS : n1 - 1;
+                const int64_t n = nb + u * BWD_THREADS < n_end ? nb + u * BWD_THREADS : n_end - 1;
                 const int64_t ray = small ? (int64_t)((unsigned)n / (unsigned)a.spr) : n / a.spr;
                 t0[u] = a.t0[n];
                 t1[u] = mid ? a.t1[n] : 0.0f;
@@ -310,7 +383,7 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_kernel(HashArgs a, B
                     d[u][j] = a.d[ray * 3 + j];
                 }
 #pragma unroll
-                for (int f = 0; f < F; ++f) gv[u][f] = g[n * ld + (int64_t)l * F + f];
+                for (int f = 0; f < F; ++f) gv[u][f] = gt ? gt[n * F + f] : g[n * ld + (int64_t)l * F + f];
             }
             // ... then the positions, as sample_position computes them
 #pragma unroll
@@ -322,16 +395,16 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_kernel(HashArgs a, B
         } else {
 #pragma unroll
             for (int u = 0; u < BWD_UNROLL; ++u) {
-                const int64_t n = nb + u * BWD_THREADS < n1 ? nb + u * BWD_THREADS : n1 - 1;
+                const int64_t n = nb + u * BWD_THREADS < n_end ? nb + u * BWD_THREADS : n_end - 1;
 #pragma unroll
                 for (int j = 0; j < 3; ++j) p[u][j] = a.x[n * 3 + j];
 #pragma unroll
-                for (int f = 0; f < F; ++f) gv[u][f] = g[n * ld + (int64_t)l * F + f];
+                for (int f = 0; f < F; ++f) gv[u][f] = gt ? gt[n * F + f] : g[n * ld + (int64_t)l * F + f];
             }
         }
 #pragma unroll
         for (int u = 0; u < BWD_UNROLL; ++u) {
-            if (nb + u * BWD_THREADS >= n1) continue;
+            if (nb + u * BWD_THREADS >= n_end) continue;
             const Corners c = level_corners(p[u], a.p, res, T);
             // An LDS atomic costs the same per wave-instruction however few lanes are active, and a
             // part holds only ~1/parts of a sample's corners: so each lane queues its in-range
@@ -365,7 +438,12 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_kernel(HashArgs a, B
             }
         }
     }
-    __syncthreads();
+}
+
+// the part's accumulators out to the global ones: one contiguous pass of atomics
+template <int F>
+__device__ __forceinline__ void flush_part(const HashArgs& a, int l, int64_t row0, int prow,
+                                           const unsigned long long* part, unsigned long long* __restrict__ acc) {
     unsigned long long* dst = acc + (a.off[l] + row0) * F;
     for (int e = threadIdx.x; e < prow * F; e += BWD_THREADS) {
         const unsigned long long v = part[e];
@@ -373,10 +451,118 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_kernel(HashArgs a, B
     }
 }
 
+__device__ __forceinline__ void part_of(const HashArgs& a, const BwdPlan& pl, int w, int& l, int64_t& row0, int& prow) {
+    l = 0;
+    while (w >= pl.start[l + 1]) ++l;
+    row0 = (int64_t)(w - pl.start[l]) * pl.rows_per_part;
+    const int64_t rows = level_rows(a.p.res[l], a.p.table_size) - row0;
+    prow = (int)(rows < pl.rows_per_part ? rows : pl.rows_per_part);
+}
+
+// One workgroup per (part, slab) (NERF_HG_BWD_WALK=0).
 template <int F>
-void launch_bwd(int64_t blocks, hipStream_t s, const HashArgs& a, const BwdPlan& pl, const float* g, int64_t ld,
-                const unsigned* gmax, unsigned long long* acc) {
-    hipLaunchKernelGGL(hashgrid_bwd_kernel<F>, dim3((unsigned)blocks), dim3(BWD_THREADS), 0, s, a, pl, g, ld, gmax, acc);
+__global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_kernel(HashArgs a, BwdPlan pl, const float* __restrict__ g,
+                                                                   int64_t ld, const float* __restrict__ gt,
+                                                                   const unsigned* __restrict__ gmax,
+                                                                   unsigned long long* __restrict__ acc) {
+    __shared__ unsigned long long part[PART_ENTRIES];
+    const int w = (int)(blockIdx.x % (unsigned)pl.parts);
+    const int64_t slab = blockIdx.x / (unsigned)pl.parts;
+    int l, prow;
+    int64_t row0;
+    part_of(a, pl, w, l, row0, prow);
+    const int s = fixed_shift(*gmax, a.n);
+    if (s == -1000) return;                         // uniform: the finish pass writes NaN
+    const double scale = ldexp(1.0, s);
+    for (int e = threadIdx.x; e < prow * F; e += BWD_THREADS) part[e] = 0ull;
+    __syncthreads();
+    const int64_t n1 = (slab + 1) * pl.slab < a.n ? (slab + 1) * pl.slab : a.n;
+    walk_part<F>(a, l, a.p.res[l], row0, prow, scale, slab * pl.slab, n1, g, ld, gt ? gt + (int64_t)l * a.n * F : nullptr,
+                 part);
+    __syncthreads();
+    flush_part<F>(a, l, row0, prow, part, acc);
+}
+
+// Persistent form: one workgroup per CU walks a contiguous run of the (part, slab) items, part-major,
+// so that every workgroup gets the same number of slabs (the per-item grid ran ~4.2 waves of
+// workgroups: the last one 1/5 full) and keeps a part in LDS across its consecutive slabs (one flush
+// per part change, not one per item).
+template <int F>
+__global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_walk_kernel(HashArgs a, BwdPlan pl, const float* __restrict__ g,
+                                                                        int64_t ld, const float* __restrict__ gt,
+                                                                        const unsigned* __restrict__ gmax,
+                                                                        unsigned long long* __restrict__ acc) {
+    __shared__ unsigned long long part[PART_ENTRIES];
+    const int s = fixed_shift(*gmax, a.n);
+    if (s == -1000) return;                         // uniform: the finish pass writes NaN
+    const double scale = ldexp(1.0, s);
+    const int64_t items = (int64_t)pl.parts * pl.nslab;
+    const int64_t i0 = items * blockIdx.x / gridDim.x, i1 = items * (blockIdx.x + 1) / gridDim.x;
+    int cur = -1, l = 0, prow = 0;
+    int64_t row0 = 0;
+    for (int64_t i = i0; i < i1; ++i) {
+        const int w = (int)(i / pl.nslab);
+        const int64_t slab = i - (int64_t)w * pl.nslab;
+        if (w != cur) {
+            if (cur >= 0) {
+                __syncthreads();
+                flush_part<F>(a, l, row0, prow, part, acc);
+                __syncthreads();
+            }
+            cur = w;
+            part_of(a, pl, w, l, row0, prow);
+            for (int e = threadIdx.x; e < prow * F; e += BWD_THREADS) part[e] = 0ull;
+            __syncthreads();
+        }
+        const int64_t n0 = slab * pl.slab;
+        const int64_t n1 = n0 + pl.slab < a.n ? n0 + pl.slab : a.n;
+        if (n0 < n1)
+            walk_part<F>(a, l, a.p.res[l], row0, prow, scale, n0, n1, g, ld,
+                         gt ? gt + (int64_t)l * a.n * F : nullptr, part);
+    }
+    if (cur >= 0) {
+        __syncthreads();
+        flush_part<F>(a, l, row0, prow, part, acc);
+    }
+}
+
+template <int F>
+void launch_bwd(bool walk, int64_t blocks, hipStream_t s, const HashArgs& a, const BwdPlan& pl, const float* g, int64_t ld,
+                const float* gt, const unsigned* gmax, unsigned long long* acc) {
+    if (walk)
+        hipLaunchKernelGGL(hashgrid_bwd_walk_kernel<F>, dim3((unsigned)blocks), dim3(BWD_THREADS), 0, s, a, pl, g, ld, gt,
+                           gmax, acc);
+    else
+        hipLaunchKernelGGL(hashgrid_bwd_kernel<F>, dim3((unsigned)blocks), dim3(BWD_THREADS), 0, s, a, pl, g, ld, gt, gmax,
+                           acc);
+}
+
+template <int F>
+void launch_fwd_tile(hipStream_t s, const HashArgs& a, const float* table, float* out, int64_t ld) {
+    hipLaunchKernelGGL(hashgrid_fwd_tile_kernel<F>, dim3((unsigned)((a.n + TILE_SAMPLES - 1) / TILE_SAMPLES)),
+                       dim3(64 * a.p.levels), 0, s, a, table, out, ld);
+}
+
+template <int F>
+void launch_gtr(hipStream_t s, const float* g, int64_t ld, int64_t n, int L, float* gt, unsigned* gmax) {
+    hipLaunchKernelGGL(hashgrid_gtr_kernel<F>, dim3((unsigned)((n + TILE_SAMPLES - 1) / TILE_SAMPLES)), dim3(256), 0, s,
+                       g, ld, n, L, gt, gmax);
+}
+
+int env_mode(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return (e && e[0] >= '0' && e[0] <= '9') ? e[0] - '0' : dflt;
+}
+
+int num_cus() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+    }
+    return n;
 }
 
 // table gradient = accumulator * 2^-s (or NaN after a non-finite gradient)
@@ -433,19 +619,24 @@ extern "C" int nerf_hashgrid_fwd(const nerf_hashgrid_params* params, const float
                                   (params->query == 0 || t_end)));
     if (n_samples == 0) return NERF_OK;
     const HashArgs a = make_args(params, x, ray_o, ray_d, t_start, t_end, n_samples, samples_per_ray);
-    static const bool by_level = [] {
-        const char* e = getenv("NERF_HG_FWD_LEVEL");
-        return !(e && e[0] == '0');
-    }();
-    const bool f2_aligned = params->features != 2 || ((reinterpret_cast<uintptr_t>(out) & 7) == 0 && out_ld % 2 == 0 &&
-                                                      (reinterpret_cast<uintptr_t>(table) & 7) == 0);
-    if (by_level && f2_aligned && (n_samples + 255) / 256 < (1ll << 31)) {
-        hipLaunchKernelGGL(hashgrid_fwd_level_kernel, dim3((unsigned)((n_samples + 255) / 256), (unsigned)params->levels),
-                           dim3(256), 0, as_stream(stream), a, table, out, out_ld);
+    // NERF_HG_FWD: 2 (default) 64-sample tiles, one wave per level, whole output rows; 1 the level
+    // grid; 0 one thread per (sample, level) — bitwise the same features
+    static const int mode = env_mode("NERF_HG_FWD", 2);
+    const int F = params->features, L = params->levels;
+    const bool f2_aligned = F != 2 || ((reinterpret_cast<uintptr_t>(out) & 7) == 0 && out_ld % 2 == 0 &&
+                                       (reinterpret_cast<uintptr_t>(table) & 7) == 0);
+    hipStream_t st = as_stream(stream);
+    if (mode == 2 && L <= 16 && (F == 1 || F == 2 || F == 4) && (n_samples + TILE_SAMPLES - 1) / TILE_SAMPLES < (1ll << 31)) {
+        if (F == 1) launch_fwd_tile<1>(st, a, table, out, out_ld);
+        else if (F == 2) launch_fwd_tile<2>(st, a, table, out, out_ld);
+        else launch_fwd_tile<4>(st, a, table, out, out_ld);
+    } else if (mode >= 1 && f2_aligned && (n_samples + 255) / 256 < (1ll << 31)) {
+        hipLaunchKernelGGL(hashgrid_fwd_level_kernel, dim3((unsigned)((n_samples + 255) / 256), (unsigned)L),
+                           dim3(256), 0, st, a, table, out, out_ld);
     } else {
-        const int64_t threads = n_samples * params->levels;
-        hipLaunchKernelGGL(hashgrid_fwd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
-                           as_stream(stream), a, table, out, out_ld);
+        const int64_t threads = n_samples * L;
+        hipLaunchKernelGGL(hashgrid_fwd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, a, table,
+                           out, out_ld);
     }
     NERF_CHECK_LAUNCH();
     return NERF_OK;
@@ -459,6 +650,15 @@ extern "C" int64_t nerf_hashgrid_table_rows(const nerf_hashgrid_params* params, 
 extern "C" size_t nerf_hashgrid_workspace(const nerf_hashgrid_params* params) {
     if (!valid_params(params)) return 0;
     return 256 + (size_t)total_rows(params) * params->features * sizeof(unsigned long long);
+}
+
+namespace {
+size_t gt_offset(const nerf_hashgrid_params* params) { return (nerf_hashgrid_workspace(params) + 255) & ~(size_t)255; }
+}  // namespace
+
+extern "C" size_t nerf_hashgrid_workspace_n(const nerf_hashgrid_params* params, int64_t n_samples) {
+    if (!valid_params(params) || n_samples < 0) return 0;
+    return gt_offset(params) + (size_t)n_samples * params->levels * params->features * sizeof(float);
 }
 
 extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float* x, const float* ray_o,
@@ -481,15 +681,29 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
     const HashArgs a = make_args(params, x, ray_o, ray_d, t_start, t_end, n_samples, samples_per_ray);
     if (n_samples > 0) {
         const int cols = params->levels * params->features;
-        const bool vec = cols % 4 == 0 && g_ld % 4 == 0 && (reinterpret_cast<uintptr_t>(grad_out) & 15) == 0;
-        int64_t blocks = (n_samples * (vec ? cols / 4 : cols) + 255) / 256;
-        blocks = blocks < 1024 ? blocks : 1024;
-        if (vec)
-            hipLaunchKernelGGL(hashgrid_gmax_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, s, grad_out, g_ld,
-                               n_samples, cols, gmax);
-        else
-            hipLaunchKernelGGL(hashgrid_gmax_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, s, grad_out, g_ld,
-                               n_samples, cols, gmax);
+        // grad_out restaged level-major (with its max) when the workspace has room for it
+        // (nerf_hashgrid_workspace_n) and the walks read it (NERF_HG_BWD: 2 persistent walk over the
+        // restaged values, default; 1 the per-item grid over them; 0 the per-item grid on the rows)
+        static const int mode = env_mode("NERF_HG_BWD", 2);
+        const int F = params->features;
+        float* gt = nullptr;
+        if (mode >= 1 && workspace_bytes >= nerf_hashgrid_workspace_n(params, n_samples) && (F == 1 || F == 2 || F == 4) &&
+            (n_samples + TILE_SAMPLES - 1) / TILE_SAMPLES < (1ll << 31)) {
+            gt = reinterpret_cast<float*>(static_cast<char*>(workspace) + gt_offset(params));
+            if (F == 1) launch_gtr<1>(s, grad_out, g_ld, n_samples, params->levels, gt, gmax);
+            else if (F == 2) launch_gtr<2>(s, grad_out, g_ld, n_samples, params->levels, gt, gmax);
+            else launch_gtr<4>(s, grad_out, g_ld, n_samples, params->levels, gt, gmax);
+        } else {
+            const bool vec = cols % 4 == 0 && g_ld % 4 == 0 && (reinterpret_cast<uintptr_t>(grad_out) & 15) == 0;
+            int64_t blocks = (n_samples * (vec ? cols / 4 : cols) + 255) / 256;
+            blocks = blocks < 1024 ? blocks : 1024;
+            if (vec)
+                hipLaunchKernelGGL(hashgrid_gmax_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, s, grad_out, g_ld,
+                                   n_samples, cols, gmax);
+            else
+                hipLaunchKernelGGL(hashgrid_gmax_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, s, grad_out, g_ld,
+                                   n_samples, cols, gmax);
+        }
         NERF_CHECK_LAUNCH();
         BwdPlan pl{};
         pl.rows_per_part = PART_ENTRIES / params->features;
@@ -498,12 +712,28 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
             pl.start[l + 1] = pl.start[l] + (int)((rows + pl.rows_per_part - 1) / pl.rows_per_part);
         }
         pl.parts = pl.start[params->levels];
-        // about four workgroups per CU in all, slabs of at least 4096 samples
-        int64_t slabs = (1024 + pl.parts - 1) / pl.parts;
-        const int64_t most = (n_samples + 4095) / 4096;
-        slabs = slabs < most ? slabs : most;
-        pl.slab = (n_samples + slabs - 1) / slabs;
-        void (*launch)(int64_t, hipStream_t, const HashArgs&, const BwdPlan&, const float*, int64_t,
+        const bool walk = mode == 2 && gt != nullptr;
+        int64_t blocks;
+        if (walk) {
+            // ~16 slabs per CU-resident workgroup, slabs of at least one 4096-sample trip
+            const int64_t G = num_cus();
+            int64_t slabs = (16 * G + pl.parts - 1) / pl.parts;
+            const int64_t most = (n_samples + 4095) / 4096;
+            slabs = slabs < most ? slabs : most;
+            pl.slab = (n_samples + slabs - 1) / slabs;
+            pl.nslab = (n_samples + pl.slab - 1) / pl.slab;
+            const int64_t items = (int64_t)pl.parts * pl.nslab;
+            blocks = items < G ? items : G;
+        } else {
+            // about four workgroups per CU in all, slabs of at least 4096 samples
+            int64_t slabs = (1024 + pl.parts - 1) / pl.parts;
+            const int64_t most = (n_samples + 4095) / 4096;
+            slabs = slabs < most ? slabs : most;
+            pl.slab = (n_samples + slabs - 1) / slabs;
+            pl.nslab = slabs;
+            blocks = slabs * pl.parts;
+        }
+        void (*launch)(bool, int64_t, hipStream_t, const HashArgs&, const BwdPlan&, const float*, int64_t, const float*,
                        const unsigned*, unsigned long long*) = nullptr;
         switch (params->features) {
             case 1: launch = launch_bwd<1>; break;
@@ -515,7 +745,7 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
             case 7: launch = launch_bwd<7>; break;
             default: launch = launch_bwd<8>; break;
         }
-        launch(slabs * pl.parts, s, a, pl, grad_out, g_ld, gmax, acc);
+        launch(walk, blocks, s, a, pl, grad_out, g_ld, gt, gmax, acc);
         NERF_CHECK_LAUNCH();
     }
     int64_t fb = (count + 255) / 256;

@@ -108,6 +108,7 @@ struct FusedArgs {
     int n_layers;
     int M;
     int ntiles;
+    int span;          // tiles a workgroup runs back to back (2: rays of 256 samples), ntiles % span == 0
     int comp_on;       // forward: composite every tile's rays (nerf_mlp_fused_render)
     nerf_fused_composite comp;
 };
@@ -226,6 +227,9 @@ struct Ctx {
     // output and the interval length of the lane's samples (lanes g = 0)
     f4 head[SB];
     float sig[SB], cdist[SB];
+    // rays of two tiles (S = 256): the first tile's heads and interval lengths, held over the second
+    f4 phead[SB];
+    float pcdist[SB];
 };
 
 __device__ __forceinline__ int dma_units(Ctx& c, int l) { return LF(int, chunk_units, l); }
@@ -1123,8 +1127,15 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
 // 2 SB KB of its image and its image is not read back; every wave passed that layer's chunk barrier
 // after reading back its previous image, and a region is next written by its own wave (the next
 // tile's generated rows, then its first layer) after it has composited: one barrier suffices.
+// A ray of 256 samples spans two tiles, which one workgroup runs back to back (the tile loop walks
+// tile pairs): after the first the waves keep their samples' heads and interval lengths in
+// registers; after the second they hand both halves to wave 0, which composites the ray (4 samples
+// per lane) with the same routine.  Scratch layout: heads [s] 16 B at 0, interval lengths [s] at
+// COMP_DEL.
 constexpr int COMP_OFF = 8192;
-static_assert(COMP_OFF >= SB * 2048 && COMP_OFF + TILE * 20 <= XIMG_BYTES, "composite scratch");
+constexpr int COMP_SMAX = 2 * TILE;
+constexpr int COMP_DEL = COMP_SMAX * 16;
+static_assert(COMP_OFF >= SB * 2048 && COMP_OFF + COMP_SMAX * 20 <= XIMG_BYTES, "composite scratch");
 
 template <int R>
 __device__ __forceinline__ void composite_wave(Ctx& c, int64_t ray, int S) {
@@ -1138,7 +1149,7 @@ __device__ __forceinline__ void composite_wave(Ctx& c, int64_t ray, int S) {
         if (s < S) {
             const f4 h = *reinterpret_cast<const f4*>(reg + s * 16);
             rc[r][0] = h[0]; rc[r][1] = h[1]; rc[r][2] = h[2]; rd[r] = h[3];
-            del[r] = *reinterpret_cast<const float*>(reg + TILE * 16 + s * 4);
+            del[r] = *reinterpret_cast<const float*>(reg + COMP_DEL + s * 4);
         }
     }
     float w[R], rgb[3], cc[R][3], cs[R][3];
@@ -1171,6 +1182,35 @@ __device__ __forceinline__ void composite_wave(Ctx& c, int64_t ray, int S) {
 __device__ __forceinline__ void composite_tile(Ctx& c, int tile) {
     const int S = CF(int32_t, samples_per_ray);
     const bool col_sigma = CF(int32_t, sigma_layer) >= 0;
+    if (S > TILE) {
+        // S = 2 TILE: the ray of tiles (2 q, 2 q + 1); M % S == 0, so every sample is valid
+        if ((tile & 1) == 0) {
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) {
+                c.phead[sb] = c.head[sb];
+                if (col_sigma) c.phead[sb][3] = c.sig[sb];
+                c.pcdist[sb] = c.cdist[sb];
+            }
+            return;
+        }
+        if (c.lane < 16) {
+            char* reg = c.smem + NSLOT * SLOT_BYTES + COMP_OFF;    // wave 0's region
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) {
+                const int j = c.wave * SPW + 16 * sb + c.lane;
+                f4 h = c.head[sb];
+                if (col_sigma) h[3] = c.sig[sb];
+                *reinterpret_cast<f4*>(reg + j * 16) = c.phead[sb];
+                *reinterpret_cast<float*>(reg + COMP_DEL + j * 4) = c.pcdist[sb];
+                *reinterpret_cast<f4*>(reg + (TILE + j) * 16) = h;
+                *reinterpret_cast<float*>(reg + COMP_DEL + (TILE + j) * 4) = c.cdist[sb];
+            }
+        }
+        barrier();
+        asm volatile("" ::: "memory");
+        if (c.wave == 0) composite_wave<(2 * TILE) / 64>(c, (int64_t)(tile >> 1), S);
+        return;
+    }
     if (c.lane < 16) {
 #pragma unroll
         for (int sb = 0; sb < SB; ++sb) {
@@ -1181,7 +1221,7 @@ __device__ __forceinline__ void composite_tile(Ctx& c, int tile) {
                 f4 h = c.head[sb];
                 if (col_sigma) h[3] = c.sig[sb];
                 *reinterpret_cast<f4*>(reg + o * 16) = h;
-                *reinterpret_cast<float*>(reg + TILE * 16 + o * 4) = c.cdist[sb];
+                *reinterpret_cast<float*>(reg + COMP_DEL + o * 4) = c.cdist[sb];
             }
         }
     }
@@ -1216,7 +1256,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
 #ifdef NERF_FUSED_PRIO_HALF      // tuning: static issue priority for the second-dispatched half of the waves
     if (c.wave >= NWAVE / 2) __builtin_amdgcn_s_setprio(1);
 #endif
-    const int my_tiles = (a.ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int ngroups = a.ntiles / a.span;
+    const int my_tiles = a.span * ((ngroups - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x);
     int per_tile = 0;
     for (int l = 0; l < a.n_layers; ++l)
         if (dma_units(c, l) > 0) per_tile += n16_of(LF(int, N, l));
@@ -1250,7 +1291,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
             c.xh[kb][sb] = bf16x8{};
             c.xl[kb][sb] = bf16x8{};
         }
-    for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    // tile groups of `span` consecutive tiles (one group: one tile, unless rays span two)
+    const int span_log = a.span >> 1;                 // span 1 or 2
+    for (int it = 0; it < my_tiles; ++it) {
+        const int tile = (((int)blockIdx.x + (it >> span_log) * (int)gridDim.x) << span_log) + (it & span_log);
         const int base = tile * TILE + c.wave * SPW;
         if (MODE == MODE_FWD && a.comp_on) {
             // the samples' interval lengths for the tile-end compositing (long landed by then)
@@ -1481,6 +1525,7 @@ int fused_launch(const nerf_fused_layer* layers, int32_t n_layers, const void* i
     a.n_layers = n_layers;
     a.M = (int)M;
     a.ntiles = (int)((M + TILE - 1) / TILE);
+    a.span = 1;
     // compositing fused into the forward (include/nerf_amd.h nerf_fused_composite)
     a.comp_on = 0;
     memset(&a.comp, 0, sizeof(a.comp));
@@ -1488,7 +1533,9 @@ int fused_launch(const nerf_fused_layer* layers, int32_t n_layers, const void* i
         a.comp = *comp;
         const int S = comp->samples_per_ray;
         if (!dgrad) {
-            NERF_REQUIRE(S >= 16 && S <= 128 && TILE % S == 0 && TILE / S <= NWAVE && M % S == 0);
+            NERF_REQUIRE(((S >= 16 && S <= TILE && TILE % S == 0 && TILE / S <= NWAVE) || S == 2 * TILE) &&
+                         M % S == 0);
+            if (S == 2 * TILE) a.span = 2;
             NERF_REQUIRE(comp->dist != nullptr && comp->rgb != nullptr);
             NERF_REQUIRE(comp->coef == nullptr || (aligned16(comp->coef) && M * 32 < ((int64_t)1 << 31)));
             // the heads: the last layer, one 16-row chunk with a barrier (a register-fed part)
@@ -1500,7 +1547,8 @@ int fused_launch(const nerf_fused_layer* layers, int32_t n_layers, const void* i
             a.comp_on = 1;
         }
     }
-    const int grid = a.ntiles < num_cus() ? a.ntiles : num_cus();
+    const int ngroups = a.ntiles / a.span;
+    const int grid = ngroups < num_cus() ? ngroups : num_cus();
     if (dgrad)
         hipLaunchKernelGGL(mlp_fused_kernel<MODE_DGRAD>, dim3(grid), dim3(WG), 0, as_stream(stream), a);
     else

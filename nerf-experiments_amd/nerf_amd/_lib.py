@@ -234,6 +234,7 @@ _SIGNATURES = {
     "nerf_prop_loss": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f, c_vp, c_f, c_vp,
                                c_i64, c_vp]),
     "nerf_hashgrid_workspace": (c_sz, [ctypes.POINTER(NerfHashgridParams)]),
+    "nerf_hashgrid_workspace_n": (c_sz, [ctypes.POINTER(NerfHashgridParams), c_i64]),
     "nerf_hashgrid_table_rows": (c_i64, [ctypes.POINTER(NerfHashgridParams), c_i32]),
     "nerf_hashgrid_bwd": (c_i32, [ctypes.POINTER(NerfHashgridParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
                                   c_vp, c_i64, c_vp, c_i32, c_vp, c_sz, c_vp]),
@@ -262,7 +263,7 @@ def load(path: str | None = None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.nerf_abi_version() != 7:
+    if lib.nerf_abi_version() != 8:
         raise RuntimeError("nerf_amd: ABI version mismatch between Python binding and libnerf_amd.so")
     for which, st in enumerate(STRUCTS):
         if lib.nerf_struct_size(which) != ctypes.sizeof(st):

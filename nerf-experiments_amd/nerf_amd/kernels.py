@@ -672,10 +672,13 @@ def _hashgrid_table_check(name: str, params, table: torch.Tensor) -> None:
                          f"(got {tuple(table.shape)})")
 
 
-# the forward kernel the library runs (NERF_HG_FWD_LEVEL=0: one thread per (sample, level) in
-# sample-major order; the same switch is read by the library)
-HASHGRID_FWD_FN = ("hashgrid_fwd_kernel" if os.environ.get("NERF_HG_FWD_LEVEL", "1") == "0"
-                   else "hashgrid_fwd_level_kernel")
+# the kernels the library runs (NERF_HG_FWD: 2 64-sample tiles with whole output rows, 1 the level
+# grid, 0 one thread per (sample, level); NERF_HG_BWD: 2 the persistent part walk over grad_out
+# restaged level-major, 1 the per-item grid over it, 0 the per-item grid on the rows — the same
+# switches are read by the library; tile / restaging for F in {1, 2, 4} and <= 16 levels)
+_HG_FWD = os.environ.get("NERF_HG_FWD", "2")[:1]
+HASHGRID_FWD_FN = {"0": "hashgrid_fwd_kernel", "1": "hashgrid_fwd_level_kernel"}.get(_HG_FWD, "hashgrid_fwd_tile_kernel")
+HASHGRID_BWD_FN = "hashgrid_bwd_walk_kernel" if os.environ.get("NERF_HG_BWD", "2")[:1] == "2" else "hashgrid_bwd_kernel"
 
 
 def hashgrid_fwd(params, table: torch.Tensor, out: torch.Tensor, *, x=None, ray_o=None, ray_d=None, t_start=None,
@@ -697,8 +700,13 @@ def hashgrid_fwd(params, table: torch.Tensor, out: torch.Tensor, *, x=None, ray_
     _lib.check(st, "nerf_hashgrid_fwd")
 
 
-def hashgrid_workspace_bytes(params) -> int:
-    return 256 + hashgrid_table_rows(params) * params.features * 8
+def hashgrid_workspace_bytes(params, n_samples: int | None = None) -> int:
+    """nerf_hashgrid_workspace(params), or with n_samples nerf_hashgrid_workspace_n: room for grad_out
+    restaged level-major as well (the backward's part walks then read contiguous values)."""
+    acc = 256 + hashgrid_table_rows(params) * params.features * 8
+    if n_samples is None:
+        return acc
+    return ((acc + 255) // 256) * 256 + int(n_samples) * params.levels * params.features * 4
 
 
 def hashgrid_bwd(params, grad_out: torch.Tensor, grad_table: torch.Tensor, workspace: torch.Tensor, *, x=None,
@@ -717,7 +725,7 @@ def hashgrid_bwd(params, grad_out: torch.Tensor, grad_table: torch.Tensor, works
         raise ValueError(f"workspace must be a contiguous, 256-byte aligned device buffer of >= {need} bytes")
     # algorithmic work: F fp32 gradients read and 8 corners x F 8-byte fixed-point adds per (sample, level)
     end = TIMER.bracket("hashgrid_bwd", 0.0, 8.0 * n_samples * params.levels * params.features * 8
-                        + 4.0 * n_samples * params.levels * params.features, fn="hashgrid_bwd_kernel") \
+                        + 4.0 * n_samples * params.levels * params.features, fn=HASHGRID_BWD_FN) \
         if TIMER is not None else None
     st = _lib.load().nerf_hashgrid_bwd(ctypes.byref(params), _ptr(x), _ptr(ray_o), _ptr(ray_d), _ptr(t_start),
                                        _ptr(t_end), n_samples, samples_per_ray, grad_out.data_ptr(),

@@ -85,7 +85,8 @@ def composite_eligible(plan, M: int, S: int) -> bool:
     """The fused forward runs this plan and its last layer can hand its heads to the compositing."""
     if not FUSE_COMPOSITE or matmul_precision() != "x3" or not mlp_fused.eligible(plan, M):
         return False
-    if not (16 <= S <= 128 and 128 % S == 0 and M % S == 0 and M * 32 < (1 << 31)):
+    # whole rays per 128-sample tile, or rays of 256 samples over two tiles run back to back
+    if not ((16 <= S <= 128 and 128 % S == 0) or S == 256) or M % S or M * 32 >= (1 << 31):
         return False
     L = len(plan.layers)
     if len(plan.column_outputs) > 1 or (plan.column_outputs and plan.column_outputs[0][0] == L - 1):

@@ -96,7 +96,7 @@ class _HashGridFn(th.autograd.Function):
         grads = [None] * len(ctx.rows)
         if g is not None and any(ctx.needs_input_grad[11:]):
             gp = th.empty(shape, device=g.device, dtype=th.float32)
-            ws = th.empty((K.hashgrid_workspace_bytes(ctx.params) + 7) // 8, dtype=th.int64, device=g.device)
+            ws = th.empty((K.hashgrid_workspace_bytes(ctx.params, n) + 7) // 8, dtype=th.int64, device=g.device)
             K.hashgrid_bwd(ctx.params, g.contiguous(), gp, ws, x=x, ray_o=o, ray_d=d, t_start=t0, t_end=t1,
                            n_samples=n, samples_per_ray=spr)
             off = 0
@@ -358,8 +358,8 @@ class NaiveINGP(nn.Module):
         if isinstance(model, NerfModel):
             # fused: positions o + t d generated in the encoding kernel, direction encoding once per
             # ray, softplus(z - 1) / sigmoid applied in the compositor — inside the field MLP's
-            # launches when the rays fill its tiles (the 64-sample coarse pass; the 256-sample fine
-            # pass takes the stand-alone compositing kernels, 0.07 ms of the C5 step)
+            # launches when the rays fill its tiles (the 64-sample coarse pass) or span two of them
+            # (the 256-sample fine pass: a workgroup runs a ray's two tiles back to back)
             if model.fused_composite_ok(batch_size * samples_per_ray, samples_per_ray):
                 rgb, weights = model.render_composite(ray_origs, ray_dirs, None, t, t_end, samples_per_ray, 0, 1,
                                                       sample_dist, 1.0, 1.0)

@@ -8,7 +8,8 @@ weights are BITWISE those of render_raw + composite_raw.  Backward: the chain fo
 density gradient rows from the forward's per-sample coefficients (linear in grad_rgb: no scan), a
 different fp32 rounding order than nerf_composite_bwd — bar 2e-5 relative to each gradient's scale
 (the compositing tolerance of test_gpu_parity.py).  Covers the C3 mip workload's S = 64 / 128,
-S = 16 / 32 (8 / 4 rays per tile), ragged ray counts (the last tile partial), the density as a
+S = 16 / 32 (8 / 4 rays per tile), S = 256 (one ray over two tiles run back to back: 3d-ingp's
+fine pass), ragged ray counts (the last tile partial), the density as a
 column output (NerfModel) and as head row 3 (delayed density), pose gradients to the rays, and the
 torch fallback taken when the chain cannot form the rows."""
 import pytest
@@ -79,7 +80,8 @@ def _close(a, b, rel=2e-5):
 
 
 @pytest.mark.parametrize("n_rays,S,delayed", [(4096, 64, False), (4096, 128, False), (37, 64, False),
-                                              (301, 32, False), (75, 16, False), (203, 128, True)])
+                                              (301, 32, False), (75, 16, False), (203, 128, True),
+                                              (1024, 256, False), (37, 256, False), (45, 256, True)])
 def test_fused_composite_forward_bitwise_and_gradients(n_rays, S, delayed):
     model = _model(delayed)
     o, d, t0, t1, pw = _rays(n_rays, S)

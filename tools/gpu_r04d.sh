@@ -17,7 +17,7 @@ timeout -k 10 200 python -u tools/wgrad_ab.py --out "$OUT/b.pt" --compare "$OUT/
   || { echo "ab tr failed"; tail "$OUT/ab_tr.txt"; exit 1; }
 paste "$OUT/ab_dma.txt" "$OUT/ab_tr.txt" | cut -c1-220
 for rep in 1 2; do
-  for lib in nerf-experiments_amd/nerf_amd/libnerf_amd.so nerf-experiments_amd/var/lib_unroll0.so nerf-experiments_amd/var/lib_wreg0.so; do
+  for lib in nerf-experiments_amd/nerf_amd/libnerf_amd.so nerf-experiments_amd/var/lib_head.so nerf-experiments_amd/var/lib_unroll0.so nerf-experiments_amd/var/lib_wreg0.so; do
     NERF_AMD_LIB=$lib timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --no-frame-roofline --steps 100 \
       > "$OUT/$(basename $lib)_$rep.json" 2> "$OUT/$(basename $lib)_$rep.err" || { echo "failed $lib"; tail "$OUT/$(basename $lib)_$rep.err"; exit 1; }
     python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['value']/1e6,2), round(d['ms_per_step'],3), d['final_loss'], {k: round(v['ms_per_step'],3) for k,v in d['kernel_functions'].items() if v['ms_per_step']>0.3})" "$OUT/$(basename $lib)_$rep.json" "$(basename $lib)"

@@ -51,7 +51,7 @@ def main():
         out = torch.empty(n, L * F, device=dev)
         gout = torch.randn(n, L * F, generator=g).to(dev)
         gt = torch.empty_like(table)
-        ws = torch.empty(kernels.hashgrid_workspace_bytes(p) // 8 + 1, dtype=torch.int64, device=dev)
+        ws = torch.empty(kernels.hashgrid_workspace_bytes(p, n) // 8 + 1, dtype=torch.int64, device=dev)
         kw = dict(ray_o=o, ray_d=d, t_start=t0, t_end=t1, n_samples=n, samples_per_ray=S)
         f = timed(lambda: kernels.hashgrid_fwd(p, table, out, **kw))
         b = timed(lambda: kernels.hashgrid_bwd(p, gout, gt, ws, **kw))
