@@ -1894,12 +1894,20 @@ static int wgrad_x3_rows_impl(const float* dY, int64_t ld_dy, const nerf_seg* se
     int64_t mps = (M + splits - 1) / splits;
     mps = ((mps + TBM - 1) / TBM) * TBM;
     if (raysum != nullptr) {
-        // per-ray sums of dY from the streamed kernel: rays of 16..128 samples (S | 128) that no step or
-        // split cuts (splits and block 1 start at multiples of 128 rows)
-        auto s_ok = [](int S) { return S >= 16 && S <= 128 && 128 % S == 0; };
-        NERF_REQUIRE(s_ok(S0) && (M1 == 0 || s_ok(S1)) && M0 % 128 == 0 && M0 % S0 == 0 && M1 % (M1 ? S1 : 1) == 0);
+        // per-ray sums of dY from the streamed kernel: rays of 16..128 samples (S | 128) or of a multiple
+        // of 128 samples (3d-ingp's 256-sample fine pass) that no step or split cuts (splits and block 1
+        // start at multiples of lcm(128, S0, S1) rows)
+        auto s_ok = [](int S) { return S >= 16 && S <= 4096 && (128 % S == 0 || S % 128 == 0); };
+        auto lcm = [](int64_t x, int64_t y) {
+            int64_t g = x, h = y;
+            while (h) { const int64_t t = g % h; g = h; h = t; }
+            return x / g * y;
+        };
+        NERF_REQUIRE(s_ok(S0) && (M1 == 0 || s_ok(S1)));
+        const int64_t R = lcm(lcm(128, S0), M1 ? S1 : 1);
+        NERF_REQUIRE((M1 == 0 || M0 % R == 0) && M0 % S0 == 0 && M1 % (M1 ? S1 : 1) == 0);
         NERF_REQUIRE((N > 128 || L.ktot > 128) && N <= 256 && L.ktot <= 256);
-        mps = ((mps + 127) / 128) * 128;
+        mps = ((mps + R - 1) / R) * R;
     }
     TNArgs a{dY, ld_dy, N, L, (int)M, (int)mps, splits, slab, db_slab, (int)M0, dY, ld_dy, {}, {}, {},
              raysum, S0 > 0 ? S0 : 1, S1 > 0 ? S1 : 1, S0 > 0 ? (int)(M0 / S0) : 0};

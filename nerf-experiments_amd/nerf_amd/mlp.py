@@ -20,6 +20,7 @@ it, and a stale pack would silently train on old weights).
 """
 from __future__ import annotations
 
+import math
 import os
 from dataclasses import dataclass, field
 
@@ -130,13 +131,17 @@ def _ray_split(blocks, N4: int):
         if len(segs) < 2 or M == 0:
             return None
         t, k, S = segs[-1]
-        if not (16 <= S <= 128 and 128 % S == 0 and M % S == 0) or any(rd != 1 for _, _, rd in segs[:-1]):
+        # rays of S | 128 samples, or of a multiple of 128 (nerf_linear_wgrad_x3_rays: no split cuts a ray)
+        if not (16 <= S <= 4096 and (128 % S == 0 or S % 128 == 0) and M % S == 0) \
+                or any(rd != 1 for _, _, rd in segs[:-1]):
             return None
         mains.append(segs[:-1])
         rays.append((t, k, S))
     kmain = sum(K.pad32(k) for _, k, _ in mains[0])
     if kmain > 256 or not (N4 > 128 or kmain > 128) or blocks[0][2] % 128:
         return None
+    if len(blocks) > 1 and blocks[0][2] % math.lcm(128, *(S for _, _, S in rays)):
+        return None                                     # block 1 would start inside a split's ray
     return mains, rays
 
 

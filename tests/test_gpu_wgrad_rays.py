@@ -2,7 +2,7 @@
 encoding read once per ray, row divisor S) through nerf_linear_wgrad_x3_rays: the streamed kernel over
 the per-sample inputs also sums dY over each ray's samples, and the per-ray input's columns come from
 those sums over the B rays (mlp._wgrad_rays).  Against fp64 over every sample's row with the
-split-precision bound of test_gpu_parity.py (2^-15 of |dY|^T |X|), one or two row blocks (the two
+split-precision bound of test_gpu_parity.py (2^-15 of |dY|^T |X|), rays of S | 128 or 256 samples (3d-ingp's fine pass), one or two row blocks (the two
 passes of a shared field), and the layer-level switch (NERF_WGRAD_RAYS) on a NerfModel step."""
 import types
 
@@ -14,7 +14,9 @@ DEV = "cuda"
 
 
 @pytest.mark.parametrize("B0,S0,B1,S1,N,kmain,kray", [(64, 64, 32, 128, 128, 256, 27), (100, 64, 0, 0, 128, 256, 27),
-                                                       (48, 16, 16, 32, 200, 96, 12), (2048, 128, 4096, 64, 128, 256, 27)])
+                                                       (48, 16, 16, 32, 200, 96, 12), (2048, 128, 4096, 64, 128, 256, 27),
+                                                       (300, 256, 0, 0, 128, 256, 24), (512, 64, 37, 256, 128, 256, 24),
+                                                       (20, 256, 64, 128, 200, 256, 24)])
 def test_wgrad_rays_matches_fp64(B0, S0, B1, S1, N, kmain, kray):
     from nerf_amd import kernels as K, mlp
     torch.manual_seed(B0 + B1 + N)
@@ -44,6 +46,19 @@ def test_wgrad_rays_matches_fp64(B0, S0, B1, S1, N, kmain, kray):
     bound = 2.0 ** -15 * (Y.abs().T @ X.abs()) + 1e-6
     assert ((gW.cpu().double() - refw).abs() <= bound).all()
     assert torch.allclose(gb.cpu().double(), Y.sum(0), rtol=1e-4, atol=2e-4)
+
+
+def test_ray_split_refuses_a_block_boundary_inside_a_ray():
+    """Two blocks whose rays of 256 samples would start inside a split (block 0 of 384 rows: a
+    multiple of 128, not of 256) take the per-sample route instead."""
+    from nerf_amd import mlp
+    blocks = []
+    for B, S in ((6, 64), (4, 256)):
+        M = B * S
+        blocks.append((torch.zeros(M, 128, device=DEV), [(torch.zeros(M, 256, device=DEV), 256, 1),
+                                                         (torch.zeros(B, 24, device=DEV), 24, S)], M))
+    assert mlp._ray_split(blocks, 128) is None
+    assert mlp._ray_split(blocks[1:], 128) is not None
 
 
 def test_ray_route_in_a_training_step():
