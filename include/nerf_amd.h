@@ -151,7 +151,7 @@ int nerf_resample_pdf(const float* t_coarse, const float* weights, const float* 
  * out row stride out_ld >= output_dim; columns [output_dim, out_ld) are zeroed.
  * ------------------------------------------------------------------------- */
 typedef struct nerf_pe_params {
-    int32_t kind;               /* 0 fourier/barf, 1 integrated */
+    int32_t kind;               /* 0 fourier/barf, 1 integrated (2 hash grid: nerf_fused_encoding only) */
     int32_t levels;             /* L */
     int32_t include_identity;   /* 0/1 */
     int32_t query;              /* 0 left, 1 middle (ray mode) */
@@ -384,7 +384,12 @@ typedef struct nerf_fused_layer {
 /* An encoding generated inside the fused forward: every entry with out_dim > 0 is computed at the
  * start of each 128-sample tile (exactly as nerf_encode_fwd computes it) and its rows are stored
  * to out (required), where later layers (seg_ptr = out) and the weight gradients read them; the
- * first layer may take them straight from LDS (seg_gen). */
+ * first layer may take them straight from LDS (seg_gen).
+ * params.kind 2 (ABI 8): the multiresolution hash-grid features of ray-mode positions, exactly as
+ * nerf_hashgrid_fwd computes them (out_dim = levels * features <= 64, levels <= 16, features 1, 2
+ * or 4; params.query as hash->query): `hash` points to the host-side parameters (copied at the
+ * launch), `hash_table` to the packed device table; at most one kind-2 entry per launch. */
+struct nerf_hashgrid_params;
 typedef struct nerf_fused_encoding {
     nerf_pe_params params;     /* as nerf_encode_fwd takes it (ray mode: query, pw_mode) */
     const float* ray_o;        /* [n_rays][3] */
@@ -399,6 +404,8 @@ typedef struct nerf_fused_encoding {
     int32_t per_ray;           /* 0: position encoding of o + tq d; 1: encoding of the ray direction */
     int32_t out_dim;           /* encoding columns (the rest of a 32-column block reads 0) */
     int32_t reserved;
+    const struct nerf_hashgrid_params* hash;  /* kind 2: host pointer, read at the launch */
+    const float* hash_table;   /* kind 2: [sum_l rows_l][features] device table */
 } nerf_fused_encoding;
 
 /* encodings: NULL, or 2 entries (generated segments index them) */

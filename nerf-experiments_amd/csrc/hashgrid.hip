@@ -25,8 +25,10 @@
 #include <stdlib.h>
 
 #include "common.h"
+#include "hashgrid_common.h"
 
 namespace {
+using namespace nerf;
 
 struct HashArgs {
     nerf_hashgrid_params p;
@@ -54,62 +56,6 @@ __device__ __forceinline__ void sample_position(const HashArgs& a, int64_t n, fl
     for (int j = 0; j < 3; ++j) p[j] = a.o[ray * 3 + j] + tq * a.d[ray * 3 + j];
 }
 
-struct Corners {
-    int idx[8];           // table rows (< T < 2^31)
-    float w[8];
-};
-
-// the hash of one corner: int64 (x*pi1) ^ (y*pi2) ^ (z*pi3) with wrap-around products and the
-// non-negative remainder modulo T (torch.remainder); modulo a power of two that is the low bits,
-// which only the low 32 bits of corners and primes determine (two's complement): 32-bit arithmetic
-__device__ __forceinline__ int hash_row(const long long* cc, const nerf_hashgrid_params& p, int T, bool pow2) {
-    if (pow2) {
-        const unsigned h = ((unsigned)cc[0] * (unsigned)p.primes[0]) ^ ((unsigned)cc[1] * (unsigned)p.primes[1]) ^
-                           ((unsigned)cc[2] * (unsigned)p.primes[2]);
-        return (int)(h & (unsigned)(T - 1));
-    }
-    const unsigned long long h = ((unsigned long long)cc[0] * (unsigned long long)p.primes[0]) ^
-                                 ((unsigned long long)cc[1] * (unsigned long long)p.primes[1]) ^
-                                 ((unsigned long long)cc[2] * (unsigned long long)p.primes[2]);
-    const long long m = (long long)h % (long long)T;
-    return (int)(m < 0 ? m + T : m);
-}
-
-__device__ __forceinline__ Corners level_corners(const float* p, const nerf_hashgrid_params& prm, int r, int T) {
-#pragma clang fp contract(off)
-    Corners c;
-    float xh[3];
-    long long base[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        xh[j] = (prm.normalize ? (p[j] / 8.0f + 0.5f) : p[j]) * (float)r;
-        base[j] = (long long)floorf(xh[j]);
-    }
-    const bool bij = (long long)(r + 1) * (r + 1) * (r + 1) <= (long long)T;
-    const bool pow2 = (T & (T - 1)) == 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        long long cc[3];
-        float dw[3];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            cc[j] = base[j] + ((k >> (2 - j)) & 1);         // z fastest: the reference's stacking order
-            dw[j] = 1.0f - fabsf(xh[j] - (float)cc[j]);
-        }
-        c.w[k] = (dw[0] * dw[1]) * dw[2];
-        if (bij) {
-            const int r1 = r + 1;
-            int q[3];
-#pragma unroll
-            for (int j = 0; j < 3; ++j) q[j] = cc[j] < 0 ? 0 : (cc[j] > r ? r : (int)cc[j]);
-            c.idx[k] = q[0] + r1 * q[1] + r1 * r1 * q[2];
-        } else {
-            c.idx[k] = hash_row(cc, prm, T, pow2);
-        }
-    }
-    return c;
-}
-
 __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(HashArgs a, const float* __restrict__ table,
                                                            float* __restrict__ out, int64_t ld) {
 #pragma clang fp contract(off)
@@ -120,7 +66,7 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(HashArgs a, const flo
     if (n >= a.n) return;
     float p[3];
     sample_position(a, n, p);
-    const Corners c = level_corners(p, a.p, a.p.res[l], T);
+    const Corners c = level_corners(p, a.p.normalize, a.p.res[l], T, a.p.primes);
     const float* tab = table + a.off[l] * F;
     float acc[NERF_HASHGRID_MAX_FEATURES];
 #pragma unroll
@@ -151,7 +97,7 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_level_kernel(HashArgs a, con
     if (n >= a.n) return;
     float p[3];
     sample_position(a, n, p);
-    const Corners c = level_corners(p, a.p, a.p.res[l], T);
+    const Corners c = level_corners(p, a.p.normalize, a.p.res[l], T, a.p.primes);
     const float* tab = table + a.off[l] * F;
     float acc[NERF_HASHGRID_MAX_FEATURES];
 #pragma unroll
@@ -199,7 +145,7 @@ __global__ __launch_bounds__(1024) void hashgrid_fwd_tile_kernel(HashArgs a, con
     if (n < a.n) {
         float p[3];
         sample_position(a, n, p);
-        const Corners c = level_corners(p, a.p, a.p.res[l], T);
+        const Corners c = level_corners(p, a.p.normalize, a.p.res[l], T, a.p.primes);
         const float* tab = table + a.off[l] * F;
         float v[8][F];
 #pragma unroll
@@ -344,10 +290,6 @@ struct BwdPlan {
     int64_t nslab;                                  // slabs (the persistent walk's items: parts x nslab)
 };
 
-__host__ __device__ inline int64_t level_rows(int r, int T) {
-    const int64_t r1 = r + 1;
-    return r1 * r1 * r1 <= T ? r1 * r1 * r1 : T;
-}
 
 // Each thread takes BWD_UNROLL samples per trip and issues all their loads (positions or ray
 // origin / direction / interval, and the F gradient values) before any is used, so a trip costs one
@@ -405,7 +347,7 @@ __device__ __forceinline__ void walk_part(const HashArgs& a, int l, int res, int
 #pragma unroll
         for (int u = 0; u < BWD_UNROLL; ++u) {
             if (nb + u * BWD_THREADS >= n_end) continue;
-            const Corners c = level_corners(p[u], a.p, res, T);
+            const Corners c = level_corners(p[u], a.p.normalize, res, T, a.p.primes);
             // An LDS atomic costs the same per wave-instruction however few lanes are active, and a
             // part holds only ~1/parts of a sample's corners: so each lane queues its in-range
             // corners and the wave issues one add per queued-corner round (its longest queue)
@@ -653,6 +595,7 @@ extern "C" size_t nerf_hashgrid_workspace(const nerf_hashgrid_params* params) {
 }
 
 namespace {
+using namespace nerf;
 size_t gt_offset(const nerf_hashgrid_params* params) { return (nerf_hashgrid_workspace(params) + 255) & ~(size_t)255; }
 }  // namespace
 

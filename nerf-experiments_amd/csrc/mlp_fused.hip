@@ -39,6 +39,7 @@
 #include "common.h"
 #include "encode_common.h"
 #include "composite_common.h"
+#include "hashgrid_common.h"
 
 using namespace nerf;
 
@@ -111,7 +112,12 @@ struct FusedArgs {
     int span;          // tiles a workgroup runs back to back (2: rays of 256 samples), ntiles % span == 0
     int comp_on;       // forward: composite every tile's rays (nerf_mlp_fused_render)
     nerf_fused_composite comp;
+    // a generated hash-grid encoding (params.kind 2): its parameters, table and level row offsets
+    nerf_hashgrid_params hg;
+    const float* hg_table;
+    int hg_off[16];
 };
+static_assert(sizeof(FusedArgs) <= 4096, "kernel arguments");
 
 typedef __attribute__((address_space(4))) const char kchar_t;
 typedef float* fptr_t;
@@ -134,6 +140,10 @@ typedef const uint8_t* cu8ptr_t;
     (*(const __attribute__((address_space(4))) T*)(c.kargs + offsetof(FusedArgs, enc) +                      \
                                                    (size_t)(e) * sizeof(nerf_fused_encoding) +               \
                                                    offsetof(nerf_fused_encoding, f)))
+
+// fields of the generated hash grid, from the kernel-argument segment
+#define HG(T, f) (*(const __attribute__((address_space(4))) T*)(c.kargs + offsetof(FusedArgs, hg) +               \
+                                                               offsetof(nerf_hashgrid_params, f)))
 
 // fields of the fused composite, from the kernel-argument segment
 #define CF(T, f)                                                                                             \
@@ -353,12 +363,89 @@ __device__ __forceinline__ void gen_load(const Ctx& c, int e, int base, float (&
     }
 }
 
+// Hash-grid features (params.kind 2) of the wave's samples into its LDS scratch, as
+// hashgrid_fwd_tile_kernel computes them (hashgrid_common.h: the same corner arithmetic, the 8
+// corners' feature loads issued before the sums, products rounded then added in corner order):
+// the samples' positions first (lanes < SPW), then one (sample, level) task per lane and trip —
+// 16 lanes per level, so a wave-instruction's gathers hit four levels' tables.
+__device__ __forceinline__ void gen_hash_rows(const Ctx& c, int base, const float (&v)[9]) {
+#pragma clang fp contract(off)
+    float* R = reinterpret_cast<float*>(c.ximg);          // [SPW][GEN_LD]
+    float* P = R + SPW * GEN_LD;                            // [SPW][8]: position xyz
+    const int L = HG(int32_t, levels), F = HG(int32_t, features), T = HG(int32_t, table_size);
+    const int cols = L * F;
+    if (c.lane < SPW) {
+        float p[3] = {0.f, 0.f, 0.f};
+        if (base + c.lane < c.M) {
+            // as sample_position (hashgrid.hip): o + tq d
+            const float tq = HG(int32_t, query) == 0 ? v[6] : (v[6] + v[7]) / 2.0f;
+            p[0] = v[0] + tq * v[3];
+            p[1] = v[1] + tq * v[4];
+            p[2] = v[2] + tq * v[5];
+        }
+        float* pr = P + c.lane * 8;
+        pr[0] = p[0]; pr[1] = p[1]; pr[2] = p[2];
+        float* row = R + c.lane * GEN_LD;
+        for (int col = cols; col < 64; ++col) row[col] = 0.f;
+    }
+    // (same wave: its LDS operations complete in order, so the positions above are visible below)
+    const int normalize = HG(int32_t, normalize);
+    const __attribute__((address_space(4))) int64_t* primes =
+        (const __attribute__((address_space(4))) int64_t*)(c.kargs + offsetof(FusedArgs, hg) +
+                                                           offsetof(nerf_hashgrid_params, primes));
+    const long long pr[3] = {(long long)primes[0], (long long)primes[1], (long long)primes[2]};
+    const __attribute__((address_space(4))) int32_t* res =
+        (const __attribute__((address_space(4))) int32_t*)(c.kargs + offsetof(FusedArgs, hg) +
+                                                           offsetof(nerf_hashgrid_params, res));
+    const __attribute__((address_space(4))) int* offs =
+        (const __attribute__((address_space(4))) int*)(c.kargs + offsetof(FusedArgs, hg_off));
+    const float* table = *(const __attribute__((address_space(4))) cfptr_t*)(c.kargs + offsetof(FusedArgs, hg_table));
+    for (int i = c.lane; i < SPW * L; i += 64) {
+        const int r = i & (SPW - 1), l = i / SPW;
+        const float p[3] = {P[r * 8 + 0], P[r * 8 + 1], P[r * 8 + 2]};
+        const Corners cn = level_corners(p, normalize, res[l], T, pr);
+        const float* tab = table + (int64_t)offs[l] * F;
+        float* o = R + r * GEN_LD + l * F;
+        if (F == 2) {
+            float2 g[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) g[k] = *reinterpret_cast<const float2*>(tab + (int64_t)cn.idx[k] * 2);
+            float a0 = 0.0f, a1 = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                a0 = a0 + cn.w[k] * g[k].x;
+                a1 = a1 + cn.w[k] * g[k].y;
+            }
+            o[0] = a0;
+            o[1] = a1;
+        } else {
+            float g[8][4];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+#pragma unroll
+                for (int f = 0; f < 4; ++f) g[k][f] = f < F ? tab[(int64_t)cn.idx[k] * F + f] : 0.f;
+            float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+#pragma unroll
+                for (int f = 0; f < 4; ++f) acc[f] = acc[f] + cn.w[k] * g[k][f];
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+                if (f < F) o[f] = acc[f];
+        }
+    }
+}
+
 // Rows of encoding e from its inputs (gen_load) into the wave's LDS scratch.
 __device__ __forceinline__ void gen_rows_lds(const Ctx& c, int e, int base, const float (&v)[9]) {
 #pragma clang fp contract(off)
     float* R = reinterpret_cast<float*>(c.ximg);          // [SPW][GEN_LD]
     float* P = R + SPW * GEN_LD;                            // [SPW][8]: pm xyz, vb xyz
     const __attribute__((address_space(4))) nerf_pe_params& prm = EF(nerf_pe_params, params, e);
+    if (prm.kind == 2) {
+        gen_hash_rows(c, base, v);
+        return;
+    }
     const int per_ray = EF(int, per_ray, e);
     const int out_dim = EF(int, out_dim, e);
     const int L = prm.levels, id = prm.include_identity ? 3 : 0;
@@ -1345,6 +1432,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
 #undef LFI
 #undef EF
 #undef CF
+#undef HG
 
 struct PackArgs {
     const float* src[NERF_FUSED_MAX_SRCS];
@@ -1392,10 +1480,27 @@ namespace {
 int enc_out_dim(const nerf_pe_params& p) { return (2 * p.levels + (p.include_identity ? 1 : 0)) * 3; }
 
 // a generated segment's encoding, checked as nerf_encode_fwd checks its arguments
+bool hash_ok(const nerf_fused_encoding& e) {
+    const nerf_hashgrid_params* h = e.hash;
+    if (h == nullptr || e.hash_table == nullptr || !aligned16(e.hash_table)) return false;
+    if (h->levels < 1 || h->levels > 16 || !(h->features == 1 || h->features == 2 || h->features == 4)) return false;
+    if (h->table_size < 1 || (int64_t)h->levels * h->table_size * h->features >= ((int64_t)1 << 31)) return false;
+    if (!(h->normalize == 0 || h->normalize == 1) || !(h->query == 0 || h->query == 1)) return false;
+    if (e.params.query != h->query || e.per_ray || e.out_dim != h->levels * h->features) return false;
+    for (int l = 0; l < h->levels; ++l)
+        if (h->res[l] < 1 || h->res[l] > (1 << 20)) return false;
+    return true;
+}
+
 bool encoding_ok(const nerf_fused_encoding& e, int64_t M) {
     const nerf_pe_params& p = e.params;
-    if (!(p.levels >= 0 && p.levels <= 16 && (p.kind == 0 || p.kind == 1))) return false;
-    if (e.out_dim != enc_out_dim(p) || e.out_dim <= 0 || e.samples_per_ray < 1 || e.n_rays < 1) return false;
+    if (p.kind == 2) {
+        if (!hash_ok(e)) return false;
+    } else if (!(p.levels >= 0 && p.levels <= 16 && (p.kind == 0 || p.kind == 1))) {
+        return false;
+    }
+    if ((p.kind != 2 && e.out_dim != enc_out_dim(p)) || e.out_dim <= 0 || e.samples_per_ray < 1 || e.n_rays < 1)
+        return false;
     if (e.n_rays * e.samples_per_ray < M || M >= ((int64_t)1 << 31)) return false;
     if (e.ray_d == nullptr) return false;
     if (e.per_ray) {
@@ -1508,11 +1613,25 @@ int fused_launch(const nerf_fused_layer* layers, int32_t n_layers, const void* i
     // generated encodings (out_dim > 0): checked as nerf_encode_fwd checks its arguments; their rows
     // are always stored (later layers and the weight gradients read them)
     int gen_mask = 0;
+    memset(&a.hg, 0, sizeof(a.hg));
+    a.hg_table = nullptr;
+    memset(a.hg_off, 0, sizeof(a.hg_off));
     for (int e = 0; e < 2; ++e) {
         if (encodings != nullptr && encodings[e].out_dim > 0) {
             NERF_REQUIRE(!dgrad && encoding_ok(encodings[e], M) && encodings[e].out != nullptr && encodings[e].ld <= 64);
             a.enc[e] = encodings[e];
             gen_mask |= 1 << e;
+            if (encodings[e].params.kind == 2) {
+                // one hash grid per launch: its parameters and level row offsets by value
+                NERF_REQUIRE(a.hg_table == nullptr);
+                a.hg = *encodings[e].hash;
+                a.hg_table = encodings[e].hash_table;
+                int64_t off = 0;
+                for (int l = 0; l < a.hg.levels; ++l) {
+                    a.hg_off[l] = (int)off;
+                    off += level_rows(a.hg.res[l], a.hg.table_size);
+                }
+            }
         } else {
             memset(&a.enc[e], 0, sizeof(a.enc[e]));
         }

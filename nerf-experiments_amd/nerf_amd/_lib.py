@@ -131,6 +131,8 @@ class NerfFusedEncoding(ctypes.Structure):
         ("per_ray", c_i32),
         ("out_dim", c_i32),
         ("reserved", c_i32),
+        ("hash", c_vp),
+        ("hash_table", c_vp),
     ]
 
 

@@ -231,6 +231,9 @@ class FusedForward:
             t = pos if kind == "pos" else dirs
             nbytes += 4.0 * t.stride(0) * t.shape[0]
             nbytes += (8.0 * M + 28.0 * encs[e].n_rays) if not encs[e].per_ray else 12.0 * encs[e].n_rays
+            if encs[e].params.kind == 2:
+                # hash-grid features: 8 corners x F fp32 gathered per (sample, level)
+                nbytes += 32.0 * M * encs[e].out_dim
         flops = 0.0
         for idx, lp in enumerate(self.plan.layers):
             kbr, kbh, hbm, nb, n16, off, hbm_off, bias_off = self.layers[idx]

@@ -42,12 +42,14 @@ the renderer):
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import torch as th
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import _lib
 from . import kernels as K
 from . import positional_encodings as _pe
 from .mlp import nerf_model_plan
@@ -71,18 +73,46 @@ def _refuse_position_grad(*ts) -> None:
                          "pass detached positions / rays")
 
 
+def _hash_spec(params, packed, out, ray_o, ray_d, t_start, t_end, samples_per_ray: int, n: int):
+    """nerf_fused_encoding of kind 2: the features of ray-mode positions generated inside the fused
+    field-MLP forward at every tile start (include/nerf_amd.h), bitwise as nerf_hashgrid_fwd."""
+    e = _lib.NerfFusedEncoding()
+    e.params = K.make_pe_params(0, 0, False, 1.0, query=params.query)
+    e.params.kind = 2
+    e.ray_o, e.ray_d, e.t_start = ray_o.data_ptr(), ray_d.data_ptr(), t_start.data_ptr()
+    e.t_end = t_end.data_ptr() if t_end is not None else None
+    e.samples_per_ray, e.n_rays, e.per_ray = samples_per_ray, n // samples_per_ray, 0
+    e.out, e.ld, e.out_dim = out.data_ptr(), out.stride(0), params.levels * params.features
+    e.hash = ctypes.addressof(params)
+    e.hash_table = packed.data_ptr()
+    return e
+
+
 class _HashGridFn(th.autograd.Function):
     """Features of every level in one launch; the gradient of each level's table is a view of one
-    packed fixed-point gradient (nerf_hashgrid_bwd)."""
+    packed fixed-point gradient (nerf_hashgrid_bwd).  defer (ray-mode positions, a table the fused
+    kernel can read): the rows are left to the consuming fused field-MLP forward, which generates
+    them at every tile start (kernels.DeferredEncoding; any other consumer fills them first)."""
 
     @staticmethod
-    def forward(ctx, params, packed, rows, out_cols, x, ray_o, ray_d, t_start, t_end, samples_per_ray, n, *tables):
+    def forward(ctx, params, packed, rows, out_cols, x, ray_o, ray_d, t_start, t_end, samples_per_ray, n, defer,
+                *tables):
         out = th.empty(n, out_cols, device=packed.device, dtype=th.float32)
         used = params.levels * params.features
-        if out_cols > used:
-            out[:, used:].zero_()
-        K.hashgrid_fwd(params, packed, out, x=x, ray_o=ray_o, ray_d=ray_d, t_start=t_start, t_end=t_end,
-                       n_samples=n, samples_per_ray=samples_per_ray)
+
+        def fill(out):
+            if out_cols > used:
+                out[:, used:].zero_()
+            K.hashgrid_fwd(params, packed, out, x=x, ray_o=ray_o, ray_d=ray_d, t_start=t_start, t_end=t_end,
+                           n_samples=n, samples_per_ray=samples_per_ray)
+
+        if (defer and x is None and n > 0 and params.levels <= 16 and params.features in (1, 2, 4)
+                and used <= 64 and out_cols <= 64 and packed.data_ptr() % 16 == 0):
+            spec = _hash_spec(params, packed, out, ray_o, ray_d, t_start, t_end, samples_per_ray, n)
+            # keep: the inputs the spec points at, and the params struct its `hash` pointer names
+            out._nerf_deferred = K.DeferredEncoding(spec, (ray_o, ray_d, t_start, t_end, packed, params), fill)
+        else:
+            fill(out)
         ctx.params = params
         ctx.rows = rows
         ctx.meta = (samples_per_ray, n, packed.shape)
@@ -94,7 +124,7 @@ class _HashGridFn(th.autograd.Function):
         spr, n, shape = ctx.meta
         x, o, d, t0, t1 = (t if t.numel() else None for t in ctx.saved_tensors)
         grads = [None] * len(ctx.rows)
-        if g is not None and any(ctx.needs_input_grad[11:]):
+        if g is not None and any(ctx.needs_input_grad[12:]):
             gp = th.empty(shape, device=g.device, dtype=th.float32)
             ws = th.empty((K.hashgrid_workspace_bytes(ctx.params, n) + 7) // 8, dtype=th.int64, device=g.device)
             K.hashgrid_bwd(ctx.params, g.contiguous(), gp, ws, x=x, ray_o=o, ray_d=d, t_start=t0, t_end=t1,
@@ -103,7 +133,7 @@ class _HashGridFn(th.autograd.Function):
             for l, r in enumerate(ctx.rows):
                 grads[l] = gp[off:off + r]
                 off += r
-        return (None,) * 11 + tuple(grads)
+        return (None,) * 12 + tuple(grads)
 
 
 class INGPTable(nn.Module):
@@ -132,7 +162,7 @@ class INGPTable(nn.Module):
         if not table.is_contiguous():
             raise ValueError("INGPTable.table must be contiguous")
         return _HashGridFn.apply(self._params(), table, [table.shape[0]], self.n_features, x, None, None, None, None,
-                                 1, x.shape[0], table)
+                                 1, x.shape[0], False, table)
 
 
 class INGPEncoding(nn.Module):
@@ -204,17 +234,17 @@ class INGPEncoding(nn.Module):
     def packed_table(self) -> th.Tensor:
         return self._pack()
 
-    def _run(self, x, ray_o, ray_d, t_start, t_end, samples_per_ray, query, n):
+    def _run(self, x, ray_o, ray_d, t_start, t_end, samples_per_ray, query, n, defer=False):
         packed = self._pack()
         tables = [e.table for e in self.encodings]
         return _HashGridFn.apply(self._params(query), packed, self._rows, K.pad32(self.output_dim), x, ray_o, ray_d,
-                                 t_start, t_end, samples_per_ray, n, *tables)
+                                 t_start, t_end, samples_per_ray, n, defer, *tables)
 
     # -- kernel-facing API (the NerfModel lowering's encoder interface) -------------------------
     def encode_padded(self, x: th.Tensor, dir=None, pixel_width=None, t_start=None, t_end=None,
                       defer: bool = False) -> th.Tensor:
         """[N, pad32(output_dim)] features of explicit positions x [N, 3] (defer: accepted, ignored —
-        hash features are never generated inside the fused MLP)."""
+        only ray-mode positions are generated inside the fused MLP)."""
         if x.dim() != 2 or x.shape[1] != 3:
             raise ValueError(f"x must be [N, 3] (got {tuple(x.shape)})")
         _refuse_position_grad(x)
@@ -223,11 +253,14 @@ class INGPEncoding(nn.Module):
 
     def encode_rays(self, ray_origs, ray_dirs, t_start, t_end, pixel_width, samples_per_ray: int, query: int,
                     pw_mode: int = 0, defer: bool = False) -> th.Tensor:
-        """Features of the samples o + t_q d generated in-kernel (rays that require grad are refused)."""
+        """Features of the samples o + t_q d generated in-kernel (rays that require grad are refused);
+        defer: the rows may be generated by the consuming fused field-MLP forward itself (only for a
+        tensor handed straight to the field MLP, as PositionalEncoding.encode_rays)."""
         _refuse_position_grad(ray_origs, ray_dirs)
         n = t_start.numel()
         return self._run(None, ray_origs.contiguous(), ray_dirs.contiguous(),
-                         t_start.detach().contiguous(), t_end.detach().contiguous(), samples_per_ray, query, n)
+                         t_start.detach().contiguous(), t_end.detach().contiguous(), samples_per_ray, query, n,
+                         defer)
 
     # -- reference API ----------------------------------------------------------------------------
     def forward(self, x: th.Tensor, dir=None, pixel_width=None, t_start=None, t_end=None) -> th.Tensor:
