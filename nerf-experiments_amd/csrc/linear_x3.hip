@@ -1390,9 +1390,13 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             for (int q = 0; q < 4; ++q) {
                 const unsigned rm = lr + q < valid ? cmask : 0u;
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    rv[q][e] = __builtin_bit_cast(float, __builtin_bit_cast(int, rv[q][e]) &
+                for (int e = 0; e < 4; ++e) {
+                    // through a scalar: __builtin_bit_cast of the vector element lvalue rv[q][e] reads
+                    // element 0 (hipcc), which filled the masked rows' columns 1-3 with column 0
+                    const float xe = rv[q][e];
+                    rv[q][e] = __builtin_bit_cast(float, __builtin_bit_cast(int, xe) &
                                                              __builtin_amdgcn_sbfe((int)rm, (unsigned)e, 1u));
+                }
             }
         }
 #pragma unroll
@@ -1868,10 +1872,12 @@ static const bool SMALLN_ON = [] {
     return !(e && e[0] == '0');
 }();
 
-// NERF_WGRAD_TR=0: the single-tile layers on the LDS-DMA stream kernel (A/B switch, read once)
+// NERF_WGRAD_TR=1: the single-tile layers on the register-staged transposed-read kernel (A/B
+// switch, read once; default the LDS-DMA stream kernel — the transposed-read kernel failed its
+// parity tests on the first GPU run and stays off until it passes them)
 static const bool WGRAD_TR = [] {
     const char* e = getenv("NERF_WGRAD_TR");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
 }();
 
 static int wgrad_x3_rows_impl(const float* dY, int64_t ld_dy, const nerf_seg* segs, int64_t M0,

@@ -509,10 +509,11 @@ def linear_gauss_x3(segs, M: int, Wx: torch.Tensor, ldw: int, N: int, out: torch
     return True
 
 
-# the single-tile layers' weight-gradient kernel the library runs (NERF_WGRAD_TR=0: the LDS-DMA stream
-# kernel; the same switch is read by the library), for the timer's per-function grouping
-WGRAD_TILE_FN = ("linear_wgrad_x3_stream_kernel" if os.environ.get("NERF_WGRAD_TR", "1") == "0"
-                 else "linear_wgrad_x3_tr_kernel")
+# the single-tile layers' weight-gradient kernel the library runs (NERF_WGRAD_TR=1: the register-staged
+# transposed-read kernel, default the LDS-DMA stream kernel; the same switch is read by the library),
+# for the timer's per-function grouping
+WGRAD_TILE_FN = ("linear_wgrad_x3_tr_kernel" if os.environ.get("NERF_WGRAD_TR", "0") == "1"
+                 else "linear_wgrad_x3_stream_kernel")
 
 
 def linear_wgrad_x3(dY: torch.Tensor, N4: int, segs, M: int, workspace: torch.Tensor) -> None:

@@ -27,7 +27,7 @@ timeout -k 10 300 python3 -u bench.py --workload ingp --no-cpu-baseline --no-fra
 python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('ingp', round(d['value']/1e6,2), round(d['ms_per_step'],3), {k: round(v['ms_per_step'],3) for k,v in d['kernels'].items()})" "$OUT/bench_ingp.json"
 NERF_WGRAD_TR=0 timeout -k 10 200 python -u tools/wgrad_ab.py --out "$OUT/a.pt" > "$OUT/ab_dma.txt" 2>&1 \
   || { echo "ab dma failed"; tail "$OUT/ab_dma.txt"; exit 1; }
-timeout -k 10 200 python -u tools/wgrad_ab.py --out "$OUT/b.pt" --compare "$OUT/a.pt" > "$OUT/ab_tr.txt" 2>&1 \
+NERF_WGRAD_TR=1 timeout -k 10 200 python -u tools/wgrad_ab.py --out "$OUT/b.pt" --compare "$OUT/a.pt" > "$OUT/ab_tr.txt" 2>&1 \
   || { echo "ab tr failed"; tail "$OUT/ab_tr.txt"; exit 1; }
 paste "$OUT/ab_dma.txt" "$OUT/ab_tr.txt" | cut -c1-220
 for rep in 1 2; do
