@@ -366,8 +366,7 @@ __device__ __forceinline__ void gen_load(const Ctx& c, int e, int base, float (&
 // Hash-grid features (params.kind 2) of the wave's samples into its LDS scratch, as
 // hashgrid_fwd_tile_kernel computes them (hashgrid_common.h: the same corner arithmetic, the 8
 // corners' feature loads issued before the sums, products rounded then added in corner order):
-// the samples' positions first (lanes < SPW), then one (sample, level) task per lane and trip —
-// 16 lanes per level, so a wave-instruction's gathers hit four levels' tables.
+// the samples' positions first (lanes < SPW), then one level per trip.
 __device__ __forceinline__ void gen_hash_rows(const Ctx& c, int base, const float (&v)[9]) {
 #pragma clang fp contract(off)
     float* R = reinterpret_cast<float*>(c.ximg);          // [SPW][GEN_LD]
@@ -389,6 +388,11 @@ __device__ __forceinline__ void gen_hash_rows(const Ctx& c, int base, const floa
         for (int col = cols; col < 64; ++col) row[col] = 0.f;
     }
     // (same wave: its LDS operations complete in order, so the positions above are visible below)
+    // One level per trip, its resolution and row offset uniform (scalar loads), lane s < SPW on
+    // sample s.  (Four levels per trip on the four 16-lane groups, each group's level parameters
+    // selected from scalars, gave non-repeatable features in the last trip's fourth group of the
+    // second half of the waves on the GPU — cause not found; this form is repeatable and bitwise
+    // the stand-alone kernel, tests/test_hashgrid.py.)
     const int normalize = HG(int32_t, normalize);
     const __attribute__((address_space(4))) int64_t* primes =
         (const __attribute__((address_space(4))) int64_t*)(c.kargs + offsetof(FusedArgs, hg) +
@@ -400,28 +404,17 @@ __device__ __forceinline__ void gen_hash_rows(const Ctx& c, int base, const floa
     const __attribute__((address_space(4))) int* offs =
         (const __attribute__((address_space(4))) int*)(c.kargs + offsetof(FusedArgs, hg_off));
     const float* table = *(const __attribute__((address_space(4))) cfptr_t*)(c.kargs + offsetof(FusedArgs, hg_table));
-    for (int i = c.lane; i < SPW * L; i += 64) {
-        const int r = i & (SPW - 1), l = i / SPW;
-        const float p[3] = {P[r * 8 + 0], P[r * 8 + 1], P[r * 8 + 2]};
-        const Corners cn = level_corners(p, normalize, res[l], T, pr);
-        const float* tab = table + (int64_t)offs[l] * F;
-        float* o = R + r * GEN_LD + l * F;
-        if (F == 2) {
-            float2 g[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) g[k] = *reinterpret_cast<const float2*>(tab + (int64_t)cn.idx[k] * 2);
-            float a0 = 0.0f, a1 = 0.0f;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                a0 = a0 + cn.w[k] * g[k].x;
-                a1 = a1 + cn.w[k] * g[k].y;
-            }
-            o[0] = a0;
-            o[1] = a1;
-        } else {
+    for (int l = 0; l < L; ++l) {
+        const int rl = res[l], ol = offs[l];
+        if (c.lane < SPW) {
+            const int r = c.lane;
+            const float p[3] = {P[r * 8 + 0], P[r * 8 + 1], P[r * 8 + 2]};
+            const Corners cn = level_corners(p, normalize, rl, T, pr);
+            const float* tab = table + (int64_t)ol * F;
+            float* o = R + r * GEN_LD + l * F;
             float g[8][4];
 #pragma unroll
-            for (int k = 0; k < 8; ++k)
+            for (int k = 0; k < 8; ++k)          // the 8 corners' feature loads before the sums
 #pragma unroll
                 for (int f = 0; f < 4; ++f) g[k][f] = f < F ? tab[(int64_t)cn.idx[k] * F + f] : 0.f;
             float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};

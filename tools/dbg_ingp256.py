@@ -1,0 +1,39 @@
+"""Where the 256-sample NaiveINGP fine pass's fused weights differ from the stand-alone compositing."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "nerf-experiments_amd"))
+from nerf_amd import mlp  # noqa: E402
+from nerf_amd import model_interpolation_architecture as A  # noqa: E402
+from nerf_amd.model_ingp import FourierFeatures, INGPEncoding, NaiveINGP  # noqa: E402
+
+dev = torch.device("cuda", 0)
+torch.set_float32_matmul_precision("high")
+torch.manual_seed(0)
+ren = NaiveINGP(2, 7, 192, 64, INGPEncoding(1600, 16, 2 ** 16, 2, 16), FourierFeatures(4), 8, 256).to(dev)
+g = torch.Generator().manual_seed(5)
+S = 256
+for B in (256, 300, 1024):
+    for fe in (True, False):
+        A.FUSE_ENCODINGS = fe
+        model = ren.model_fine
+        o = (torch.randn(B, 3, generator=g) * 0.3 + torch.tensor([0.0, 0.0, 4.0])).to(dev)
+        d = torch.nn.functional.normalize(torch.randn(B, 3, generator=g) * 0.2 - torch.tensor([0.0, 0.0, 1.0]), dim=1).to(dev)
+        t = (torch.linspace(2.0, 7.0 - 5.0 / S, S).repeat(B, 1) + torch.rand(B, S, generator=g) * (5.0 / S)).to(dev)
+        out = {}
+        for fuse in (True, False):
+            mlp.FUSE_COMPOSITE = fuse
+            with torch.no_grad():
+                rgb, w, _ = ren._compute_color(model, t, o, d, B, S)
+            out[fuse] = (rgb.clone(), w.clone().view(B, S))
+        (r1, w1), (r0, w0) = out[True], out[False]
+        bad = (w1 != w0).nonzero()
+        print(f"B={B} fuse_enc={fe}: rgb equal {torch.equal(r1, r0)}, weights differ at {bad.shape[0]} of {B * S}; "
+              f"max {(w1 - w0).abs().max().item():.3e}; nan {torch.isnan(w1).sum().item()} {torch.isnan(w0).sum().item()}")
+        if bad.shape[0]:
+            rays = bad[:, 0].unique()
+            print("   rays", rays[:10].tolist(), "samples", bad[:10, 1].tolist())
+            r, s_ = bad[0].tolist()
+            print("   w1", w1[r, max(0, s_ - 2):s_ + 3].tolist(), "w0", w0[r, max(0, s_ - 2):s_ + 3].tolist())
