@@ -40,6 +40,8 @@ class KernelTimer:
 
     def summary(self, by: str = "tag"):
         out = {}
+        for *_, e, _fn in self.records:
+            e.synchronize()                     # (every end event recorded: durations are final)
         for tag, flops, nbytes, s, e, fn in self.records:
             ms = s.elapsed_time(e)
             d = out.setdefault(fn if by == "fn" else tag,
