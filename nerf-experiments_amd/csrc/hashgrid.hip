@@ -244,7 +244,9 @@ __global__ __launch_bounds__(256) void hashgrid_gtr_kernel(const float* __restri
         m = wm[0] > wm[1] ? wm[0] : wm[1];
         m = m > wm[2] ? m : wm[2];
         m = m > wm[3] ? m : wm[3];
-        if (m != 0) atomicMax(gmax, m);
+        // same-address atomics serialise at the memory side (one per block of 20 K blocks: ~0.2 ms):
+        // only a block whose max exceeds the running one adds its atomic
+        if (m != 0 && m > __hip_atomic_load(gmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(gmax, m);
     }
     const int run = nr * F;                       // one level's values of the workgroup's rows
     for (int e = threadIdx.x; e < L * run; e += 256) {
@@ -561,9 +563,10 @@ extern "C" int nerf_hashgrid_fwd(const nerf_hashgrid_params* params, const float
                                   (params->query == 0 || t_end)));
     if (n_samples == 0) return NERF_OK;
     const HashArgs a = make_args(params, x, ray_o, ray_d, t_start, t_end, n_samples, samples_per_ray);
-    // NERF_HG_FWD: 2 (default) 64-sample tiles, one wave per level, whole output rows; 1 the level
-    // grid; 0 one thread per (sample, level) — bitwise the same features
-    static const int mode = env_mode("NERF_HG_FWD", 2);
+    // NERF_HG_FWD: 1 (default) the level grid; 2 64-sample tiles, one wave per level, whole output
+    // rows; 0 one thread per (sample, level) — bitwise the same features (1.31 M samples x 16 levels:
+    // 361 / 375 / 764 us, profiles/r04e/hg_*.txt)
+    static const int mode = env_mode("NERF_HG_FWD", 1);
     const int F = params->features, L = params->levels;
     const bool f2_aligned = F != 2 || ((reinterpret_cast<uintptr_t>(out) & 7) == 0 && out_ld % 2 == 0 &&
                                        (reinterpret_cast<uintptr_t>(table) & 7) == 0);
@@ -625,9 +628,12 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
     if (n_samples > 0) {
         const int cols = params->levels * params->features;
         // grad_out restaged level-major (with its max) when the workspace has room for it
-        // (nerf_hashgrid_workspace_n) and the walks read it (NERF_HG_BWD: 2 persistent walk over the
-        // restaged values, default; 1 the per-item grid over them; 0 the per-item grid on the rows)
-        static const int mode = env_mode("NERF_HG_BWD", 2);
+        // (nerf_hashgrid_workspace_n) and the walks read it (NERF_HG_BWD: 0 (default) the per-item grid
+        // on the rows; 1 the per-item grid over the restaged values; 2 the persistent walk over them).
+        // Measured (1.31 M samples x 16 levels, profiles/r04e/hg_*.txt): 2807 / 3042 / 5586 us — the
+        // 97 concurrent parts of a slab share its rows in L2, so the strided reads cost nothing, and
+        // the part-major walk loses that sharing
+        static const int mode = env_mode("NERF_HG_BWD", 0);
         const int F = params->features;
         float* gt = nullptr;
         if (mode >= 1 && workspace_bytes >= nerf_hashgrid_workspace_n(params, n_samples) && (F == 1 || F == 2 || F == 4) &&

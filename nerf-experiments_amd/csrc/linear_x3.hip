@@ -1872,12 +1872,13 @@ static const bool SMALLN_ON = [] {
     return !(e && e[0] == '0');
 }();
 
-// NERF_WGRAD_TR=1: the single-tile layers on the register-staged transposed-read kernel (A/B
-// switch, read once; default the LDS-DMA stream kernel — the transposed-read kernel failed its
-// parity tests on the first GPU run and stays off until it passes them)
+// NERF_WGRAD_TR=0: the single-tile layers on the LDS-DMA stream kernel instead of the register-staged
+// transposed-read kernel (A/B switch, read once).  The two are bitwise equal (tests/
+// test_gpu_wgrad_tr.py); the transposed-read kernel runs 313 vs 363 us at M = 524 288, N = K = 256
+// and 264 vs 349 us for the 257-row layer (profiles/r04e/ab_*.txt)
 static const bool WGRAD_TR = [] {
     const char* e = getenv("NERF_WGRAD_TR");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
 }();
 
 static int wgrad_x3_rows_impl(const float* dY, int64_t ld_dy, const nerf_seg* segs, int64_t M0,

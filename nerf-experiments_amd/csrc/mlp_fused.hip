@@ -264,12 +264,13 @@ __device__ __forceinline__ void dma_seek(Ctx& c, int l) {
 // ones repeat pieces, and past the end of the stream the last chunk is fetched again), so that the
 // count of vector-memory ops in a chunk is the same on every path
 constexpr int DMA_PER_WAVE = 2 * KBMAX / NWAVE;
-// NERF_FUSED_WREG (default 1): the same pieces by plain buffer loads into VGPRs at the chunk start
-// and ds_write_b128 into the ring slot at the chunk end, instead of LDS-DMA.  A DMA piece costs its
-// wave 60-185 issue cycles beside MFMAs and LDS reads (MI355X_MICROARCH.md, LDS-DMA issue cost), a
-// load + ds_write_b128 pair ~17; the 8 VGPRs fit under the two-waves-per-SIMD budget.
+// NERF_FUSED_WREG=1: the same pieces by plain buffer loads into VGPRs at the chunk start and
+// ds_write_b128 into the ring slot at the chunk end, instead of LDS-DMA (a DMA piece costs its wave
+// 60-185 issue cycles beside MFMAs and LDS reads, MI355X_MICROARCH.md; a load + ds_write_b128 pair
+// ~17).  Measured slower on the mip step: 12.53 vs 12.22 ms, forward 3.93 / 3.97 vs 3.84 ms and
+// chain 3.73 vs 3.53 ms (two interleaved repetitions on one box, profiles/r04e), so off by default.
 #ifndef NERF_FUSED_WREG
-#define NERF_FUSED_WREG 1
+#define NERF_FUSED_WREG 0
 #endif
 __device__ __forceinline__ void dma_advance(Ctx& c) {
     if (c.d_remaining > 1) {

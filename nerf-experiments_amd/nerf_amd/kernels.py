@@ -511,11 +511,11 @@ def linear_gauss_x3(segs, M: int, Wx: torch.Tensor, ldw: int, N: int, out: torch
     return True
 
 
-# the single-tile layers' weight-gradient kernel the library runs (NERF_WGRAD_TR=1: the register-staged
-# transposed-read kernel, default the LDS-DMA stream kernel; the same switch is read by the library),
+# the single-tile layers' weight-gradient kernel the library runs (NERF_WGRAD_TR=0: the LDS-DMA stream
+# kernel, default the register-staged transposed-read kernel; the same switch is read by the library),
 # for the timer's per-function grouping
-WGRAD_TILE_FN = ("linear_wgrad_x3_tr_kernel" if os.environ.get("NERF_WGRAD_TR", "0") == "1"
-                 else "linear_wgrad_x3_stream_kernel")
+WGRAD_TILE_FN = ("linear_wgrad_x3_stream_kernel" if os.environ.get("NERF_WGRAD_TR", "1") == "0"
+                 else "linear_wgrad_x3_tr_kernel")
 
 
 def linear_wgrad_x3(dY: torch.Tensor, N4: int, segs, M: int, workspace: torch.Tensor) -> None:
@@ -675,13 +675,15 @@ def _hashgrid_table_check(name: str, params, table: torch.Tensor) -> None:
                          f"(got {tuple(table.shape)})")
 
 
-# the kernels the library runs (NERF_HG_FWD: 2 64-sample tiles with whole output rows, 1 the level
-# grid, 0 one thread per (sample, level); NERF_HG_BWD: 2 the persistent part walk over grad_out
-# restaged level-major, 1 the per-item grid over it, 0 the per-item grid on the rows — the same
-# switches are read by the library; tile / restaging for F in {1, 2, 4} and <= 16 levels)
-_HG_FWD = os.environ.get("NERF_HG_FWD", "2")[:1]
-HASHGRID_FWD_FN = {"0": "hashgrid_fwd_kernel", "1": "hashgrid_fwd_level_kernel"}.get(_HG_FWD, "hashgrid_fwd_tile_kernel")
-HASHGRID_BWD_FN = "hashgrid_bwd_walk_kernel" if os.environ.get("NERF_HG_BWD", "2")[:1] == "2" else "hashgrid_bwd_kernel"
+# the kernels the library runs (NERF_HG_FWD: 1 (default) the level grid, 2 64-sample tiles with whole
+# output rows, 0 one thread per (sample, level); NERF_HG_BWD: 0 (default) the per-item grid on the
+# rows, 1 the per-item grid over grad_out restaged level-major, 2 the persistent part walk over it —
+# the same switches are read by the library; tile / restaging for F in {1, 2, 4} and <= 16 levels;
+# measured on a 1.31 M-sample batch, profiles/r04e/hg_*.txt: forward 361 / 375 / 764 us, backward
+# 2807 / 3042 / 5586 us)
+_HG_FWD = os.environ.get("NERF_HG_FWD", "1")[:1]
+HASHGRID_FWD_FN = {"0": "hashgrid_fwd_kernel", "2": "hashgrid_fwd_tile_kernel"}.get(_HG_FWD, "hashgrid_fwd_level_kernel")
+HASHGRID_BWD_FN = "hashgrid_bwd_walk_kernel" if os.environ.get("NERF_HG_BWD", "0")[:1] == "2" else "hashgrid_bwd_kernel"
 
 
 def hashgrid_fwd(params, table: torch.Tensor, out: torch.Tensor, *, x=None, ray_o=None, ray_d=None, t_start=None,

@@ -44,6 +44,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch as th
 import torch.nn as nn
@@ -71,6 +72,13 @@ def _refuse_position_grad(*ts) -> None:
     if th.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts):
         raise ValueError("INGPEncoding: no position gradient through the hash grid on this path; "
                          "pass detached positions / rays")
+
+
+# Hash-grid features generated inside the fused field-MLP forward (NERF_FUSE_HASH=1).  Off by default:
+# bitwise equal to the stand-alone launch, but on the C5 step the forward grew by 1.9 ms against the
+# 0.45 ms of the level-grid launches it replaces (the tile-start gathers of all eight waves at once,
+# one level per trip; profiles/r04e)
+FUSE_HASH = os.environ.get("NERF_FUSE_HASH", "0") == "1"
 
 
 def _hash_spec(params, packed, out, ray_o, ray_d, t_start, t_end, samples_per_ray: int, n: int):
@@ -106,7 +114,7 @@ class _HashGridFn(th.autograd.Function):
             K.hashgrid_fwd(params, packed, out, x=x, ray_o=ray_o, ray_d=ray_d, t_start=t_start, t_end=t_end,
                            n_samples=n, samples_per_ray=samples_per_ray)
 
-        if (defer and x is None and n > 0 and params.levels <= 16 and params.features in (1, 2, 4)
+        if (defer and FUSE_HASH and x is None and n > 0 and params.levels <= 16 and params.features in (1, 2, 4)
                 and used <= 64 and out_cols <= 64 and packed.data_ptr() % 16 == 0):
             spec = _hash_spec(params, packed, out, ray_o, ray_d, t_start, t_end, samples_per_ray, n)
             # keep: the inputs the spec points at, and the params struct its `hash` pointer names
