@@ -384,6 +384,117 @@ __device__ __forceinline__ void walk_part(const HashArgs& a, int l, int res, int
     }
 }
 
+// The same walk with each thread on BWD_UNROLL CONSECUTIVE samples (one ray's neighbours) and a
+// run-length merge per corner slot: a corner whose row equals the previous sample's corner k adds
+// its fixed-point contribution to a register sum, which goes to the LDS accumulator once the row
+// changes (or at the end).  At the coarse levels the samples of a ray share cells, so most of their
+// LDS atomics — same-address atomics, serialised by the LDS — disappear; the integer sums are
+// associative, so the result is bitwise that of walk_part.
+template <int F>
+__device__ __forceinline__ void walk_part_merged(const HashArgs& a, int l, int res, int64_t row0, int prow, double scale,
+                                                 int64_t n_begin, int64_t n_end, const float* __restrict__ g,
+                                                 int64_t ld, const float* __restrict__ gt, unsigned long long* part) {
+#pragma clang fp contract(off)
+    const int T = a.p.table_size;
+    const bool rays = a.x == nullptr, mid = a.p.query != 0, small = a.n < ((int64_t)1 << 31);
+    for (int64_t base = n_begin; base < n_end; base += BWD_UNROLL * BWD_THREADS) {
+        const int64_t nb = base + (int64_t)threadIdx.x * BWD_UNROLL;
+        float p[BWD_UNROLL][3], gv[BWD_UNROLL][F];
+        if (rays) {
+            float t0[BWD_UNROLL], t1[BWD_UNROLL], o[BWD_UNROLL][3], d[BWD_UNROLL][3];
+#pragma unroll
+            for (int u = 0; u < BWD_UNROLL; ++u) {
+                const int64_t n = nb + u < n_end ? nb + u : n_end - 1;
+                const int64_t ray = small ? (int64_t)((unsigned)n / (unsigned)a.spr) : n / a.spr;
+                t0[u] = a.t0[n];
+                t1[u] = mid ? a.t1[n] : 0.0f;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    o[u][j] = a.o[ray * 3 + j];
+                    d[u][j] = a.d[ray * 3 + j];
+                }
+#pragma unroll
+                for (int f = 0; f < F; ++f) gv[u][f] = gt ? gt[n * F + f] : g[n * ld + (int64_t)l * F + f];
+            }
+#pragma unroll
+            for (int u = 0; u < BWD_UNROLL; ++u) {
+                const float tq = mid ? (t0[u] + t1[u]) / 2.0f : t0[u];
+#pragma unroll
+                for (int j = 0; j < 3; ++j) p[u][j] = o[u][j] + tq * d[u][j];
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < BWD_UNROLL; ++u) {
+                const int64_t n = nb + u < n_end ? nb + u : n_end - 1;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) p[u][j] = a.x[n * 3 + j];
+#pragma unroll
+                for (int f = 0; f < F; ++f) gv[u][f] = gt ? gt[n * F + f] : g[n * ld + (int64_t)l * F + f];
+            }
+        }
+        // run-length slots per corner: the row (relative to the part; -1 = none) and its sums
+        int srow[8];
+        long long sq[8][F];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            srow[k] = -1;
+#pragma unroll
+            for (int f = 0; f < F; ++f) sq[k][f] = 0;
+        }
+        auto flush = [&](unsigned pend) __attribute__((always_inline)) {
+            // one LDS add per queued round (the wave's longest queue), as walk_part
+            while (pend != 0u) {
+                const int k = __builtin_ctz(pend);
+                pend &= pend - 1u;
+                int rk = srow[0];
+                long long qk[F];
+#pragma unroll
+                for (int f = 0; f < F; ++f) qk[f] = sq[0][f];
+#pragma unroll
+                for (int j = 1; j < 8; ++j)
+                    if (k == j) {
+                        rk = srow[j];
+#pragma unroll
+                        for (int f = 0; f < F; ++f) qk[f] = sq[j][f];
+                    }
+#pragma unroll
+                for (int f = 0; f < F; ++f)
+                    if (qk[f] != 0) atomicAdd(&part[rk * F + f], (unsigned long long)qk[f]);
+            }
+        };
+#pragma unroll
+        for (int u = 0; u < BWD_UNROLL; ++u) {
+            if (nb + u >= n_end) break;
+            const Corners c = level_corners(p[u], a.p.normalize, res, T, a.p.primes);
+            int rel[8];
+            unsigned change = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int64_t r = (int64_t)c.idx[k] - row0;
+                rel[k] = (uint64_t)r < (uint64_t)prow ? (int)r : -1;
+                if (rel[k] != srow[k] && srow[k] >= 0) change |= 1u << k;
+            }
+            flush(change);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const bool same = rel[k] == srow[k];
+#pragma unroll
+                for (int f = 0; f < F; ++f) {
+                    // w * g is exact in fp64 (two 24-bit mantissas); one rounding to the fixed-point grid
+                    const long long q = rel[k] >= 0 ? llrint((double)c.w[k] * (double)gv[u][f] * scale) : 0;
+                    sq[k][f] = same ? sq[k][f] + q : q;
+                }
+                srow[k] = rel[k];
+            }
+        }
+        unsigned rest = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (srow[k] >= 0) rest |= 1u << k;
+        flush(rest);
+    }
+}
+
 // the part's accumulators out to the global ones: one contiguous pass of atomics
 template <int F>
 __device__ __forceinline__ void flush_part(const HashArgs& a, int l, int64_t row0, int prow,
@@ -403,8 +514,8 @@ __device__ __forceinline__ void part_of(const HashArgs& a, const BwdPlan& pl, in
     prow = (int)(rows < pl.rows_per_part ? rows : pl.rows_per_part);
 }
 
-// One workgroup per (part, slab) (NERF_HG_BWD_WALK=0).
-template <int F>
+// One workgroup per (part, slab).  MERGED: walk_part_merged (consecutive samples per thread).
+template <int F, bool MERGED>
 __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_kernel(HashArgs a, BwdPlan pl, const float* __restrict__ g,
                                                                    int64_t ld, const float* __restrict__ gt,
                                                                    const unsigned* __restrict__ gmax,
@@ -421,8 +532,12 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_kernel(HashArgs a, B
     for (int e = threadIdx.x; e < prow * F; e += BWD_THREADS) part[e] = 0ull;
     __syncthreads();
     const int64_t n1 = (slab + 1) * pl.slab < a.n ? (slab + 1) * pl.slab : a.n;
-    walk_part<F>(a, l, a.p.res[l], row0, prow, scale, slab * pl.slab, n1, g, ld, gt ? gt + (int64_t)l * a.n * F : nullptr,
-                 part);
+    if constexpr (MERGED)
+        walk_part_merged<F>(a, l, a.p.res[l], row0, prow, scale, slab * pl.slab, n1, g, ld,
+                            gt ? gt + (int64_t)l * a.n * F : nullptr, part);
+    else
+        walk_part<F>(a, l, a.p.res[l], row0, prow, scale, slab * pl.slab, n1, g, ld,
+                     gt ? gt + (int64_t)l * a.n * F : nullptr, part);
     __syncthreads();
     flush_part<F>(a, l, row0, prow, part, acc);
 }
@@ -471,14 +586,17 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_walk_kernel(HashArgs
 }
 
 template <int F>
-void launch_bwd(bool walk, int64_t blocks, hipStream_t s, const HashArgs& a, const BwdPlan& pl, const float* g, int64_t ld,
+void launch_bwd(bool walk, bool merged, int64_t blocks, hipStream_t s, const HashArgs& a, const BwdPlan& pl, const float* g, int64_t ld,
                 const float* gt, const unsigned* gmax, unsigned long long* acc) {
     if (walk)
         hipLaunchKernelGGL(hashgrid_bwd_walk_kernel<F>, dim3((unsigned)blocks), dim3(BWD_THREADS), 0, s, a, pl, g, ld, gt,
                            gmax, acc);
+    else if (merged)
+        hipLaunchKernelGGL((hashgrid_bwd_kernel<F, true>), dim3((unsigned)blocks), dim3(BWD_THREADS), 0, s, a, pl, g, ld, gt,
+                           gmax, acc);
     else
-        hipLaunchKernelGGL(hashgrid_bwd_kernel<F>, dim3((unsigned)blocks), dim3(BWD_THREADS), 0, s, a, pl, g, ld, gt, gmax,
-                           acc);
+        hipLaunchKernelGGL((hashgrid_bwd_kernel<F, false>), dim3((unsigned)blocks), dim3(BWD_THREADS), 0, s, a, pl, g, ld, gt,
+                           gmax, acc);
 }
 
 template <int F>
@@ -682,8 +800,8 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
             pl.nslab = slabs;
             blocks = slabs * pl.parts;
         }
-        void (*launch)(bool, int64_t, hipStream_t, const HashArgs&, const BwdPlan&, const float*, int64_t, const float*,
-                       const unsigned*, unsigned long long*) = nullptr;
+        void (*launch)(bool, bool, int64_t, hipStream_t, const HashArgs&, const BwdPlan&, const float*, int64_t,
+                       const float*, const unsigned*, unsigned long long*) = nullptr;
         switch (params->features) {
             case 1: launch = launch_bwd<1>; break;
             case 2: launch = launch_bwd<2>; break;
@@ -694,7 +812,12 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
             case 7: launch = launch_bwd<7>; break;
             default: launch = launch_bwd<8>; break;
         }
-        launch(walk, blocks, s, a, pl, grad_out, g_ld, gt, gmax, acc);
+        // NERF_HG_MERGE=1: consecutive samples per thread with run-length merged corner contributions
+        // (walk_part_merged); default 0, samples strided by the workgroup (walk_part).  Bitwise equal;
+        // measured (profiles/r04g): the merge saves a fifth at the coarsest level (98 vs 125 us) but
+        // costs 60 % at the hashed ones (283 vs 175 us): 3261 vs 2845 us over 16 levels
+        static const int merge = env_mode("NERF_HG_MERGE", 0);
+        launch(walk, merge != 0, blocks, s, a, pl, grad_out, g_ld, gt, gmax, acc);
         NERF_CHECK_LAUNCH();
     }
     int64_t fb = (count + 255) / 256;

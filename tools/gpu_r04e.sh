@@ -11,7 +11,7 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 timeout -k 10 600 python -u -m pytest tests/test_gpu_wgrad_tr.py tests/test_gpu_wgrad_rays.py tests/test_gpu_direct_sink.py \
   tests/test_gpu_fused.py tests/test_gpu_fused_composite.py tests/test_gpu_fused_encoding.py tests/test_hashgrid.py \
-  tests/test_gpu_frame_render.py tests/test_capi.py tests/test_gpu_dp_equivalence.py \
+  tests/test_gpu_frame_render.py tests/test_capi.py \
   -m gpu -x -q --timeout 240 --timeout-method thread > "$OUT/tests.txt" 2>&1 || { echo "tests failed: $?"; tail -40 "$OUT/tests.txt"; exit 1; }
 tail -2 "$OUT/tests.txt"
 for v in "2" "1" "0"; do
