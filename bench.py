@@ -625,7 +625,7 @@ def frame_render(ren, wl: dict, device, name: str, H: int = 800, W: int = 800):
     ms = s.elapsed_time(e)
     ks = timer.summary()
     spr = wl["coarse"] + wl["fine"]
-    return {"view": f"{H}x{W} ({B} rays x {spr} samples), batches of 65536 rays through forward, clip to [0, 1]",
+    return {"view": f"{H}x{W} ({B} rays x {spr} samples), batches of up to 65536 rays through forward (render_image: at most 2 GB of fused-pass rows per batch), clip to [0, 1]",
             "ms": ms, "ray_samples_per_s": B * spr / (ms * 1e-3),
             "launches": {k: v["launches"] for k, v in ks.items()},
             "encode_launches": ks.get("encode_fwd", {}).get("launches", 0),

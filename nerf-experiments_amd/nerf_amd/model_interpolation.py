@@ -298,6 +298,12 @@ class NerfInterpolation(nn.Module):
         if not isinstance(pixel_width, th.Tensor):
             pixel_width = th.full((n, 1), float(pixel_width), device=ray_origs.device)
         out = th.empty(n, 3, device=ray_origs.device, dtype=th.float32)
+        # the fused field-MLP launch addresses a pass's [samples, 260] fp32 rows with 32-bit offsets
+        # (mlp_fused.eligible): batches of at most 2 GB of them per pass, so that every batch takes it
+        # (rays are independent: the image does not depend on the batching)
+        spr = max(int(self.samples_per_ray_radiance), int(self.samples_per_ray_proposal or 0), 1)
+        while batch_size > 1024 and batch_size * spr * 272 * 4 >= (1 << 31):
+            batch_size //= 2
         for i in range(0, n, batch_size):
             j = min(n, i + batch_size)
             out[i:j] = self.forward(ray_origs[i:j], ray_dirs[i:j], pixel_width[i:j])[0].clip(0, 1)
