@@ -301,7 +301,17 @@ constexpr int BWD_UNROLL = 4;
 // One part's walk over the samples [n_begin, n_end): every corner contribution whose row falls in
 // the part [row0, row0 + prow) of level l, added to the LDS accumulators.  g: the level's F values of
 // sample n at gt[n F + f] when restaged level-major (gt != null), else at g[n ld + l F + f].
-template <int F>
+// round-to-nearest-even of |x| < 2^51 to int64 (llrint's value): adding 1.5 * 2^52 rounds x to an
+// integer in the binade [2^52, 2^53), whose mantissa bits then hold it — 3 instructions, not ~8
+__device__ __forceinline__ long long rint_fixed(double x) {
+#pragma clang fp contract(off)
+    const double m = 6755399441055744.0;
+    return __builtin_bit_cast(long long, x + m) - __builtin_bit_cast(long long, m);
+}
+
+// SMALL: a.n >= 256, so that every contribution |w g 2^s| <= gmax 2^s < 2^62 / (8 n) <= 2^51 rounds
+// with rint_fixed
+template <int F, bool SMALL>
 __device__ __forceinline__ void walk_part(const HashArgs& a, int l, int res, int64_t row0, int prow, double scale,
                                           int64_t n_begin, int64_t n_end, const float* __restrict__ g, int64_t ld,
                                           const float* __restrict__ gt, unsigned long long* part) {
@@ -350,17 +360,20 @@ __device__ __forceinline__ void walk_part(const HashArgs& a, int l, int res, int
         for (int u = 0; u < BWD_UNROLL; ++u) {
             if (nb + u * BWD_THREADS >= n_end) continue;
             const Corners c = level_corners(p[u], a.p.normalize, res, T, a.p.primes);
+            // w g 2^s = w (g 2^s): both products exact in fp64 (24-bit mantissas, power-of-two scale)
+            double gs[F];
+#pragma unroll
+            for (int f = 0; f < F; ++f) gs[f] = (double)gv[u][f] * scale;
             // An LDS atomic costs the same per wave-instruction however few lanes are active, and a
             // part holds only ~1/parts of a sample's corners: so each lane queues its in-range
             // corners and the wave issues one add per queued-corner round (its longest queue)
-            // instead of one per corner.
+            // instead of one per corner.  Rows and part bounds are < T < 2^31: 32-bit offsets.
             unsigned pend = 0;
             int rel[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                const int64_t r = (int64_t)c.idx[k] - row0;
-                rel[k] = (int)r;
-                if ((uint64_t)r < (uint64_t)prow) pend |= 1u << k;
+                rel[k] = c.idx[k] - (int)row0;
+                if ((unsigned)rel[k] < (unsigned)prow) pend |= 1u << k;
             }
             while (pend != 0u) {
                 const int k = __builtin_ctz(pend);
@@ -375,8 +388,9 @@ __device__ __forceinline__ void walk_part(const HashArgs& a, int l, int res, int
                     }
 #pragma unroll
                 for (int f = 0; f < F; ++f) {
-                    // w * g is exact in fp64 (two 24-bit mantissas); one rounding to the fixed-point grid
-                    const long long q = llrint((double)wk * (double)gv[u][f] * scale);
+                    // one rounding to the fixed-point grid
+                    const double x = (double)wk * gs[f];
+                    const long long q = SMALL ? rint_fixed(x) : llrint(x);
                     if (q != 0) atomicAdd(&part[rk * F + f], (unsigned long long)q);
                 }
             }
@@ -535,9 +549,12 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_kernel(HashArgs a, B
     if constexpr (MERGED)
         walk_part_merged<F>(a, l, a.p.res[l], row0, prow, scale, slab * pl.slab, n1, g, ld,
                             gt ? gt + (int64_t)l * a.n * F : nullptr, part);
+    else if (a.n >= 256)
+        walk_part<F, true>(a, l, a.p.res[l], row0, prow, scale, slab * pl.slab, n1, g, ld,
+                           gt ? gt + (int64_t)l * a.n * F : nullptr, part);
     else
-        walk_part<F>(a, l, a.p.res[l], row0, prow, scale, slab * pl.slab, n1, g, ld,
-                     gt ? gt + (int64_t)l * a.n * F : nullptr, part);
+        walk_part<F, false>(a, l, a.p.res[l], row0, prow, scale, slab * pl.slab, n1, g, ld,
+                            gt ? gt + (int64_t)l * a.n * F : nullptr, part);
     __syncthreads();
     flush_part<F>(a, l, row0, prow, part, acc);
 }
@@ -575,9 +592,12 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_walk_kernel(HashArgs
         }
         const int64_t n0 = slab * pl.slab;
         const int64_t n1 = n0 + pl.slab < a.n ? n0 + pl.slab : a.n;
-        if (n0 < n1)
-            walk_part<F>(a, l, a.p.res[l], row0, prow, scale, n0, n1, g, ld,
-                         gt ? gt + (int64_t)l * a.n * F : nullptr, part);
+        if (n0 < n1 && a.n >= 256)
+            walk_part<F, true>(a, l, a.p.res[l], row0, prow, scale, n0, n1, g, ld,
+                               gt ? gt + (int64_t)l * a.n * F : nullptr, part);
+        else if (n0 < n1)
+            walk_part<F, false>(a, l, a.p.res[l], row0, prow, scale, n0, n1, g, ld,
+                                gt ? gt + (int64_t)l * a.n * F : nullptr, part);
     }
     if (cur >= 0) {
         __syncthreads();

@@ -37,20 +37,61 @@ __device__ __forceinline__ int hash_row(const long long* cc, long long pr0, long
 
 // x_hat = (x / 8 + 0.5) * r (normalize) or x * r; corners floor(x_hat) + {0,1}^3 in the reference's
 // stacking order (z fastest), their rows (bijective: clipped x + (r+1) y + (r+1)^2 z; else the
-// hash) and weights prod_d (1 - |x_hat_d - corner_d|) on the unclipped corner
+// hash) and weights prod_d (1 - |x_hat_d - corner_d|) on the unclipped corner.
+// The corner coordinates are the reference's int64 floor values; while |x_hat| < 2^30 (any position
+// within 2^26 of the scene at r <= 2^20, normalised by 8) they are carried in 32-bit integers, whose
+// sums, conversions to float and low 32 bits of the hash products equal the 64-bit ones exactly, and
+// the two per-dimension weight factors are formed once (the same expressions); beyond that, or for a
+// table size that is not a power of two (64-bit remainder), the 64-bit form.
 template <typename PR>
 __device__ __forceinline__ Corners level_corners(const float* p, int normalize, int r, int T, const PR& primes) {
 #pragma clang fp contract(off)
     Corners c;
     float xh[3];
-    long long base[3];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        xh[j] = (normalize ? (p[j] / 8.0f + 0.5f) : p[j]) * (float)r;
-        base[j] = (long long)floorf(xh[j]);
-    }
+    for (int j = 0; j < 3; ++j) xh[j] = (normalize ? (p[j] / 8.0f + 0.5f) : p[j]) * (float)r;
     const bool bij = (long long)(r + 1) * (r + 1) * (r + 1) <= (long long)T;
     const bool pow2 = (T & (T - 1)) == 0;
+    const bool small = fabsf(xh[0]) < 1073741824.0f && fabsf(xh[1]) < 1073741824.0f && fabsf(xh[2]) < 1073741824.0f;
+    if (small && (bij || pow2)) {
+        int b[3];
+        float f0[3], f1[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            b[j] = (int)floorf(xh[j]);
+            f0[j] = 1.0f - fabsf(xh[j] - (float)b[j]);
+            f1[j] = 1.0f - fabsf(xh[j] - (float)(b[j] + 1));
+        }
+        const unsigned pr0 = (unsigned)(long long)primes[0], pr1 = (unsigned)(long long)primes[1],
+                       pr2 = (unsigned)(long long)primes[2];
+        unsigned hx[2], hy[2], hz[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            hx[e] = (unsigned)(b[0] + e) * pr0;
+            hy[e] = (unsigned)(b[1] + e) * pr1;
+            hz[e] = (unsigned)(b[2] + e) * pr2;
+        }
+        const int r1 = r + 1;
+        int q[3][2];
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int v = b[j] + e;
+                q[j][e] = v < 0 ? 0 : (v > r ? r : v);
+            }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int ex = (k >> 2) & 1, ey = (k >> 1) & 1, ez = k & 1;   // z fastest
+            c.w[k] = ((ex ? f1[0] : f0[0]) * (ey ? f1[1] : f0[1])) * (ez ? f1[2] : f0[2]);
+            c.idx[k] = bij ? q[0][ex] + r1 * q[1][ey] + r1 * r1 * q[2][ez]
+                           : (int)((hx[ex] ^ hy[ey] ^ hz[ez]) & (unsigned)(T - 1));
+        }
+        return c;
+    }
+    long long base[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) base[j] = (long long)floorf(xh[j]);
     const long long pr0 = (long long)primes[0], pr1 = (long long)primes[1], pr2 = (long long)primes[2];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
