@@ -40,6 +40,7 @@ struct HashArgs {
     const float* t1;
     int64_t n;
     int spr;
+    const float4* pos;                              // backward: position records (or null)
 };
 
 __device__ __forceinline__ void sample_position(const HashArgs& a, int64_t n, float* p) {
@@ -298,9 +299,6 @@ struct BwdPlan {
 // memory round trip instead of one per load.
 constexpr int BWD_UNROLL = 4;
 
-// One part's walk over the samples [n_begin, n_end): every corner contribution whose row falls in
-// the part [row0, row0 + prow) of level l, added to the LDS accumulators.  g: the level's F values of
-// sample n at gt[n F + f] when restaged level-major (gt != null), else at g[n ld + l F + f].
 // round-to-nearest-even of |x| < 2^51 to int64 (llrint's value): adding 1.5 * 2^52 rounds x to an
 // integer in the binade [2^52, 2^53), whose mantissa bits then hold it — 3 instructions, not ~8
 __device__ __forceinline__ long long rint_fixed(double x) {
@@ -309,17 +307,131 @@ __device__ __forceinline__ long long rint_fixed(double x) {
     return __builtin_bit_cast(long long, x + m) - __builtin_bit_cast(long long, m);
 }
 
-// SMALL: a.n >= 256, so that every contribution |w g 2^s| <= gmax 2^s < 2^62 / (8 n) <= 2^51 rounds
-// with rint_fixed
+// Sample positions as float4 records (x, y, z, 0), computed once per backward call for the ray
+// form — as sample_position computes them — instead of once per part walk (97 parts at C5)
+__global__ __launch_bounds__(256) void hashgrid_pos_kernel(HashArgs a, float4* __restrict__ pos) {
+    const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (n >= a.n) return;
+    float p[3];
+    sample_position(a, n, p);
+    pos[n] = make_float4(p[0], p[1], p[2], 0.0f);
+}
+
+#ifndef NERF_HG_QUEUE
+#define NERF_HG_QUEUE 0
+#endif
+
+// One trip's corner contributions of BWD_UNROLL samples (nb + u BWD_THREADS) whose rows fall in the
+// part [row0, row0 + prow), added to the LDS accumulators.  SMALL: a.n >= 256, so that every
+// contribution |w g 2^s| <= gmax 2^s < 2^62 / (8 n) <= 2^51 rounds with rint_fixed.
+template <int F, bool SMALL>
+__device__ __forceinline__ void add_trip(const HashArgs& a, int res, int64_t row0, int prow, double scale, int64_t nb,
+                                         int64_t n_end, const float (&p)[BWD_UNROLL][3],
+                                         const float (&gv)[BWD_UNROLL][F], unsigned long long* part) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int u = 0; u < BWD_UNROLL; ++u) {
+        if (nb + u * BWD_THREADS >= n_end) continue;
+        const Corners c = level_corners(p[u], a.p.normalize, res, a.p.table_size, a.p.primes);
+        // w g 2^s = w (g 2^s): both products exact in fp64 (24-bit mantissas, power-of-two scale)
+        double gs[F];
+#pragma unroll
+        for (int f = 0; f < F; ++f) gs[f] = (double)gv[u][f] * scale;
+        int rel[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) rel[k] = c.idx[k] - (int)row0;     // rows, part bounds < T < 2^31
+        if (NERF_HG_QUEUE) {
+            // each lane queues its in-range corners and the wave issues one add per queued-corner
+            // round (its longest queue), selecting the corner's row and weight per round
+            unsigned pend = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if ((unsigned)rel[k] < (unsigned)prow) pend |= 1u << k;
+            while (pend != 0u) {
+                const int k = __builtin_ctz(pend);
+                pend &= pend - 1u;
+                int rk = rel[0];
+                float wk = c.w[0];
+#pragma unroll
+                for (int j = 1; j < 8; ++j)
+                    if (k == j) {
+                        rk = rel[j];
+                        wk = c.w[j];
+                    }
+#pragma unroll
+                for (int f = 0; f < F; ++f) {
+                    // one rounding to the fixed-point grid
+                    const double x = (double)wk * gs[f];
+                    const long long q = SMALL ? rint_fixed(x) : llrint(x);
+                    if (q != 0) atomicAdd(&part[rk * F + f], (unsigned long long)q);
+                }
+            }
+        } else {
+            // corner by corner, the lanes whose corner falls in the part (a corner no lane holds is
+            // skipped): no per-round selection of the row and weight
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if ((unsigned)rel[k] < (unsigned)prow) {
+                    const double wk = (double)c.w[k];
+#pragma unroll
+                    for (int f = 0; f < F; ++f) {
+                        const double x = wk * gs[f];
+                        const long long q = SMALL ? rint_fixed(x) : llrint(x);
+                        if (q != 0) atomicAdd(&part[rel[k] * F + f], (unsigned long long)q);
+                    }
+                }
+            }
+        }
+    }
+}
+
+#ifndef NERF_HG_PIPE
+#define NERF_HG_PIPE 1
+#endif
+
+// One part's walk over the samples [n_begin, n_end): every corner contribution whose row falls in
+// the part [row0, row0 + prow) of level l, added to the LDS accumulators.  g: the level's F values of
+// sample n at gt[n F + f] when restaged level-major (gt != null), else at g[n ld + l F + f].
+// Positions from the float4 records (a.pos, hashgrid_pos_kernel) when present: two loads per sample,
+// the next trip's issued before this trip's corners (NERF_HG_PIPE), so a wave waits on memory once
+// per walk instead of once per trip; else from the inputs (x, or ray o / d and the interval).
 template <int F, bool SMALL>
 __device__ __forceinline__ void walk_part(const HashArgs& a, int l, int res, int64_t row0, int prow, double scale,
                                           int64_t n_begin, int64_t n_end, const float* __restrict__ g, int64_t ld,
                                           const float* __restrict__ gt, unsigned long long* part) {
 #pragma clang fp contract(off)
-    const int T = a.p.table_size;
+    constexpr int STEP = BWD_UNROLL * BWD_THREADS;
     const bool rays = a.x == nullptr, mid = a.p.query != 0, small = a.n < ((int64_t)1 << 31);
-    // samples past the range are masked, their loads clamped into it
-    for (int64_t base = n_begin; base < n_end; base += BWD_UNROLL * BWD_THREADS) {
+    if (a.pos != nullptr) {
+        float4 qn[BWD_UNROLL];
+        float gn[BWD_UNROLL][F];
+        // indices clamped into the range, so every load is in bounds; samples past it are masked
+        auto load = [&](int64_t base) __attribute__((always_inline)) {
+#pragma unroll
+            for (int u = 0; u < BWD_UNROLL; ++u) {
+                const int64_t n = base + threadIdx.x + u * BWD_THREADS < n_end ? base + threadIdx.x + u * BWD_THREADS
+                                                                               : n_end - 1;
+                qn[u] = a.pos[n];
+#pragma unroll
+                for (int f = 0; f < F; ++f) gn[u][f] = gt ? gt[n * F + f] : g[n * ld + (int64_t)l * F + f];
+            }
+        };
+        load(n_begin);
+        for (int64_t base = n_begin; base < n_end; base += STEP) {
+            float p[BWD_UNROLL][3], gv[BWD_UNROLL][F];
+#pragma unroll
+            for (int u = 0; u < BWD_UNROLL; ++u) {
+                p[u][0] = qn[u].x, p[u][1] = qn[u].y, p[u][2] = qn[u].z;
+#pragma unroll
+                for (int f = 0; f < F; ++f) gv[u][f] = gn[u][f];
+            }
+            if (NERF_HG_PIPE && base + STEP < n_end) load(base + STEP);
+            add_trip<F, SMALL>(a, res, row0, prow, scale, base + threadIdx.x, n_end, p, gv, part);
+            if (!NERF_HG_PIPE && base + STEP < n_end) load(base + STEP);
+        }
+        return;
+    }
+    for (int64_t base = n_begin; base < n_end; base += STEP) {
         const int64_t nb = base + threadIdx.x;
         float p[BWD_UNROLL][3], gv[BWD_UNROLL][F];
         // loads first (indices clamped into the range, so every load is in bounds) ...
@@ -356,45 +468,7 @@ __device__ __forceinline__ void walk_part(const HashArgs& a, int l, int res, int
                 for (int f = 0; f < F; ++f) gv[u][f] = gt ? gt[n * F + f] : g[n * ld + (int64_t)l * F + f];
             }
         }
-#pragma unroll
-        for (int u = 0; u < BWD_UNROLL; ++u) {
-            if (nb + u * BWD_THREADS >= n_end) continue;
-            const Corners c = level_corners(p[u], a.p.normalize, res, T, a.p.primes);
-            // w g 2^s = w (g 2^s): both products exact in fp64 (24-bit mantissas, power-of-two scale)
-            double gs[F];
-#pragma unroll
-            for (int f = 0; f < F; ++f) gs[f] = (double)gv[u][f] * scale;
-            // An LDS atomic costs the same per wave-instruction however few lanes are active, and a
-            // part holds only ~1/parts of a sample's corners: so each lane queues its in-range
-            // corners and the wave issues one add per queued-corner round (its longest queue)
-            // instead of one per corner.  Rows and part bounds are < T < 2^31: 32-bit offsets.
-            unsigned pend = 0;
-            int rel[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                rel[k] = c.idx[k] - (int)row0;
-                if ((unsigned)rel[k] < (unsigned)prow) pend |= 1u << k;
-            }
-            while (pend != 0u) {
-                const int k = __builtin_ctz(pend);
-                pend &= pend - 1u;
-                int rk = rel[0];
-                float wk = c.w[0];
-#pragma unroll
-                for (int j = 1; j < 8; ++j)
-                    if (k == j) {
-                        rk = rel[j];
-                        wk = c.w[j];
-                    }
-#pragma unroll
-                for (int f = 0; f < F; ++f) {
-                    // one rounding to the fixed-point grid
-                    const double x = (double)wk * gs[f];
-                    const long long q = SMALL ? rint_fixed(x) : llrint(x);
-                    if (q != 0) atomicAdd(&part[rk * F + f], (unsigned long long)q);
-                }
-            }
-        }
+        add_trip<F, SMALL>(a, res, row0, prow, scale, nb, n_end, p, gv, part);
     }
 }
 
@@ -740,9 +814,11 @@ using namespace nerf;
 size_t gt_offset(const nerf_hashgrid_params* params) { return (nerf_hashgrid_workspace(params) + 255) & ~(size_t)255; }
 }  // namespace
 
+// [header + accumulators][position records: n float4][grad_out restaged level-major: L n F floats]
 extern "C" size_t nerf_hashgrid_workspace_n(const nerf_hashgrid_params* params, int64_t n_samples) {
     if (!valid_params(params) || n_samples < 0) return 0;
-    return gt_offset(params) + (size_t)n_samples * params->levels * params->features * sizeof(float);
+    return gt_offset(params) + (size_t)n_samples * sizeof(float4) +
+           (size_t)n_samples * params->levels * params->features * sizeof(float);
 }
 
 extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float* x, const float* ray_o,
@@ -762,9 +838,20 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
     // header and accumulators zeroed by every call (no state carried between calls)
     if (hipMemsetAsync(workspace, 0, 256 + (size_t)count * sizeof(unsigned long long), s) != hipSuccess)
         return NERF_ERR_LAUNCH;
-    const HashArgs a = make_args(params, x, ray_o, ray_d, t_start, t_end, n_samples, samples_per_ray);
+    HashArgs a = make_args(params, x, ray_o, ray_d, t_start, t_end, n_samples, samples_per_ray);
     if (n_samples > 0) {
         const int cols = params->levels * params->features;
+        const bool room = workspace_bytes >= nerf_hashgrid_workspace_n(params, n_samples);
+        char* const tail = static_cast<char*>(workspace) + gt_offset(params);
+        // NERF_HG_POS (default 1): the ray form's positions computed once into float4 records when the
+        // workspace has room (nerf_hashgrid_workspace_n), instead of in every part walk
+        static const int pos_mode = env_mode("NERF_HG_POS", 1);
+        if (pos_mode == 1 && room && x == nullptr && (n_samples + 255) / 256 < (1ll << 31)) {
+            float4* pos = reinterpret_cast<float4*>(tail);
+            hipLaunchKernelGGL(hashgrid_pos_kernel, dim3((unsigned)((n_samples + 255) / 256)), dim3(256), 0, s, a, pos);
+            NERF_CHECK_LAUNCH();
+            a.pos = pos;
+        }
         // grad_out restaged level-major (with its max) when the workspace has room for it
         // (nerf_hashgrid_workspace_n) and the walks read it (NERF_HG_BWD: 0 (default) the per-item grid
         // on the rows; 1 the per-item grid over the restaged values; 2 the persistent walk over them).
@@ -774,9 +861,8 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
         static const int mode = env_mode("NERF_HG_BWD", 0);
         const int F = params->features;
         float* gt = nullptr;
-        if (mode >= 1 && workspace_bytes >= nerf_hashgrid_workspace_n(params, n_samples) && (F == 1 || F == 2 || F == 4) &&
-            (n_samples + TILE_SAMPLES - 1) / TILE_SAMPLES < (1ll << 31)) {
-            gt = reinterpret_cast<float*>(static_cast<char*>(workspace) + gt_offset(params));
+        if (mode >= 1 && room && (F == 1 || F == 2 || F == 4) && (n_samples + TILE_SAMPLES - 1) / TILE_SAMPLES < (1ll << 31)) {
+            gt = reinterpret_cast<float*>(tail + (size_t)n_samples * sizeof(float4));
             if (F == 1) launch_gtr<1>(s, grad_out, g_ld, n_samples, params->levels, gt, gmax);
             else if (F == 2) launch_gtr<2>(s, grad_out, g_ld, n_samples, params->levels, gt, gmax);
             else launch_gtr<4>(s, grad_out, g_ld, n_samples, params->levels, gt, gmax);

@@ -62,30 +62,34 @@ __device__ __forceinline__ Corners level_corners(const float* p, int normalize, 
             f0[j] = 1.0f - fabsf(xh[j] - (float)b[j]);
             f1[j] = 1.0f - fabsf(xh[j] - (float)(b[j] + 1));
         }
-        const unsigned pr0 = (unsigned)(long long)primes[0], pr1 = (unsigned)(long long)primes[1],
-                       pr2 = (unsigned)(long long)primes[2];
-        unsigned hx[2], hy[2], hz[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            hx[e] = (unsigned)(b[0] + e) * pr0;
-            hy[e] = (unsigned)(b[1] + e) * pr1;
-            hz[e] = (unsigned)(b[2] + e) * pr2;
-        }
-        const int r1 = r + 1;
-        int q[3][2];
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
+        // the row form is uniform per level: one branch for all eight corners
+        if (bij) {
+            const int r1 = r + 1;
+            int qx[2], qy[2], qz[2];
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
-                const int v = b[j] + e;
-                q[j][e] = v < 0 ? 0 : (v > r ? r : v);
+                const int vx = b[0] + e, vy = b[1] + e, vz = b[2] + e;
+                qx[e] = vx < 0 ? 0 : (vx > r ? r : vx);
+                qy[e] = r1 * (vy < 0 ? 0 : (vy > r ? r : vy));
+                qz[e] = r1 * r1 * (vz < 0 ? 0 : (vz > r ? r : vz));
             }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) c.idx[k] = qx[(k >> 2) & 1] + qy[(k >> 1) & 1] + qz[k & 1];
+        } else {
+            const unsigned pr0 = (unsigned)(long long)primes[0], pr1 = (unsigned)(long long)primes[1],
+                           pr2 = (unsigned)(long long)primes[2];
+            unsigned hxy[4], hz[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) hz[e] = (unsigned)(b[2] + e) * pr2;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) hxy[e] = ((unsigned)(b[0] + (e >> 1)) * pr0) ^ ((unsigned)(b[1] + (e & 1)) * pr1);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) c.idx[k] = (int)((hxy[k >> 1] ^ hz[k & 1]) & (unsigned)(T - 1));
+        }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const int ex = (k >> 2) & 1, ey = (k >> 1) & 1, ez = k & 1;   // z fastest
             c.w[k] = ((ex ? f1[0] : f0[0]) * (ey ? f1[1] : f0[1])) * (ez ? f1[2] : f0[2]);
-            c.idx[k] = bij ? q[0][ex] + r1 * q[1][ey] + r1 * r1 * q[2][ez]
-                           : (int)((hx[ex] ^ hy[ey] ^ hz[ez]) & (unsigned)(T - 1));
         }
         return c;
     }
