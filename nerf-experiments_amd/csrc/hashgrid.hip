@@ -317,6 +317,9 @@ __global__ __launch_bounds__(256) void hashgrid_pos_kernel(HashArgs a, float4* _
     pos[n] = make_float4(p[0], p[1], p[2], 0.0f);
 }
 
+#ifndef NERF_HG_SKIPZERO
+#define NERF_HG_SKIPZERO 0
+#endif
 #ifndef NERF_HG_QUEUE
 #define NERF_HG_QUEUE 0
 #endif
@@ -377,7 +380,7 @@ __device__ __forceinline__ void add_trip(const HashArgs& a, int res, int64_t row
                     for (int f = 0; f < F; ++f) {
                         const double x = wk * gs[f];
                         const long long q = SMALL ? rint_fixed(x) : llrint(x);
-                        if (q != 0) atomicAdd(&part[rel[k] * F + f], (unsigned long long)q);
+                        if (!NERF_HG_SKIPZERO || q != 0) atomicAdd(&part[rel[k] * F + f], (unsigned long long)q);
                     }
                 }
             }
@@ -898,9 +901,29 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
             const int64_t items = (int64_t)pl.parts * pl.nslab;
             blocks = items < G ? items : G;
         } else {
-            // about four workgroups per CU in all, slabs of at least 4096 samples
-            int64_t slabs = (1024 + pl.parts - 1) / pl.parts;
+            // slabs of at least 4096 samples; the grid runs one 1024-thread workgroup per CU at a time,
+            // so its time goes as ceil(slabs parts / CUs) rounds of 1/slabs of the samples each: the
+            // slab count minimising that (the fewest slabs within 1 %: fewer flushes of parts) from
+            // three rounds up to twice four workgroups per CU (97 parts at C5: 13 slabs, 1261 workgroups =
+            // 4.93 rounds; four per CU gave 11, 1067 = 4.17 rounds, the last one a sixth full).
+            // NERF_HG_SLABS=0: four per CU; =k: k slabs.
+            static const int slab_env = [] {
+                const char* e = getenv("NERF_HG_SLABS");
+                return e ? atoi(e) : -1;
+            }();
             const int64_t most = (n_samples + 4095) / 4096;
+            const int64_t G = num_cus(), four = (1024 + pl.parts - 1) / pl.parts;
+            int64_t slabs = four;
+            if (slab_env > 0) {
+                slabs = slab_env;
+            } else if (slab_env < 0) {
+                double best = 1e30;
+                const int64_t k0 = (3 * G + pl.parts - 1) / pl.parts, k1 = k0 > 2 * four ? k0 : 2 * four;
+                for (int64_t k = k0; k <= k1; ++k) {
+                    const double c = (double)((k * pl.parts + G - 1) / G) / (double)k;
+                    if (c < 0.99 * best) best = c, slabs = k;
+                }
+            }
             slabs = slabs < most ? slabs : most;
             pl.slab = (n_samples + slabs - 1) / slabs;
             pl.nslab = slabs;
