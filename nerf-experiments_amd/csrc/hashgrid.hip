@@ -395,9 +395,10 @@ __device__ __forceinline__ void add_trip(const HashArgs& a, int res, int64_t row
 // One part's walk over the samples [n_begin, n_end): every corner contribution whose row falls in
 // the part [row0, row0 + prow) of level l, added to the LDS accumulators.  g: the level's F values of
 // sample n at gt[n F + f] when restaged level-major (gt != null), else at g[n ld + l F + f].
-// Positions from the float4 records (a.pos, hashgrid_pos_kernel) when present: two loads per sample,
-// the next trip's issued before this trip's corners (NERF_HG_PIPE), so a wave waits on memory once
-// per walk instead of once per trip; else from the inputs (x, or ray o / d and the interval).
+// Positions from the float4 records (a.pos, hashgrid_pos_kernel; NERF_HG_POS=1) when present: two
+// loads per sample, the next trip's issued before this trip's corners (NERF_HG_PIPE); measured no
+// faster than the walks' own position arithmetic (profiles/r04n: the walk is not load-latency
+// bound); else from the inputs (x, or ray o / d and the interval).
 template <int F, bool SMALL>
 __device__ __forceinline__ void walk_part(const HashArgs& a, int l, int res, int64_t row0, int prow, double scale,
                                           int64_t n_begin, int64_t n_end, const float* __restrict__ g, int64_t ld,
@@ -846,9 +847,10 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
         const int cols = params->levels * params->features;
         const bool room = workspace_bytes >= nerf_hashgrid_workspace_n(params, n_samples);
         char* const tail = static_cast<char*>(workspace) + gt_offset(params);
-        // NERF_HG_POS (default 1): the ray form's positions computed once into float4 records when the
-        // workspace has room (nerf_hashgrid_workspace_n), instead of in every part walk
-        static const int pos_mode = env_mode("NERF_HG_POS", 1);
+        // NERF_HG_POS=1: the ray form's positions computed once into float4 records when the workspace
+        // has room (nerf_hashgrid_workspace_n), instead of in every part walk; bitwise the same, and
+        // measured no faster (2.68 vs 2.65 ms per ingp step, profiles/r04n): off by default
+        static const int pos_mode = env_mode("NERF_HG_POS", 0);
         if (pos_mode == 1 && room && x == nullptr && (n_samples + 255) / 256 < (1ll << 31)) {
             float4* pos = reinterpret_cast<float4*>(tail);
             hipLaunchKernelGGL(hashgrid_pos_kernel, dim3((unsigned)((n_samples + 255) / 256)), dim3(256), 0, s, a, pos);

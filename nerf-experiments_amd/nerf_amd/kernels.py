@@ -706,12 +706,15 @@ def hashgrid_fwd(params, table: torch.Tensor, out: torch.Tensor, *, x=None, ray_
 
 
 def hashgrid_workspace_bytes(params, n_samples: int | None = None) -> int:
-    """nerf_hashgrid_workspace(params), or with n_samples nerf_hashgrid_workspace_n: room for grad_out
-    restaged level-major as well (the backward's part walks then read contiguous values)."""
-    acc = 256 + hashgrid_table_rows(params) * params.features * 8
-    if n_samples is None:
-        return acc
-    return ((acc + 255) // 256) * 256 + int(n_samples) * params.levels * params.features * 4
+    """nerf_hashgrid_workspace(params), or with n_samples nerf_hashgrid_workspace_n: room for the ray
+    form's float4 position records (computed once per backward instead of in every part walk) and
+    grad_out restaged level-major as well.  The library's own sizes, not a restatement of them."""
+    lib = _lib.load()
+    size = lib.nerf_hashgrid_workspace(ctypes.byref(params)) if n_samples is None \
+        else lib.nerf_hashgrid_workspace_n(ctypes.byref(params), int(n_samples))
+    if size == 0:
+        raise ValueError("invalid hash-grid parameters")
+    return int(size)
 
 
 def hashgrid_bwd(params, grad_out: torch.Tensor, grad_table: torch.Tensor, workspace: torch.Tensor, *, x=None,
