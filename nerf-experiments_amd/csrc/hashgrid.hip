@@ -683,6 +683,175 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_walk_kernel(HashArgs
     }
 }
 
+// ---- Bucketed backward for the hashed levels (NERF_HG_BUCKET): the walk above re-derives every
+// sample's corners once per 160 KB part (7 parts per 2^16-row level at C5).  Instead one pass
+// derives each (sample, hashed level)'s corners once and files the (sample, row in part, weight)
+// contributions into per-(level, part) buckets of the workspace; a second pass per bucket chunk adds
+// them to its part in LDS with every lane active, and flushes the part as the walk does.  Integer
+// fixed-point sums: bitwise the walk's result in any order.  A bucket's contributions past its
+// capacity (sized 1.25x the uniform share plus a margin; the hash spreads rows evenly) go straight
+// to the global accumulators, so no input can lose one.
+constexpr int BUCKET_MAXP = 64;
+// Every bucket is split into BUCKET_SUB sub-buckets with their own fill counters: pass-A workgroup w
+// files into sub-bucket w % BUCKET_SUB, so a counter takes the atomics of 1/16 of the workgroups, all
+// on one XCD (workgroups are dealt to the 8 XCDs round-robin) — one shared counter per bucket took
+// one same-address global atomic per workgroup (5120 at C5's fine pass), serialised in L2
+constexpr int BUCKET_SUB = 16;
+
+struct BucketPlan {
+    int first;              // first hashed level: levels first .. L-1 are bucketed
+    int nparts;             // parts per hashed level (ceil(T / rpp))
+    int rpp;                // rows per part
+    int chunks;             // pass-B workgroups per bucket (one per sub-bucket)
+    int64_t cap;            // entries per sub-bucket
+    unsigned* count;        // [(L - first) * nparts][BUCKET_SUB] entries filed (zeroed per call)
+    unsigned* en;           // [bucket][sub][cap] sample
+    unsigned* er;           // [bucket][sub][cap] row within the part
+    float* ew;              // [bucket][sub][cap] corner weight
+};
+
+template <int F>
+__global__ __launch_bounds__(256) void hashgrid_bucket_kernel(HashArgs a, BucketPlan bp, const float* __restrict__ g,
+                                                              int64_t ld, const unsigned* __restrict__ gmax,
+                                                              unsigned long long* __restrict__ acc) {
+#pragma clang fp contract(off)
+    __shared__ unsigned cnt[BUCKET_MAXP], base[BUCKET_MAXP];
+    const int s = fixed_shift(*gmax, a.n);
+    if (s == -1000) return;                         // uniform: the finish pass writes NaN
+    const int l = bp.first + (int)blockIdx.y, P = bp.nparts;
+    const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (threadIdx.x < P) cnt[threadIdx.x] = 0u;
+    __syncthreads();
+    const bool valid = n < a.n;
+    Corners c;
+    int pk[8];
+    unsigned slot[8];
+    if (valid) {
+        float p[3];
+        sample_position(a, n, p);
+        c = level_corners(p, a.p.normalize, a.p.res[l], a.p.table_size, a.p.primes);
+    }
+    // slots: per corner, the wave's lanes grouped by part (one ballot per part present), ranks and
+    // per-part running counts in registers (lane p holds part p's), then ONE LDS add per wave for
+    // all its parts — no atomic round trip inside the loop
+    const int lane = threadIdx.x & 63;
+    unsigned runv = 0;                              // lane p: this wave's entries for part p so far
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        pk[k] = valid ? (int)((unsigned)c.idx[k] / (unsigned)bp.rpp) : -1;
+        unsigned long long rest = __ballot(valid);
+        while (rest != 0ull) {
+            const int leader = __builtin_ctzll(rest);
+            const int pp = __builtin_amdgcn_readlane(pk[k], leader);
+            const unsigned long long m = __ballot(pk[k] == pp);
+            const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+            const unsigned run = __builtin_amdgcn_readlane(runv, pp);
+            if (pk[k] == pp) slot[k] = run + rank;
+            if (lane == pp) runv += (unsigned)__builtin_popcountll(m);
+            rest &= ~m;
+        }
+    }
+    const unsigned wbase = (lane < P && runv != 0u) ? atomicAdd(&cnt[lane], runv) : 0u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) slot[k] += (unsigned)__shfl((int)wbase, pk[k] < 0 ? 0 : pk[k], 64);
+    __syncthreads();
+    const int sub = (int)(blockIdx.x % BUCKET_SUB);
+    unsigned* const gcount = bp.count + (int64_t)(l - bp.first) * P * BUCKET_SUB + sub;
+    if (threadIdx.x < P && cnt[threadIdx.x] != 0u)
+        base[threadIdx.x] = atomicAdd(&gcount[threadIdx.x * BUCKET_SUB], cnt[threadIdx.x]);
+    __syncthreads();
+    if (!valid) return;
+    const double scale = ldexp(1.0, s);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const unsigned pos = base[pk[k]] + slot[k];
+        const int64_t b = ((int64_t)(l - bp.first) * P + pk[k]) * BUCKET_SUB + sub;
+        if (pos < (uint64_t)bp.cap) {
+            const int64_t e = b * bp.cap + pos;
+            bp.en[e] = (unsigned)n;
+            bp.er[e] = (unsigned)(c.idx[k] - pk[k] * bp.rpp);
+            bp.ew[e] = c.w[k];
+        } else {
+            // past the bucket's capacity: the contribution goes to the global accumulator directly
+#pragma unroll
+            for (int f = 0; f < F; ++f) {
+                const double x = (double)c.w[k] * ((double)g[n * ld + (int64_t)l * F + f] * scale);
+                const long long q = a.n >= 256 ? rint_fixed(x) : llrint(x);
+                if (q != 0) atomicAdd(&acc[(a.off[l] + c.idx[k]) * F + f], (unsigned long long)q);
+            }
+        }
+    }
+}
+
+// g: grad_out restaged level-major (gt[l][n][f], hashgrid_gtr_kernel): a bucket's entries come in
+// runs of nearby samples, whose F values are then adjacent (from the [n][ld] rows every entry would
+// fetch its own line, and the 7 parts' buckets are not walked together to share it in L2)
+template <int F>
+__global__ __launch_bounds__(BWD_THREADS) void hashgrid_bucket_add_kernel(HashArgs a, BucketPlan bp,
+                                                                          const float* __restrict__ gt,
+                                                                          const unsigned* __restrict__ gmax,
+                                                                          unsigned long long* __restrict__ acc) {
+#pragma clang fp contract(off)
+    __shared__ unsigned long long part[PART_ENTRIES];
+    const int s = fixed_shift(*gmax, a.n);
+    if (s == -1000) return;
+    const double scale = ldexp(1.0, s);
+    const int b = (int)(blockIdx.x / (unsigned)bp.chunks), ch = (int)(blockIdx.x % (unsigned)bp.chunks);
+    const int l = bp.first + b / bp.nparts, pi = b % bp.nparts;
+    const int64_t row0 = (int64_t)pi * bp.rpp;
+    const int64_t rows = (int64_t)a.p.table_size - row0;
+    const int prow = (int)(rows < bp.rpp ? rows : bp.rpp);
+    for (int e = threadIdx.x; e < prow * F; e += BWD_THREADS) part[e] = 0ull;
+    __syncthreads();
+    const int64_t sb = (int64_t)b * BUCKET_SUB + ch;         // chunks == BUCKET_SUB: this sub-bucket
+    const unsigned cnt = bp.count[sb];
+    const int64_t e0 = 0, e1 = cnt < (uint64_t)bp.cap ? (int64_t)cnt : bp.cap;
+    const unsigned* __restrict__ en = bp.en + sb * bp.cap;
+    const unsigned* __restrict__ er = bp.er + sb * bp.cap;
+    const float* __restrict__ ew = bp.ew + sb * bp.cap;
+    const bool fast = a.n >= 256;
+    const float* __restrict__ gl = gt + (int64_t)l * a.n * F;
+    // four entries per thread per trip, all their loads issued before any is used
+    constexpr int U = 4;
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += U * BWD_THREADS) {
+        unsigned nn[U], row[U];
+        float w[U], gv[U][F];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t eu = e + u * BWD_THREADS < e1 ? e + u * BWD_THREADS : e1 - 1;
+            nn[u] = __builtin_nontemporal_load(en + eu);
+            row[u] = __builtin_nontemporal_load(er + eu);
+            w[u] = __builtin_nontemporal_load(ew + eu);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int f = 0; f < F; ++f) gv[u][f] = gl[(int64_t)nn[u] * F + f];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (e + u * BWD_THREADS >= e1) break;
+#pragma unroll
+            for (int f = 0; f < F; ++f) {
+                // the walk's arithmetic: w (g 2^s), one rounding to the fixed-point grid
+                const double x = (double)w[u] * ((double)gv[u][f] * scale);
+                const long long q = fast ? rint_fixed(x) : llrint(x);
+                atomicAdd(&part[row[u] * F + f], (unsigned long long)q);
+            }
+        }
+    }
+    __syncthreads();
+    flush_part<F>(a, l, row0, prow, part, acc);
+}
+
+template <int F>
+void launch_bucket(hipStream_t s, const HashArgs& a, const BucketPlan& bp, int nhashed, const float* g, int64_t ld,
+                   const float* gt, const unsigned* gmax, unsigned long long* acc) {
+    hipLaunchKernelGGL(hashgrid_bucket_kernel<F>, dim3((unsigned)((a.n + 255) / 256), (unsigned)nhashed), dim3(256), 0, s,
+                       a, bp, g, ld, gmax, acc);
+    hipLaunchKernelGGL(hashgrid_bucket_add_kernel<F>, dim3((unsigned)((int64_t)nhashed * bp.nparts * bp.chunks)),
+                       dim3(BWD_THREADS), 0, s, a, bp, gt, gmax, acc);
+}
+
 template <int F>
 void launch_bwd(bool walk, bool merged, int64_t blocks, hipStream_t s, const HashArgs& a, const BwdPlan& pl, const float* g, int64_t ld,
                 const float* gt, const unsigned* gmax, unsigned long long* acc) {
@@ -816,13 +985,46 @@ extern "C" size_t nerf_hashgrid_workspace(const nerf_hashgrid_params* params) {
 namespace {
 using namespace nerf;
 size_t gt_offset(const nerf_hashgrid_params* params) { return (nerf_hashgrid_workspace(params) + 255) & ~(size_t)255; }
+size_t round256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+// The bucketed backward's share of the workspace: the hashed levels from `first` on (a level whose
+// (r+1)^3 > T; the walk keeps every level before it), nparts parts of rpp rows each, buckets of cap
+// entries per sub-bucket (1.25x the uniform share of a level's 8 n corner contributions, plus 4096).  bytes = 0:
+// not eligible (no hashed level, more than BUCKET_MAXP parts a level, or n outside [1, 2^31)).
+struct BucketLayout {
+    int first = 0, nparts = 0, rpp = 0;
+    int64_t cap = 0;
+    size_t bytes = 0;
+};
+BucketLayout bucket_layout(const nerf_hashgrid_params* p, int64_t n) {
+    BucketLayout b;
+    const int L = p->levels;
+    const int64_t T = p->table_size;
+    auto hashed = [&](int l) {
+        const int64_t r1 = (int64_t)p->res[l] + 1;
+        return r1 * r1 * r1 > T;
+    };
+    int first = L;
+    while (first > 0 && hashed(first - 1)) --first;
+    b.first = first;
+    b.rpp = PART_ENTRIES / p->features;
+    b.nparts = (int)((T + b.rpp - 1) / b.rpp);
+    if (first == L || b.nparts > BUCKET_MAXP || n < 1 || n >= ((int64_t)1 << 31)) return b;
+    b.cap = ((8 * n * 5 / 4) / ((int64_t)b.nparts * BUCKET_SUB) + 4096 + 63) / 64 * 64;
+    const int64_t nb = (int64_t)(L - first) * b.nparts * BUCKET_SUB;       // sub-buckets
+    b.bytes = round256((size_t)nb * sizeof(unsigned)) + 3 * round256((size_t)nb * b.cap * sizeof(unsigned));
+    return b;
+}
+size_t bucket_offset(const nerf_hashgrid_params* p, int64_t n) {
+    return gt_offset(p) + round256((size_t)n * sizeof(float4) + (size_t)n * p->levels * p->features * sizeof(float));
+}
 }  // namespace
 
 // [header + accumulators][position records: n float4][grad_out restaged level-major: L n F floats]
+// [bucketed backward: counts | samples | rows | weights]
 extern "C" size_t nerf_hashgrid_workspace_n(const nerf_hashgrid_params* params, int64_t n_samples) {
     if (!valid_params(params) || n_samples < 0) return 0;
-    return gt_offset(params) + (size_t)n_samples * sizeof(float4) +
-           (size_t)n_samples * params->levels * params->features * sizeof(float);
+    return bucket_offset(params, n_samples) + bucket_layout(params, n_samples).bytes;
 }
 
 extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float* x, const float* ray_o,
@@ -865,13 +1067,30 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
         // the part-major walk loses that sharing
         static const int mode = env_mode("NERF_HG_BWD", 0);
         const int F = params->features;
+        // NERF_HG_BUCKET (default 1): the hashed levels through the bucketed passes when the workspace
+        // has room (nerf_hashgrid_workspace_n), F is 1, 2 or 4 (grad_out restaged level-major for
+        // them) and the walks read the rows (NERF_HG_BWD=0, no merge); the walk keeps the levels
+        // before them.  Bitwise the walk's result; 1.31 M samples x 16 levels 1610 vs 2083 us, the
+        // ingp step 23.4 vs 24.3 ms (profiles/r04r)
+        static const int bucket_mode = env_mode("NERF_HG_BUCKET", 1);
+        static const int merge = env_mode("NERF_HG_MERGE", 0);
+        const BucketLayout bl = bucket_layout(params, n_samples);
+        const bool tile_ok = (F == 1 || F == 2 || F == 4) && (n_samples + TILE_SAMPLES - 1) / TILE_SAMPLES < (1ll << 31);
+        const bool bucket = bucket_mode == 1 && room && bl.bytes > 0 && mode == 0 && merge == 0 && tile_ok;
         float* gt = nullptr;
-        if (mode >= 1 && room && (F == 1 || F == 2 || F == 4) && (n_samples + TILE_SAMPLES - 1) / TILE_SAMPLES < (1ll << 31)) {
+        float* gt_bucket = nullptr;
+        if (bucket) {
+            gt_bucket = reinterpret_cast<float*>(tail + (size_t)n_samples * sizeof(float4));
+            if (F == 1) launch_gtr<1>(s, grad_out, g_ld, n_samples, params->levels, gt_bucket, gmax);
+            else if (F == 2) launch_gtr<2>(s, grad_out, g_ld, n_samples, params->levels, gt_bucket, gmax);
+            else launch_gtr<4>(s, grad_out, g_ld, n_samples, params->levels, gt_bucket, gmax);
+        } else if (mode >= 1 && room && tile_ok) {
             gt = reinterpret_cast<float*>(tail + (size_t)n_samples * sizeof(float4));
             if (F == 1) launch_gtr<1>(s, grad_out, g_ld, n_samples, params->levels, gt, gmax);
             else if (F == 2) launch_gtr<2>(s, grad_out, g_ld, n_samples, params->levels, gt, gmax);
             else launch_gtr<4>(s, grad_out, g_ld, n_samples, params->levels, gt, gmax);
-        } else {
+        }
+        if (gt == nullptr && gt_bucket == nullptr) {
             const bool vec = cols % 4 == 0 && g_ld % 4 == 0 && (reinterpret_cast<uintptr_t>(grad_out) & 15) == 0;
             int64_t blocks = (n_samples * (vec ? cols / 4 : cols) + 255) / 256;
             blocks = blocks < 1024 ? blocks : 1024;
@@ -890,6 +1109,7 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
             pl.start[l + 1] = pl.start[l] + (int)((rows + pl.rows_per_part - 1) / pl.rows_per_part);
         }
         pl.parts = pl.start[params->levels];
+        if (bucket) pl.parts = pl.start[bl.first];
         const bool walk = mode == 2 && gt != nullptr;
         int64_t blocks;
         if (walk) {
@@ -914,15 +1134,16 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
                 return e ? atoi(e) : -1;
             }();
             const int64_t most = (n_samples + 4095) / 4096;
-            const int64_t G = num_cus(), four = (1024 + pl.parts - 1) / pl.parts;
+            const int64_t parts = pl.parts > 0 ? pl.parts : 1;     // (0: every level bucketed)
+            const int64_t G = num_cus(), four = (1024 + parts - 1) / parts;
             int64_t slabs = four;
             if (slab_env > 0) {
                 slabs = slab_env;
             } else if (slab_env < 0) {
                 double best = 1e30;
-                const int64_t k0 = (3 * G + pl.parts - 1) / pl.parts, k1 = k0 > 2 * four ? k0 : 2 * four;
+                const int64_t k0 = (3 * G + parts - 1) / parts, k1 = k0 > 2 * four ? k0 : 2 * four;
                 for (int64_t k = k0; k <= k1; ++k) {
-                    const double c = (double)((k * pl.parts + G - 1) / G) / (double)k;
+                    const double c = (double)((k * parts + G - 1) / G) / (double)k;
                     if (c < 0.99 * best) best = c, slabs = k;
                 }
             }
@@ -947,9 +1168,33 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
         // (walk_part_merged); default 0, samples strided by the workgroup (walk_part).  Bitwise equal;
         // measured (profiles/r04g): the merge saves a fifth at the coarsest level (98 vs 125 us) but
         // costs 60 % at the hashed ones (283 vs 175 us): 3261 vs 2845 us over 16 levels
-        static const int merge = env_mode("NERF_HG_MERGE", 0);
-        launch(walk, merge != 0, blocks, s, a, pl, grad_out, g_ld, gt, gmax, acc);
-        NERF_CHECK_LAUNCH();
+        if (pl.parts > 0) {
+            launch(walk, merge != 0, blocks, s, a, pl, grad_out, g_ld, gt, gmax, acc);
+            NERF_CHECK_LAUNCH();
+        }
+        if (bucket) {
+            char* const bb = static_cast<char*>(workspace) + bucket_offset(params, n_samples);
+            const int nh = params->levels - bl.first;
+            const int64_t nb = (int64_t)nh * bl.nparts * BUCKET_SUB;           // sub-buckets
+            BucketPlan bp{};
+            bp.first = bl.first;
+            bp.nparts = bl.nparts;
+            bp.rpp = bl.rpp;
+            bp.cap = bl.cap;
+            bp.count = reinterpret_cast<unsigned*>(bb);
+            bp.en = reinterpret_cast<unsigned*>(bb + round256((size_t)nb * sizeof(unsigned)));
+            bp.er = bp.en + round256((size_t)nb * bl.cap * sizeof(unsigned)) / sizeof(unsigned);
+            bp.ew = reinterpret_cast<float*>(bp.er + round256((size_t)nb * bl.cap * sizeof(unsigned)) / sizeof(unsigned));
+            if (hipMemsetAsync(bp.count, 0, (size_t)nb * sizeof(unsigned), s) != hipSuccess) return NERF_ERR_LAUNCH;
+            bp.chunks = BUCKET_SUB;
+            switch (params->features) {
+                case 1: launch_bucket<1>(s, a, bp, nh, grad_out, g_ld, gt_bucket, gmax, acc); break;
+                case 2: launch_bucket<2>(s, a, bp, nh, grad_out, g_ld, gt_bucket, gmax, acc); break;
+                case 4: launch_bucket<4>(s, a, bp, nh, grad_out, g_ld, gt_bucket, gmax, acc); break;
+                default: break;                         // (bucket requires F = 1, 2 or 4)
+            }
+            NERF_CHECK_LAUNCH();
+        }
     }
     int64_t fb = (count + 255) / 256;
     fb = fb < 4096 ? fb : 4096;
