@@ -710,6 +710,12 @@ struct BucketPlan {
     float* ew;              // [bucket][sub][cap] corner weight
 };
 
+#ifndef NERF_HG_BUCKET_LOOP
+#define NERF_HG_BUCKET_LOOP 1
+#endif
+
+// Pass A.  NERF_HG_BUCKET_LOOP (default 1): each workgroup's 256 samples through every hashed level
+// (positions derived once); 0: one level per workgroup (grid y).
 template <int F>
 __global__ __launch_bounds__(256) void hashgrid_bucket_kernel(HashArgs a, BucketPlan bp, const float* __restrict__ g,
                                                               int64_t ld, const unsigned* __restrict__ gmax,
@@ -718,66 +724,70 @@ __global__ __launch_bounds__(256) void hashgrid_bucket_kernel(HashArgs a, Bucket
     __shared__ unsigned cnt[BUCKET_MAXP], base[BUCKET_MAXP];
     const int s = fixed_shift(*gmax, a.n);
     if (s == -1000) return;                         // uniform: the finish pass writes NaN
-    const int l = bp.first + (int)blockIdx.y, P = bp.nparts;
+    const int P = bp.nparts;
+    const int l_begin = NERF_HG_BUCKET_LOOP ? bp.first : bp.first + (int)blockIdx.y;
+    const int l_end = NERF_HG_BUCKET_LOOP ? a.p.levels : l_begin + 1;
     const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (threadIdx.x < P) cnt[threadIdx.x] = 0u;
-    __syncthreads();
     const bool valid = n < a.n;
-    Corners c;
-    int pk[8];
-    unsigned slot[8];
-    if (valid) {
-        float p[3];
-        sample_position(a, n, p);
-        c = level_corners(p, a.p.normalize, a.p.res[l], a.p.table_size, a.p.primes);
-    }
-    // slots: per corner, the wave's lanes grouped by part (one ballot per part present), ranks and
-    // per-part running counts in registers (lane p holds part p's), then ONE LDS add per wave for
-    // all its parts — no atomic round trip inside the loop
     const int lane = threadIdx.x & 63;
-    unsigned runv = 0;                              // lane p: this wave's entries for part p so far
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        pk[k] = valid ? (int)((unsigned)c.idx[k] / (unsigned)bp.rpp) : -1;
-        unsigned long long rest = __ballot(valid);
-        while (rest != 0ull) {
-            const int leader = __builtin_ctzll(rest);
-            const int pp = __builtin_amdgcn_readlane(pk[k], leader);
-            const unsigned long long m = __ballot(pk[k] == pp);
-            const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-            const unsigned run = __builtin_amdgcn_readlane(runv, pp);
-            if (pk[k] == pp) slot[k] = run + rank;
-            if (lane == pp) runv += (unsigned)__builtin_popcountll(m);
-            rest &= ~m;
-        }
-    }
-    const unsigned wbase = (lane < P && runv != 0u) ? atomicAdd(&cnt[lane], runv) : 0u;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) slot[k] += (unsigned)__shfl((int)wbase, pk[k] < 0 ? 0 : pk[k], 64);
-    __syncthreads();
     const int sub = (int)(blockIdx.x % BUCKET_SUB);
-    unsigned* const gcount = bp.count + (int64_t)(l - bp.first) * P * BUCKET_SUB + sub;
-    if (threadIdx.x < P && cnt[threadIdx.x] != 0u)
-        base[threadIdx.x] = atomicAdd(&gcount[threadIdx.x * BUCKET_SUB], cnt[threadIdx.x]);
-    __syncthreads();
-    if (!valid) return;
     const double scale = ldexp(1.0, s);
+    float p[3] = {0.0f, 0.0f, 0.0f};
+    if (valid) sample_position(a, n, p);
+    for (int l = l_begin; l < l_end; ++l) {
+        if (threadIdx.x < P) cnt[threadIdx.x] = 0u;
+        __syncthreads();
+        Corners c;
+        int pk[8];
+        unsigned slot[8];
+        if (valid) c = level_corners(p, a.p.normalize, a.p.res[l], a.p.table_size, a.p.primes);
+        // slots: per corner, the wave's lanes grouped by part (one ballot per part present), ranks
+        // and per-part running counts in registers (lane p holds part p's), then ONE LDS add per wave
+        // for all its parts — no atomic round trip inside the loop
+        unsigned runv = 0;                          // lane p: this wave's entries for part p so far
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const unsigned pos = base[pk[k]] + slot[k];
-        const int64_t b = ((int64_t)(l - bp.first) * P + pk[k]) * BUCKET_SUB + sub;
-        if (pos < (uint64_t)bp.cap) {
-            const int64_t e = b * bp.cap + pos;
-            bp.en[e] = (unsigned)n;
-            bp.er[e] = (unsigned)(c.idx[k] - pk[k] * bp.rpp);
-            bp.ew[e] = c.w[k];
-        } else {
-            // past the bucket's capacity: the contribution goes to the global accumulator directly
+        for (int k = 0; k < 8; ++k) {
+            pk[k] = valid ? (int)((unsigned)c.idx[k] / (unsigned)bp.rpp) : -1;
+            unsigned long long rest = __ballot(valid);
+            while (rest != 0ull) {
+                const int leader = __builtin_ctzll(rest);
+                const int pp = __builtin_amdgcn_readlane(pk[k], leader);
+                const unsigned long long m = __ballot(pk[k] == pp);
+                const unsigned rank =
+                    __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                const unsigned run = __builtin_amdgcn_readlane(runv, pp);
+                if (pk[k] == pp) slot[k] = run + rank;
+                if (lane == pp) runv += (unsigned)__builtin_popcountll(m);
+                rest &= ~m;
+            }
+        }
+        const unsigned wbase = (lane < P && runv != 0u) ? atomicAdd(&cnt[lane], runv) : 0u;
 #pragma unroll
-            for (int f = 0; f < F; ++f) {
-                const double x = (double)c.w[k] * ((double)g[n * ld + (int64_t)l * F + f] * scale);
-                const long long q = a.n >= 256 ? rint_fixed(x) : llrint(x);
-                if (q != 0) atomicAdd(&acc[(a.off[l] + c.idx[k]) * F + f], (unsigned long long)q);
+        for (int k = 0; k < 8; ++k) slot[k] += (unsigned)__shfl((int)wbase, pk[k] < 0 ? 0 : pk[k], 64);
+        __syncthreads();
+        unsigned* const gcount = bp.count + (int64_t)(l - bp.first) * P * BUCKET_SUB + sub;
+        if (threadIdx.x < P && cnt[threadIdx.x] != 0u)
+            base[threadIdx.x] = atomicAdd(&gcount[threadIdx.x * BUCKET_SUB], cnt[threadIdx.x]);
+        __syncthreads();
+        if (valid) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const unsigned pos = base[pk[k]] + slot[k];
+                const int64_t b = ((int64_t)(l - bp.first) * P + pk[k]) * BUCKET_SUB + sub;
+                if (pos < (uint64_t)bp.cap) {
+                    const int64_t e = b * bp.cap + pos;
+                    bp.en[e] = (unsigned)n;
+                    bp.er[e] = (unsigned)(c.idx[k] - pk[k] * bp.rpp);
+                    bp.ew[e] = c.w[k];
+                } else {
+                    // past the sub-bucket's capacity: straight to the global accumulator
+#pragma unroll
+                    for (int f = 0; f < F; ++f) {
+                        const double x = (double)c.w[k] * ((double)g[n * ld + (int64_t)l * F + f] * scale);
+                        const long long q = a.n >= 256 ? rint_fixed(x) : llrint(x);
+                        if (q != 0) atomicAdd(&acc[(a.off[l] + c.idx[k]) * F + f], (unsigned long long)q);
+                    }
+                }
             }
         }
     }
@@ -846,7 +856,8 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bucket_add_kernel(HashAr
 template <int F>
 void launch_bucket(hipStream_t s, const HashArgs& a, const BucketPlan& bp, int nhashed, const float* g, int64_t ld,
                    const float* gt, const unsigned* gmax, unsigned long long* acc) {
-    hipLaunchKernelGGL(hashgrid_bucket_kernel<F>, dim3((unsigned)((a.n + 255) / 256), (unsigned)nhashed), dim3(256), 0, s,
+    hipLaunchKernelGGL(hashgrid_bucket_kernel<F>, dim3((unsigned)((a.n + 255) / 256), NERF_HG_BUCKET_LOOP ? 1u : (unsigned)nhashed),
+                       dim3(256), 0, s,
                        a, bp, g, ld, gmax, acc);
     hipLaunchKernelGGL(hashgrid_bucket_add_kernel<F>, dim3((unsigned)((int64_t)nhashed * bp.nparts * bp.chunks)),
                        dim3(BWD_THREADS), 0, s, a, bp, gt, gmax, acc);
