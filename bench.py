@@ -528,10 +528,11 @@ def _gather_roofline(ks_fn: dict, steps: int, workload: str):
     larger than one XCD's 4 MB L2, far smaller than the 256 MB Infinity Cache (MALL), whose random-row
     gather rate the guide measures at 8.6 TB/s chip-wide.  achieved = algorithmic bytes per launch
     (8 corners x F fp32 gathered + F fp32 written per (sample, level); the backward:
-    F fp32 read + 8 corners x F 8-byte fixed-point adds) / the launch's event-timed duration."""
+    F fp32 read + 8 corners x F 8-byte fixed-point adds) / the launch's event-timed duration
+    (nerf_hashgrid_bwd: the whole bucketed backward call, its kernels together)."""
     out = {}
     for fn in ("hashgrid_fwd_tile_kernel", "hashgrid_fwd_level_kernel", "hashgrid_fwd_kernel", "hashgrid_bwd_walk_kernel",
-               "hashgrid_bwd_kernel"):
+               "hashgrid_bwd_kernel", "nerf_hashgrid_bwd"):
         r = ks_fn.get(fn)
         if not r or r["ms"] <= 0:
             continue

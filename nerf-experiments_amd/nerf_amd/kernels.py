@@ -683,7 +683,11 @@ def _hashgrid_table_check(name: str, params, table: torch.Tensor) -> None:
 # 2807 / 3042 / 5586 us)
 _HG_FWD = os.environ.get("NERF_HG_FWD", "1")[:1]
 HASHGRID_FWD_FN = {"0": "hashgrid_fwd_kernel", "2": "hashgrid_fwd_tile_kernel"}.get(_HG_FWD, "hashgrid_fwd_level_kernel")
-HASHGRID_BWD_FN = "hashgrid_bwd_walk_kernel" if os.environ.get("NERF_HG_BWD", "0")[:1] == "2" else "hashgrid_bwd_kernel"
+# the backward's event bracket covers the whole call; named by its kernel when one kernel does the
+# work, else (the default bucketed form: restage, bijective-level walk, two bucket passes) by the call
+HASHGRID_BWD_FN = ("hashgrid_bwd_walk_kernel" if os.environ.get("NERF_HG_BWD", "0")[:1] == "2"
+                   else "nerf_hashgrid_bwd" if os.environ.get("NERF_HG_BUCKET", "1")[:1] != "0"
+                   else "hashgrid_bwd_kernel")
 
 
 def hashgrid_fwd(params, table: torch.Tensor, out: torch.Tensor, *, x=None, ray_o=None, ray_d=None, t_start=None,

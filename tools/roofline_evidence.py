@@ -29,7 +29,7 @@ FNS = ("mlp_fused_kernel<0>", "mlp_fused_kernel<1>", "linear_nt_x3_glds_kernel",
        "linear_wgrad_x3_tr_kernel", "linear_wgrad_x3_stream_kernel", "linear_wgrad_x3_kernel", "linear_nt_kernel",
        "linear_wgrad_kernel",
        "hashgrid_bwd_kernel", "hashgrid_fwd_kernel", "hashgrid_fwd_level_kernel", "hashgrid_fwd_tile_kernel",
-       "hashgrid_bwd_walk_kernel", "hashgrid_gtr_kernel")
+       "hashgrid_bwd_walk_kernel", "hashgrid_gtr_kernel", "hashgrid_bucket_kernel", "hashgrid_bucket_add_kernel")
 
 
 def fn_name(kernel_name: str) -> str:
