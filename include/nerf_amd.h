@@ -595,11 +595,14 @@ int nerf_hashgrid_fwd(const nerf_hashgrid_params* params, const float* x, const 
  * NaN.  workspace: nerf_hashgrid_workspace(params) bytes, 256-byte aligned; zeroed by the call
  * itself (no state is carried between calls). */
 size_t nerf_hashgrid_workspace(const nerf_hashgrid_params* params);
-/* (ABI 8) workspace for n_samples with grad_out restaged level-major: nerf_hashgrid_workspace(params)
- * rounded up to 256 bytes, plus n_samples * levels * features fp32.  With a workspace of at least
- * this size the call first copies grad_out level-major (one pass, with the max |g|) and the part
- * walks read each level's values contiguously; a workspace of only nerf_hashgrid_workspace(params)
- * bytes reads the [n][g_ld] rows in place.  Same result either way (bitwise). */
+/* (ABI 8) workspace for n_samples: nerf_hashgrid_workspace(params) rounded up to 256 bytes, room for
+ * grad_out restaged level-major (n_samples * levels * features fp32) and per-sample position
+ * records, and the buckets of the hashed levels' corner contributions (about 12 B x 8 corners x
+ * 1.25 per (sample, hashed level): ~2.1 GB for 1.31 M samples x 13 hashed levels).  With a workspace
+ * of at least this size the call restages grad_out and takes the hashed levels through the bucketed
+ * passes (NERF_HG_BUCKET, default on); with only nerf_hashgrid_workspace(params) bytes every level
+ * is walked once per 160 KB part, reading the [n][g_ld] rows in place.  Same result either way
+ * (bitwise: integer sums). */
 size_t nerf_hashgrid_workspace_n(const nerf_hashgrid_params* params, int64_t n_samples);
 int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float* x, const float* ray_o,
                       const float* ray_d, const float* t_start, const float* t_end, int64_t n_samples,
