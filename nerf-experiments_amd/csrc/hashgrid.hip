@@ -704,6 +704,8 @@ struct BucketPlan {
     int rpp;                // rows per part
     int chunks;             // pass-B workgroups per bucket (one per sub-bucket)
     int64_t cap;            // entries per sub-bucket
+    int pack_bits;          // > 0: entries packed into 8 B (uint2 {local sample << bits | row, weight}) — the
+                            // sample as its index among the sub-bucket's workgroups' samples; 0: 3 arrays
     unsigned* count;        // [(L - first) * nparts][BUCKET_SUB] entries filed (zeroed per call)
     unsigned* en;           // [bucket][sub][cap] sample
     unsigned* er;           // [bucket][sub][cap] row within the part
@@ -713,6 +715,12 @@ struct BucketPlan {
 #ifndef NERF_HG_BUCKET_LOOP
 #define NERF_HG_BUCKET_LOOP 1
 #endif
+#ifndef NERF_HG_PACK_DEFAULT
+#define NERF_HG_PACK_DEFAULT 1
+#endif
+#ifndef NERF_HG_BUCKET_RANK
+#define NERF_HG_BUCKET_RANK 1
+#endif
 
 // Pass A.  NERF_HG_BUCKET_LOOP (default 1): each workgroup's 256 samples through every hashed level
 // (positions derived once); 0: one level per workgroup (grid y).
@@ -721,10 +729,11 @@ __global__ __launch_bounds__(256) void hashgrid_bucket_kernel(HashArgs a, Bucket
                                                               int64_t ld, const unsigned* __restrict__ gmax,
                                                               unsigned long long* __restrict__ acc) {
 #pragma clang fp contract(off)
-    __shared__ unsigned cnt[BUCKET_MAXP], base[BUCKET_MAXP];
+    __shared__ unsigned cnt[BUCKET_MAXP], base[BUCKET_MAXP], cntw[4][BUCKET_MAXP];
     const int s = fixed_shift(*gmax, a.n);
     if (s == -1000) return;                         // uniform: the finish pass writes NaN
     const int P = bp.nparts;
+    const int wave = threadIdx.x >> 6;
     const int l_begin = NERF_HG_BUCKET_LOOP ? bp.first : bp.first + (int)blockIdx.y;
     const int l_end = NERF_HG_BUCKET_LOOP ? a.p.levels : l_begin + 1;
     const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -736,11 +745,41 @@ __global__ __launch_bounds__(256) void hashgrid_bucket_kernel(HashArgs a, Bucket
     if (valid) sample_position(a, n, p);
     for (int l = l_begin; l < l_end; ++l) {
         if (threadIdx.x < P) cnt[threadIdx.x] = 0u;
+        if (NERF_HG_BUCKET_RANK && threadIdx.x < 4 * P) cntw[threadIdx.x / P][threadIdx.x % P] = 0u;
         __syncthreads();
         Corners c;
         int pk[8];
         unsigned slot[8];
         if (valid) c = level_corners(p, a.p.normalize, a.p.res[l], a.p.table_size, a.p.primes);
+        if (NERF_HG_BUCKET_RANK) {
+            // slots from per-wave LDS counters (returning adds: a wave instruction's lanes on a
+            // handful of addresses, no cross-wave contention), wave offsets by a prefix after the sync.
+            // Default: the fine pass's 16 levels 1298 vs 1468 us with the ballot grouping below
+            // (NERF_HG_BUCKET_RANK=0; profiles/r04w)
+            if (valid) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    pk[k] = (int)((unsigned)c.idx[k] / (unsigned)bp.rpp);
+                    slot[k] = atomicAdd(&cntw[wave][pk[k]], 1u);
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x < P) {
+                unsigned run = 0;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    const unsigned c_w = cntw[w][threadIdx.x];
+                    cntw[w][threadIdx.x] = run;
+                    run += c_w;
+                }
+                cnt[threadIdx.x] = run;
+            }
+            __syncthreads();
+            if (valid) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) slot[k] += cntw[wave][pk[k]];
+            }
+        } else {
         // slots: per corner, the wave's lanes grouped by part (one ballot per part present), ranks
         // and per-part running counts in registers (lane p holds part p's), then ONE LDS add per wave
         // for all its parts — no atomic round trip inside the loop
@@ -765,6 +804,7 @@ __global__ __launch_bounds__(256) void hashgrid_bucket_kernel(HashArgs a, Bucket
 #pragma unroll
         for (int k = 0; k < 8; ++k) slot[k] += (unsigned)__shfl((int)wbase, pk[k] < 0 ? 0 : pk[k], 64);
         __syncthreads();
+        }
         unsigned* const gcount = bp.count + (int64_t)(l - bp.first) * P * BUCKET_SUB + sub;
         if (threadIdx.x < P && cnt[threadIdx.x] != 0u)
             base[threadIdx.x] = atomicAdd(&gcount[threadIdx.x * BUCKET_SUB], cnt[threadIdx.x]);
@@ -776,9 +816,16 @@ __global__ __launch_bounds__(256) void hashgrid_bucket_kernel(HashArgs a, Bucket
                 const int64_t b = ((int64_t)(l - bp.first) * P + pk[k]) * BUCKET_SUB + sub;
                 if (pos < (uint64_t)bp.cap) {
                     const int64_t e = b * bp.cap + pos;
-                    bp.en[e] = (unsigned)n;
-                    bp.er[e] = (unsigned)(c.idx[k] - pk[k] * bp.rpp);
-                    bp.ew[e] = c.w[k];
+                    const unsigned row = (unsigned)(c.idx[k] - pk[k] * bp.rpp);
+                    if (bp.pack_bits > 0) {
+                        const unsigned li = (blockIdx.x / BUCKET_SUB) * 256u + threadIdx.x;
+                        reinterpret_cast<uint2*>(bp.en)[e] =
+                            make_uint2((li << bp.pack_bits) | row, __float_as_uint(c.w[k]));
+                    } else {
+                        bp.en[e] = (unsigned)n;
+                        bp.er[e] = row;
+                        bp.ew[e] = c.w[k];
+                    }
                 } else {
                     // past the sub-bucket's capacity: straight to the global accumulator
 #pragma unroll
@@ -829,9 +876,19 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bucket_add_kernel(HashAr
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t eu = e + u * BWD_THREADS < e1 ? e + u * BWD_THREADS : e1 - 1;
-            nn[u] = __builtin_nontemporal_load(en + eu);
-            row[u] = __builtin_nontemporal_load(er + eu);
-            w[u] = __builtin_nontemporal_load(ew + eu);
+            if (bp.pack_bits > 0) {
+                typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                const u32x2 kw = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(bp.en) + sb * bp.cap + eu);
+                const unsigned kx = kw[0], ky = kw[1];      // scalar copies (ext-vector elements)
+                const unsigned li = kx >> bp.pack_bits;
+                nn[u] = ((li >> 8) * BUCKET_SUB + (unsigned)ch) * 256u + (li & 255u);
+                row[u] = kx & ((1u << bp.pack_bits) - 1u);
+                w[u] = __uint_as_float(ky);
+            } else {
+                nn[u] = __builtin_nontemporal_load(en + eu);
+                row[u] = __builtin_nontemporal_load(er + eu);
+                w[u] = __builtin_nontemporal_load(ew + eu);
+            }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -1198,6 +1255,14 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
             bp.ew = reinterpret_cast<float*>(bp.er + round256((size_t)nb * bl.cap * sizeof(unsigned)) / sizeof(unsigned));
             if (hipMemsetAsync(bp.count, 0, (size_t)nb * sizeof(unsigned), s) != hipSuccess) return NERF_ERR_LAUNCH;
             bp.chunks = BUCKET_SUB;
+            // 8-byte entries when the sample index among a sub-bucket's workgroups and the row fit 32
+            // bits together (C5's fine pass: 82 176 x 10 240 rows); NERF_HG_PACK=0: 12-byte entries
+            // (1538 vs 1474 us with the ballot grouping, profiles/r04v)
+            static const int pack_mode = env_mode("NERF_HG_PACK", NERF_HG_PACK_DEFAULT);
+            int rb = 0;
+            while ((1 << rb) < bl.rpp) ++rb;
+            const int64_t li_max = ((n_samples + 255) / 256 + BUCKET_SUB - 1) / BUCKET_SUB * 256;
+            bp.pack_bits = (pack_mode == 1 && rb < 32 && li_max <= ((int64_t)1 << (32 - rb))) ? rb : 0;
             switch (params->features) {
                 case 1: launch_bucket<1>(s, a, bp, nh, grad_out, g_ld, gt_bucket, gmax, acc); break;
                 case 2: launch_bucket<2>(s, a, bp, nh, grad_out, g_ld, gt_bucket, gmax, acc); break;
