@@ -715,6 +715,9 @@ struct BucketPlan {
 #ifndef NERF_HG_BUCKET_LOOP
 #define NERF_HG_BUCKET_LOOP 1
 #endif
+#ifndef NERF_HG_ADD_UNROLL
+#define NERF_HG_ADD_UNROLL 4
+#endif
 #ifndef NERF_HG_PACK_DEFAULT
 #define NERF_HG_PACK_DEFAULT 1
 #endif
@@ -868,8 +871,8 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bucket_add_kernel(HashAr
     const float* __restrict__ ew = bp.ew + sb * bp.cap;
     const bool fast = a.n >= 256;
     const float* __restrict__ gl = gt + (int64_t)l * a.n * F;
-    // four entries per thread per trip, all their loads issued before any is used
-    constexpr int U = 4;
+    // NERF_HG_ADD_UNROLL entries per thread per trip, all their loads issued before any is used
+    constexpr int U = NERF_HG_ADD_UNROLL;
     for (int64_t e = e0 + threadIdx.x; e < e1; e += U * BWD_THREADS) {
         unsigned nn[U], row[U];
         float w[U], gv[U][F];
