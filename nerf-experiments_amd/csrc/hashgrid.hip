@@ -692,6 +692,12 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bwd_walk_kernel(HashArgs
 // capacity (sized 1.25x the uniform share plus a margin; the hash spreads rows evenly) go straight
 // to the global accumulators, so no input can lose one.
 constexpr int BUCKET_MAXP = 64;
+// pass B's part: NERF_HG_BUCKET_PART entries (default 10240 = 80 KB: two workgroups share a CU, with
+// twice the parts — 1.68 vs 1.81 ms per ingp step against 20480 = 160 KB, profiles/r04z)
+#ifndef NERF_HG_BUCKET_PART
+#define NERF_HG_BUCKET_PART 10240
+#endif
+constexpr int BUCKET_PART_ENTRIES = NERF_HG_BUCKET_PART;
 // Every bucket is split into BUCKET_SUB sub-buckets with their own fill counters: pass-A workgroup w
 // files into sub-bucket w % BUCKET_SUB, so a counter takes the atomics of 1/16 of the workgroups, all
 // on one XCD (workgroups are dealt to the 8 XCDs round-robin) — one shared counter per bucket took
@@ -852,7 +858,7 @@ __global__ __launch_bounds__(BWD_THREADS) void hashgrid_bucket_add_kernel(HashAr
                                                                           const unsigned* __restrict__ gmax,
                                                                           unsigned long long* __restrict__ acc) {
 #pragma clang fp contract(off)
-    __shared__ unsigned long long part[PART_ENTRIES];
+    __shared__ unsigned long long part[BUCKET_PART_ENTRIES];
     const int s = fixed_shift(*gmax, a.n);
     if (s == -1000) return;
     const double scale = ldexp(1.0, s);
@@ -1078,7 +1084,7 @@ BucketLayout bucket_layout(const nerf_hashgrid_params* p, int64_t n) {
     int first = L;
     while (first > 0 && hashed(first - 1)) --first;
     b.first = first;
-    b.rpp = PART_ENTRIES / p->features;
+    b.rpp = BUCKET_PART_ENTRIES / p->features;
     b.nparts = (int)((T + b.rpp - 1) / b.rpp);
     if (first == L || b.nparts > BUCKET_MAXP || n < 1 || n >= ((int64_t)1 << 31)) return b;
     b.cap = ((8 * n * 5 / 4) / ((int64_t)b.nparts * BUCKET_SUB) + 4096 + 63) / 64 * 64;
