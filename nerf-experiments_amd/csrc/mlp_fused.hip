@@ -106,6 +106,7 @@ struct FusedArgs {
     int img_bytes;
     int gen_mask;      // bit e: encoding e is generated at the start of every tile (forward only)
     int gen_lds;       // the encoding the first layer reads from LDS (generated last), or -1
+    int gen_reg;       // the encoding (one k-block) a later layer reads from the tile-start registers, or -1
     int n_layers;
     int M;
     int ntiles;
@@ -240,6 +241,9 @@ struct Ctx {
     // rays of two tiles (S = 256): the first tile's heads and interval lengths, held over the second
     f4 phead[SB];
     float pcdist[SB];
+    // the split k-block of encoding gen_reg for the wave's own samples, captured from the LDS rows at
+    // the tile start and held across the layers (a later layer's generated segment, seg_gen on l > 0)
+    bf16x8 gh[SB], gl[SB];
 };
 
 __device__ __forceinline__ int dma_units(Ctx& c, int l) { return LF(int, chunk_units, l); }
@@ -980,9 +984,18 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
                                 row_ok, hh[kh], hl[kh]);
                 continue;
             }
-            if (MODE == MODE_FWD && gen != 0) {         // generated at the tile start, still in LDS
+            if (MODE == MODE_FWD && gen != 0) {
+                if constexpr (KBR == 0) {               // the first layer: generated at the tile start, still in LDS
 #pragma unroll
-                for (int sb = 0; sb < SB; ++sb) gen_block(c, 16 * sb + (c.lane & 15), 32 * khl + 8 * g, hh[kh][sb], hl[kh][sb]);
+                    for (int sb = 0; sb < SB; ++sb)
+                        gen_block(c, 16 * sb + (c.lane & 15), 32 * khl + 8 * g, hh[kh][sb], hl[kh][sb]);
+                } else {                                // a later layer: the block captured at the tile start
+#pragma unroll
+                    for (int sb = 0; sb < SB; ++sb) {
+                        hh[kh][sb] = c.gh[sb];
+                        hl[kh][sb] = c.gl[sb];
+                    }
+                }
                 continue;
             }
             const float* p = sg ? LFI(cfptr_t, seg_ptr, 1, l) : LFI(cfptr_t, seg_ptr, 0, l);
@@ -1372,6 +1385,11 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
             c.xh[kb][sb] = bf16x8{};
             c.xl[kb][sb] = bf16x8{};
         }
+#pragma unroll
+    for (int sb = 0; sb < SB; ++sb) {
+        c.gh[sb] = bf16x8{};
+        c.gl[sb] = bf16x8{};
+    }
     // tile groups of `span` consecutive tiles (one group: one tile, unless rays span two)
     const int span_log = a.span >> 1;                 // span 1 or 2
     for (int it = 0; it < my_tiles; ++it) {
@@ -1401,6 +1419,12 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
 #pragma unroll
                     for (int j = 0; j < 9; ++j) v[j] = e == 0 ? v0[j] : v1[j];
                     gen_rows_lds(c, e, base, v);
+                    if (e == a.gen_reg) {
+                        // the later layer's block from the wave's own rows (same wave: LDS in order)
+#pragma unroll
+                        for (int sb = 0; sb < SB; ++sb)
+                            gen_block(c, 16 * sb + (c.lane & 15), 8 * (c.lane >> 4), c.gh[sb], c.gl[sb]);
+                    }
                     gen_store(c, e, base);
                 }
             }
@@ -1521,7 +1545,7 @@ int fused_launch(const nerf_fused_layer* layers, int32_t n_layers, const void* i
     NERF_REQUIRE(M >= 1 && M <= (int64_t)1 << 30);
     FusedArgs a;
     int64_t img_end = 0;
-    int gen_lds = -1;
+    int gen_lds = -1, gen_reg = -1;
     // the input-gradient chain (a layer multiplies by ReLU bits or routes rows to a second output):
     // no bias, no ReLU, no mask bits or column outputs; otherwise the forward, which has none of those
     bool dgrad = false;
@@ -1575,11 +1599,18 @@ int fused_launch(const nerf_fused_layer* layers, int32_t n_layers, const void* i
                 NERF_REQUIRE(S >= 1 && M % S == 0);
                 continue;
             }
-            // read from the rows generated at the tile start: the first layer only, one segment
-            NERF_REQUIRE(!dgrad && l == 0 && encodings != nullptr && (gen == 1 || gen == 2) && gen_lds < 0);
+            // rows generated at the tile start: the first layer reads them from LDS (one segment); a
+            // later layer reads one k-block of them from the registers captured at the tile start
+            NERF_REQUIRE(!dgrad && encodings != nullptr && (gen == 1 || gen == 2));
             const nerf_fused_encoding& e = encodings[gen - 1];
             NERF_REQUIRE(e.out_dim > 0 && e.out_dim <= 32 * L.seg_kb[s] && 32 * L.seg_kb[s] <= 64);
-            gen_lds = gen - 1;
+            if (l == 0) {
+                NERF_REQUIRE(gen_lds < 0);
+                gen_lds = gen - 1;
+            } else {
+                NERF_REQUIRE(L.seg_kb[s] == 1 && (gen_reg < 0 || gen_reg == gen - 1));
+                gen_reg = gen - 1;
+            }
         }
         for (int s = 0; s < L.nseg; ++s) {
             kbs += L.seg_kb[s];
@@ -1631,8 +1662,32 @@ int fused_launch(const nerf_fused_layer* layers, int32_t n_layers, const void* i
         }
     }
     NERF_REQUIRE(gen_lds < 0 || ((gen_mask >> gen_lds) & 1));
+    NERF_REQUIRE(gen_reg < 0 || ((gen_mask >> gen_reg) & 1));
+    // Ordering rule for generated rows read back from HBM inside the launch (seg_gen 0 with seg_ptr in
+    // a generated encoding's rows): only the wave that stored a row may read it (one wave's vector
+    // memory operations complete in order through the CU's L1), i.e. per-sample rows (not per_ray)
+    // read at row divisor 1.  A per-ray row is stored once, by the wave holding the ray's first
+    // sample — possibly another workgroup of the grid, with no ordering — so a later layer must take
+    // a per-ray encoding from the tile-start registers (seg_gen) or the caller fills it beforehand.
+    for (int l = 0; l < n_layers && gen_mask != 0; ++l) {
+        const nerf_fused_layer& L = layers[l];
+        for (int s = 0; s < L.nseg; ++s) {
+            if (L.seg_gen[s] != 0) continue;
+            const char* p = static_cast<const char*>(static_cast<const void*>(L.seg_ptr[s]));
+            const char* pe = p + (int64_t)L.seg_rows[s] * L.seg_ld[s] * 4;
+            for (int e = 0; e < 2; ++e) {
+                if (!((gen_mask >> e) & 1)) continue;
+                const nerf_fused_encoding& E = encodings[e];
+                const char* q = static_cast<const char*>(static_cast<const void*>(E.out));
+                const char* qe = q + (E.per_ray ? E.n_rays : M) * E.ld * 4;
+                if (p < qe && q < pe)
+                    NERF_REQUIRE((!E.per_ray || E.samples_per_ray == 1) && L.seg_rd[s] == 1 && p == q && L.seg_ld[s] == E.ld);
+            }
+        }
+    }
     a.gen_mask = gen_mask;
     a.gen_lds = gen_lds;
+    a.gen_reg = gen_reg;
     a.img = static_cast<const char*>(image);
     a.img_bytes = (int)img_end;
     a.n_layers = n_layers;

@@ -43,6 +43,9 @@ def _pack_image(f) -> None:
 
 FUSED_TYPES = {(0, 1): 1, (0, 2): 2, (4, 0): 3, (8, 0): 6, (8, 1): 7, (8, 2): 8}   # (kbr, kbh) -> type
 ENABLED = os.environ.get("NERF_FUSED", "1") != "0"     # A/B switch (bench, tests)
+# a per-ray encoding read by a later layer comes from registers captured at the tile start; tests
+# turn this off to check that the library refuses the HBM read-back instead (the ordering rule)
+CAPTURE_PER_RAY = True
 
 
 def _layer_shape(plan, idx):
@@ -216,12 +219,24 @@ class FusedForward:
         encs = (_lib.NerfFusedEncoding * 2)()
         gen_of = {}
         nbytes = 0.0
+        # Ordering rule (csrc/mlp_fused.hip fused_launch): a later layer reads generated rows back from
+        # HBM only when its own wave stored them (per-sample rows); a per-ray encoding read by a later
+        # layer comes from the registers captured at the tile start (one 32-column block), else it is
+        # filled before the launch.
+        reg_kind = None
         for e, (kind, g) in enumerate((("pos", gens[0]), ("dir", gens[1]))):
             if g is None:
                 continue
+            later = [s for idx in range(1, L) for s in self.layers[idx][2] if s.kind == kind]
             if not any(s.kind == kind for idx in range(L) for s in self.layers[idx][2]):
                 K.materialize(pos if kind == "pos" else dirs)      # not read by the kernel
                 continue
+            per_ray = g.spec.per_ray and (dir_rd if kind == "dir" else 1) > 1
+            if later and per_ray and CAPTURE_PER_RAY and (reg_kind is not None or any(s.k_pad != 32 for s in later)):
+                K.materialize(pos if kind == "pos" else dirs)      # filled by the encoding launch
+                continue
+            if later and per_ray and CAPTURE_PER_RAY:
+                reg_kind = kind
             ctypes.memmove(ctypes.byref(encs[e]), ctypes.byref(g.spec), ctypes.sizeof(g.spec))
             if kind == "dir":
                 encs[e].samples_per_ray = dir_rd
@@ -253,6 +268,9 @@ class FusedForward:
                 d.seg_ptr[si] = t.data_ptr()
                 if idx == 0 and s.kind in gen_of:
                     # the first layer takes the rows generated at the tile start straight from LDS
+                    d.seg_gen[si] = gen_of[s.kind]
+                elif s.kind == reg_kind:
+                    # a per-ray encoding: the block captured in registers at the tile start
                     d.seg_gen[si] = gen_of[s.kind]
                 else:
                     # algorithmic bytes: an HBM-fed encoding read (generated ones: the rows the kernel

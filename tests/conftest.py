@@ -13,6 +13,11 @@ for p in (ROOT, PKG):
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+# Deferred encoding rows (generated inside the fused forward) are NaN-filled at allocation, so a
+# read of a row before the kernel stored it fails every time instead of returning whatever the
+# allocator left there (nerf_amd/kernels.py encode_fwd).
+os.environ.setdefault("NERF_POISON_DEFERRED", "1")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (ROCm device) and the built HIP library")
