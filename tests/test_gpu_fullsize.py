@@ -153,3 +153,99 @@ def test_full_size_training_step_deterministic_and_finite():
     for a, b in zip(g1, g2):
         assert torch.isfinite(a).all()
         assert torch.equal(a, b)
+
+
+def _mip_oracle_pass(sd, o, d, pw, t0, t1, dt):
+    """The bench's mip field on explicit t (masked IPE at alpha = L, masked PE of the directions,
+    NerfModel, compositing with 3 * MAGIC) in dtype dt: (rgb, weights)."""
+    B, S = t0.shape
+    o, d, t0, t1 = o.to(dt), d.to(dt), t0.to(dt), t1.to(dt)
+    pos, dirs = O.compute_positions(o, d, t0, t1, "middle")
+    n = B * S
+    pos_pe = O.integrated_pe(pos.reshape(-1, 3), dirs.reshape(-1, 3), torch.full((n, 1), float(pw[0]), dtype=dt),
+                             t0.reshape(-1, 1), t1.reshape(-1, 1), 10, 1.0, True, True, 0.0,
+                             mask=O.barf_mask(10.0, 10).to(dt))
+    dir_pe = O.barf_pe(dirs.reshape(-1, 3), 4, 4.0, True, 1.0).to(dt)
+    dens, col = O.nerf_model_forward(sd, pos_pe, dir_pe, 2, 4, True, False)
+    b = (-dens.view(B, S) * (t1 - t0)) * 3.0 * (1 / 3)
+    T = torch.cat((torch.ones(B, 1, dtype=dt), torch.exp(torch.cumsum(b[:, :-1], dim=1))), dim=1)
+    w = T * (1 - torch.exp(b))
+    return torch.sum(w.unsqueeze(-1) * col.view(B, S, 3), dim=1), w
+
+
+def test_full_size_mip_step_subset_parity_high():
+    """C3 as bench.py times it: 4096 rays x (64 coarse + 128 fine) on the fused
+    split-precision path ("high": the fused forward generating both encodings and compositing in its
+    launches, the fused input-gradient chain, the weight gradients), against the CPU oracle on a
+    seeded subset of 48 rays: coarse rgb / weights on the coarse t, fine rgb / weights on the GPU's
+    resampled fine t (2e-4 absolute, the split-precision renderer bar of test_gpu_mip_pose_feed.py),
+    and every parameter's gradient of one step's loss restricted to those rays (the other rays get
+    zero grad_rgb but run through the same full-size launches) against the oracle in float64, under
+    the per-tensor conditioning bound of test_gpu_parity.py's split-precision NerfModel test (2 x the
+    spread of the exact gradient under relative 2^-15 weight perturbations + 2 x 2^9 x the fp32
+    oracle's own error; 2^-15 = the per-product bound of three bf16 products)."""
+    from nerf_amd import BarfPositionalEncoding, IntegratedBarfFourierFeatures, NerfInterpolation, NerfModel
+    old = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision("high")
+    try:
+        torch.manual_seed(0)
+        pos = IntegratedBarfFourierFeatures(10, 10, 1.28, 6.4, True, 1.0, True)
+        pos.pixel_width_sigma = 0.0
+        model = NerfModel(4, 256, True, False, 2, pos, BarfPositionalEncoding(4, 4, 1.28, 6.4, True, 1.0),
+                          5e-4, 1e-4, 200000)
+        sd = {k: v.clone() for k, v in model.state_dict().items() if not k.endswith("alpha")}
+        ren = NerfInterpolation(2.0, 8.0, model, 128, "stratified_uniform", -1.0, "middle", model, 64).to(DEV)
+        B = 4096
+        o, d, pw = _lego_rays(B, 11)
+        target = torch.rand(B, 3, generator=torch.Generator().manual_seed(12))
+        idx = torch.arange(7, B, 85)                          # 48 rays spread over the batch
+        mask = torch.zeros(B, 1)
+        mask[idx] = 1.0
+        og, dg, pwg = o.to(DEV), d.to(DEV), pw.to(DEV)
+        torch.manual_seed(13)
+        t0c, t1c = ren._sample_t_stratified_uniform(B, 64, "stratified_uniform", -1.0)
+        rgb_c, w_c, dist = ren._compute_color(ren.model_proposal, t0c, t1c, og, dg, pwg, B, 64)
+        t0, t1 = ren._sample_t_pdf_weighted(t0c, w_c, dist, 128)
+        rgb_f, w_f, _ = ren._compute_color(ren.model_radiance, t0, t1, og, dg, pwg, B, 128)
+        loss = (((rgb_f - target.to(DEV)) ** 2 + (rgb_c - target.to(DEV)) ** 2) * mask.to(DEV)).sum()
+        model.zero_grad(set_to_none=True)
+        loss.backward()
+        torch.cuda.synchronize()
+        # forward parity on the subset
+        r_c, r_wc = _mip_oracle_pass(sd, o[idx], d[idx], pw, t0c[idx].cpu(), t1c[idx].cpu(), torch.float32)
+        np.testing.assert_allclose(rgb_c[idx.to(DEV)].detach().cpu().numpy(), r_c.numpy(), atol=2e-4, rtol=0)
+        np.testing.assert_allclose(w_c[idx.to(DEV)].detach().cpu().numpy(), r_wc.numpy(), atol=2e-4, rtol=0)
+        r_f, r_wf = _mip_oracle_pass(sd, o[idx], d[idx], pw, t0[idx].cpu(), t1[idx].cpu(), torch.float32)
+        np.testing.assert_allclose(rgb_f[idx.to(DEV)].detach().cpu().numpy(), r_f.numpy(), atol=2e-4, rtol=0)
+        np.testing.assert_allclose(w_f[idx.to(DEV)].detach().cpu().numpy(), r_wf.numpy(), atol=2e-4, rtol=0)
+        # one step's gradients: the conditioning bound of test_gpu_parity.py's split-precision
+        # NerfModel test (exact fp64 gradient; its spread under relative 2^-15 weight perturbations,
+        # three draws; the fp32 oracle's own error)
+        def grads(dt, perturb=None):
+            sdx = {k: v.detach().to(dt).clone() for k, v in sd.items()}
+            if perturb is not None:
+                gen = torch.Generator().manual_seed(perturb)
+                sdx = {k: v * (1 + (torch.rand(v.shape, generator=gen, dtype=dt) * 2 - 1) * 2.0 ** -15)
+                       for k, v in sdx.items()}
+            sdx = {k: v.requires_grad_(True) for k, v in sdx.items()}
+            c, _ = _mip_oracle_pass(sdx, o[idx], d[idx], pw, t0c[idx].cpu(), t1c[idx].cpu(), dt)
+            f, _ = _mip_oracle_pass(sdx, o[idx], d[idx], pw, t0[idx].cpu(), t1[idx].cpu(), dt)
+            tg = target[idx].to(dt)
+            (((f - tg) ** 2).sum() + ((c - tg) ** 2).sum()).backward()
+            return {k: v.grad.double() for k, v in sdx.items() if v.grad is not None}
+        exact, fp32 = grads(torch.float64), grads(torch.float32)
+        spread = {k: torch.zeros((), dtype=torch.float64) for k in exact}
+        for seed in range(3):
+            pert = grads(torch.float64, seed)
+            for k in exact:
+                spread[k] = torch.maximum(spread[k], (pert[k] - exact[k]).abs().max())
+        for k, p in model.named_parameters():
+            e = exact[k]                                    # every parameter has an oracle gradient
+            scale = e.abs().max().item()
+            err = (p.grad.detach().cpu().double() - e).abs().max().item() / scale
+            fp32_err = (fp32[k] - e).abs().max().item() / scale
+            bound = 2 * spread[k].item() / scale + 2 * 2 ** 9 * max(fp32_err, 2 ** -22)
+            print(f"{k}: err {err:.2e} bound {bound:.2e} (spread {spread[k].item() / scale:.2e}, fp32 {fp32_err:.2e})")
+            assert err <= bound, (k, err, bound)
+    finally:
+        torch.set_float32_matmul_precision(old)
