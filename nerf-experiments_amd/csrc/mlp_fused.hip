@@ -394,10 +394,11 @@ __device__ __forceinline__ void gen_hash_rows(const Ctx& c, int base, const floa
     }
     // (same wave: its LDS operations complete in order, so the positions above are visible below)
     // One level per trip, its resolution and row offset uniform (scalar loads), lane s < SPW on
-    // sample s.  (Four levels per trip on the four 16-lane groups, each group's level parameters
-    // selected from scalars, gave non-repeatable features in the last trip's fourth group of the
-    // second half of the waves on the GPU — cause not found; this form is repeatable and bitwise
-    // the stand-alone kernel, tests/test_hashgrid.py.)
+    // sample s: bitwise the stand-alone kernel and repeatable on both corner forms
+    // (tests/test_hashgrid.py).  Round 4 also ran four levels per trip (16-lane groups, per-lane
+    // level parameters); with the int64 corner arithmetic of that time it dropped corner 2's term
+    // at random in the last trip's fourth group of waves 4-7 — localised by bisection to that
+    // compiled form, not reproduced with the current corner code.
     const int normalize = HG(int32_t, normalize);
     const __attribute__((address_space(4))) int64_t* primes =
         (const __attribute__((address_space(4))) int64_t*)(c.kargs + offsetof(FusedArgs, hg) +

@@ -116,6 +116,8 @@ class _HashGridFn(th.autograd.Function):
 
         if (defer and FUSE_HASH and x is None and n > 0 and params.levels <= 16 and params.features in (1, 2, 4)
                 and used <= 64 and out_cols <= 64 and packed.data_ptr() % 16 == 0):
+            if os.environ.get("NERF_POISON_DEFERRED", "0") == "1":
+                out.fill_(float("nan"))            # tests: a row read before its store fails every time
             spec = _hash_spec(params, packed, out, ray_o, ray_d, t_start, t_end, samples_per_ray, n)
             # keep: the inputs the spec points at, and the params struct its `hash` pointer names
             out._nerf_deferred = K.DeferredEncoding(spec, (ray_o, ray_d, t_start, t_end, packed, params), fill)

@@ -9,6 +9,9 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from nerf_amd import kernels as K  # noqa: E402
 from nerf_amd import model_interpolation_architecture as A  # noqa: E402
 from nerf_amd.model_ingp import FourierFeatures, INGPEncoding, NaiveINGP  # noqa: E402
+from nerf_amd import model_ingp as M  # noqa: E402
+
+M.FUSE_HASH = True          # the in-kernel hash generation is opt-in (NERF_FUSE_HASH=1)
 
 dev = torch.device("cuda", 0)
 torch.set_float32_matmul_precision("high")
@@ -50,6 +53,10 @@ with torch.no_grad():
               f"max {(rows[:, :32] - ref[:, :32]).abs().max().item():.3e}, pad nonzero {(rows[:, 32:] != 0).sum().item()}")
         if bad.shape[0]:
             r = bad[:, 0]
+            wv = rows[bad[:, 0], bad[:, 1]]
+            print("   wrong entries NaN (never stored):", int(torch.isnan(wv).sum()), "of", bad.shape[0],
+                  "| columns", sorted(set(bad[:, 1].tolist())), "| wave", sorted(set(((r % 128) // 16).tolist())),
+                  "| sample in wave", sorted(set((r % 16).tolist())))
             print("   samples", r[:8].tolist(), "cols", bad[:8, 1].tolist(), "sample mod 128:",
                   sorted(set((r % 128).tolist()))[:20], "tile-wave:", sorted(set(((r % 128) // 16).tolist())))
 
