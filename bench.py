@@ -884,8 +884,8 @@ def main():
                 if fr is not None:
                     fr["scope"] = ("the stand-alone encoding / compositing kernels, which neither the C3 training "
                                    "step nor its frame render (frame_render) launches: they serve samples-per-ray "
-                                   "counts that do not divide the fused tile (3d-ingp's 256-sample fine pass), "
-                                   "matmul precision 'highest' and GARF's nerfacc-style rendering")
+                                   "counts the fused compositing does not take (S not dividing the 128-sample tile, "
+                                   "other than 256), matmul precision 'highest' and GARF's nerfacc-style rendering")
                 out["roofline_hbm_frame"] = fr
             except Exception as e:      # noqa: BLE001
                 out["roofline_hbm_frame"] = {"error": f"{type(e).__name__}: {e}"}

@@ -602,7 +602,11 @@ size_t nerf_hashgrid_workspace(const nerf_hashgrid_params* params);
  * of at least this size the call restages grad_out and takes the hashed levels through the bucketed
  * passes (NERF_HG_BUCKET, default on); with only nerf_hashgrid_workspace(params) bytes every level
  * is walked once per 160 KB part, reading the [n][g_ld] rows in place.  Same result either way
- * (bitwise: integer sums). */
+ * (bitwise: integer sums).  The bucketed passes take a hashed level of at most 64 parts of 80 KB
+ * (table_size * features <= 64 * 10 240 entries: T <= 327 680 at F = 2, so not the 2^19 tables of
+ * instant-ngp); a larger table takes the per-part walk for every level, with the same result.
+ * With 8-byte packed entries (the default whenever the sample index and row fit 32 bits) the
+ * buckets need two 4-byte arrays' room, not three. */
 size_t nerf_hashgrid_workspace_n(const nerf_hashgrid_params* params, int64_t n_samples);
 int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float* x, const float* ray_o,
                       const float* ray_d, const float* t_start, const float* t_end, int64_t n_samples,

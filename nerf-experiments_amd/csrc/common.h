@@ -22,7 +22,8 @@
 // translation unit compiled with one reports it through nerf_build_flags(), which load() refuses.
 #if defined(NERF_FUSED_DIAG_NOFRAG) || defined(NERF_FUSED_DIAG_MFMAONLY) || defined(NERF_FUSED_DIAG_NOMASK) || \
     defined(NERF_FUSED_DIAG_NOSPLIT) || defined(NERF_FUSED_DIAG_NOSTORE) || defined(NERF_FUSED_DIAG_NOMASKIN) || \
-    defined(NERF_FUSED_DIAG_DROPSTORE)
+    defined(NERF_FUSED_DIAG_DROPSTORE) || defined(NERF_FUSED_DIAG_NODMA) || defined(NERF_FUSED_DIAG_NOEPI) || \
+    defined(NERF_FUSED_DIAG_NOBARRIER)
 #define NERF_TU_DIAG_FUSED NERF_BUILD_DIAG_FUSED
 #else
 #define NERF_TU_DIAG_FUSED 0

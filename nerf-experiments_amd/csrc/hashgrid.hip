@@ -1070,6 +1070,7 @@ size_t round256(size_t v) { return (v + 255) & ~(size_t)255; }
 // not eligible (no hashed level, more than BUCKET_MAXP parts a level, or n outside [1, 2^31)).
 struct BucketLayout {
     int first = 0, nparts = 0, rpp = 0;
+    int pack_bits = 0;      // > 0: 8-byte packed entries (two arrays' room), else three 4-byte arrays
     int64_t cap = 0;
     size_t bytes = 0;
 };
@@ -1089,7 +1090,17 @@ BucketLayout bucket_layout(const nerf_hashgrid_params* p, int64_t n) {
     if (first == L || b.nparts > BUCKET_MAXP || n < 1 || n >= ((int64_t)1 << 31)) return b;
     b.cap = ((8 * n * 5 / 4) / ((int64_t)b.nparts * BUCKET_SUB) + 4096 + 63) / 64 * 64;
     const int64_t nb = (int64_t)(L - first) * b.nparts * BUCKET_SUB;       // sub-buckets
-    b.bytes = round256((size_t)nb * sizeof(unsigned)) + 3 * round256((size_t)nb * b.cap * sizeof(unsigned));
+    // 8-byte entries when the sample index among a sub-bucket's workgroups and the row fit 32 bits
+    // together (C5's fine pass: 82 176 x 10 240 rows); NERF_HG_PACK=0: 12-byte entries (1538 vs
+    // 1474 us with the ballot grouping, profiles/r04v).  The packed form needs two arrays' room, not
+    // three (~0.7 GB less workspace per C5 fine-pass backward)
+    int rb = 0;
+    while ((1 << rb) < b.rpp) ++rb;
+    const int64_t li_max = ((n + 255) / 256 + BUCKET_SUB - 1) / BUCKET_SUB * 256;
+    b.pack_bits = (env_mode("NERF_HG_PACK", NERF_HG_PACK_DEFAULT) == 1 && rb < 32 && li_max <= ((int64_t)1 << (32 - rb)))
+                      ? rb : 0;
+    b.bytes = round256((size_t)nb * sizeof(unsigned)) +
+              (b.pack_bits > 0 ? 2 : 3) * round256((size_t)nb * b.cap * sizeof(unsigned));
     return b;
 }
 size_t bucket_offset(const nerf_hashgrid_params* p, int64_t n) {
@@ -1261,17 +1272,13 @@ extern "C" int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float
             bp.count = reinterpret_cast<unsigned*>(bb);
             bp.en = reinterpret_cast<unsigned*>(bb + round256((size_t)nb * sizeof(unsigned)));
             bp.er = bp.en + round256((size_t)nb * bl.cap * sizeof(unsigned)) / sizeof(unsigned);
-            bp.ew = reinterpret_cast<float*>(bp.er + round256((size_t)nb * bl.cap * sizeof(unsigned)) / sizeof(unsigned));
+            // (the packed form stores uint2 entries over en and er and never touches ew)
+            bp.ew = bl.pack_bits > 0 ? nullptr
+                                     : reinterpret_cast<float*>(bp.er + round256((size_t)nb * bl.cap * sizeof(unsigned)) /
+                                                                            sizeof(unsigned));
             if (hipMemsetAsync(bp.count, 0, (size_t)nb * sizeof(unsigned), s) != hipSuccess) return NERF_ERR_LAUNCH;
             bp.chunks = BUCKET_SUB;
-            // 8-byte entries when the sample index among a sub-bucket's workgroups and the row fit 32
-            // bits together (C5's fine pass: 82 176 x 10 240 rows); NERF_HG_PACK=0: 12-byte entries
-            // (1538 vs 1474 us with the ballot grouping, profiles/r04v)
-            static const int pack_mode = env_mode("NERF_HG_PACK", NERF_HG_PACK_DEFAULT);
-            int rb = 0;
-            while ((1 << rb) < bl.rpp) ++rb;
-            const int64_t li_max = ((n_samples + 255) / 256 + BUCKET_SUB - 1) / BUCKET_SUB * 256;
-            bp.pack_bits = (pack_mode == 1 && rb < 32 && li_max <= ((int64_t)1 << (32 - rb))) ? rb : 0;
+            bp.pack_bits = bl.pack_bits;
             switch (params->features) {
                 case 1: launch_bucket<1>(s, a, bp, nh, grad_out, g_ld, gt_bucket, gmax, acc); break;
                 case 2: launch_bucket<2>(s, a, bp, nh, grad_out, g_ld, gt_bucket, gmax, acc); break;

@@ -307,7 +307,7 @@ __device__ __forceinline__ void wwrite(Ctx& c, int slot, bf16x8 (&w)[DMA_PER_WAV
 #endif
 __device__ __forceinline__ void issue_dma(Ctx& c, int slot) {
     char* dst = c.smem + slot * SLOT_BYTES;
-#ifndef NERF_FUSED_NODMA          // diagnostic builds only: time the kernel without its weight stream
+#ifndef NERF_FUSED_DIAG_NODMA          // diagnostic builds only: time the kernel without its weight stream
 #pragma unroll
     for (int i = 0; i < DMA_PER_WAVE; ++i) {
         const int u = (c.wave + NWAVE * i) & (c.d_units - 1);   // d_units: 8 or 16
@@ -640,7 +640,7 @@ __device__ __forceinline__ void pair_stores(const Ctx& c, const LayerState& st, 
 // every store dropped), -1: decided at run time
 template <int MODE, int EPAR = -1>
 __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, f4 (&a)[SB], f4 b) {
-#ifdef NERF_FUSED_NOEPI           // diagnostic builds only (timing without the chunk epilogues)
+#ifdef NERF_FUSED_DIAG_NOEPI           // diagnostic builds only (timing without the chunk epilogues)
     return;
 #endif
 #ifdef NERF_FUSED_DIAG_MFMAONLY   // diagnostic: the epilogue reduced to one add (the MFMAs stay live)
@@ -1117,7 +1117,7 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
             // chunk and followed by >= AFTER_DMA_VM vector-memory ops), then everyone else's; the
             // other slot is free
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AFTER_DMA_VM) : "memory");
-#ifndef NERF_FUSED_NOBARRIER      // diagnostic builds only (timing without the per-chunk barrier)
+#ifndef NERF_FUSED_DIAG_NOBARRIER      // diagnostic builds only (timing without the per-chunk barrier)
             barrier();
 #endif
             first_reads<KBR, 0>(fr, sa);

@@ -64,8 +64,15 @@ def test_every_diagnostic_switch_is_reported():
     listed = set(re.findall(r"defined\((NERF_\w*DIAG\w*)\)", common))
     used = set()
     for f in os.listdir(csrc):
-        if f.endswith(".hip"):
-            used |= set(re.findall(r"\b(NERF_\w*_DIAG_\w+)\b", open(os.path.join(csrc, f)).read()))
+        if f.endswith((".hip", ".h")) and f != "common.h":
+            src = open(os.path.join(csrc, f)).read()
+            used |= set(re.findall(r"\b(NERF_\w*_DIAG_\w+)\b", src))
+            # any switch next to a "diagnostic" comment, whatever its name, must be a listed DIAG switch
+            for line in src.splitlines():
+                m = re.match(r"\s*#\s*if(?:n?def)?\s+(?:defined\()?(NERF_\w+)", line)
+                if m and "diagnostic" in line:
+                    assert "_DIAG_" in m.group(1), line
+                    used.add(m.group(1))
     assert used and used <= listed, sorted(used - listed)
 
 

@@ -4,7 +4,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "nerf-experiments_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "nerf-experiments_amd"))
 from nerf_amd import mlp  # noqa: E402
 from nerf_amd import model_interpolation_architecture as A  # noqa: E402
 from nerf_amd.model_ingp import FourierFeatures, INGPEncoding, NaiveINGP  # noqa: E402
