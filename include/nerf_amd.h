@@ -47,7 +47,7 @@ extern "C" {
 
 /* Library / ABI version (bumped on any signature or data-layout change; 6: NERF_FUSED_MASK;
  * 7: nerf_fused_composite / nerf_mlp_fused_render; 8: nerf_hashgrid_workspace_n, fused compositing
- * of 256-sample rays). */
+ * of 256-sample rays; 9: nerf_hashgrid_bwd_pos, seg_gen on later layers of the fused forward). */
 int nerf_abi_version(void);
 const char* nerf_status_string(int status);
 /* sizeof of the argument structs, for bindings to check their layouts against:
@@ -612,6 +612,20 @@ int nerf_hashgrid_bwd(const nerf_hashgrid_params* params, const float* x, const 
                       const float* ray_d, const float* t_start, const float* t_end, int64_t n_samples,
                       int32_t samples_per_ray, const float* grad_out, int64_t g_ld, float* grad_table,
                       int32_t accumulate, void* workspace, size_t workspace_bytes, void* stream);
+/* (ABI 9) Gradient of sum(out * grad_out) w.r.t. the positions, through the multilinear weights
+ * (w_k = prod_d (1 - |x_hat_d - c_kd|) on the unclipped corner, x_hat = (p / 8 + 0.5) r, or p r
+ * unnormalised; torch's abs backward: sign(0) = 0; corners and rows are constants of p):
+ *   dL/dp_d = sum_l ((sum_k G_lk (-sign(x_hat_d - c_kd)) prod_{e != d} (1 - |x_hat_e - c_ke|)) r_l) / 8,
+ * G_lk = sum_f grad_out[n][l F + f] table[l][row_k][f], levels and corners in order (deterministic).
+ * x != NULL: grad_x [n][3] (ray pointers NULL).  Ray form (x == NULL, samples p = o + t_q d,
+ * n_samples a multiple of samples_per_ray): grad_o / grad_d [n_rays][3] (either may be NULL) =
+ * sum over each ray's samples of dL/dp / of t_q dL/dp; workspace >= n_samples * 12 bytes, 16-byte
+ * aligned.  accumulate: += into the outputs. */
+int nerf_hashgrid_bwd_pos(const nerf_hashgrid_params* params, const float* x, const float* ray_o,
+                          const float* ray_d, const float* t_start, const float* t_end, int64_t n_samples,
+                          int32_t samples_per_ray, const float* table, const float* grad_out, int64_t g_ld,
+                          float* grad_x, float* grad_o, float* grad_d, int32_t accumulate, void* workspace,
+                          size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Camera-pose alignment: CameraCalibrationModel.kabsch_algorithm

@@ -137,10 +137,10 @@ __device__ __forceinline__ void composite_bwd_ray(const CompositeArgs& a, int64_
         const int s = r * NERF_WAVE + lane;
         float sig;
         if (a.act) {
-            sig = softplus_thr8(rawd[r] - a.shift);
-            c[r][0] = sigmoidf_(rawc[r][0]);
-            c[r][1] = sigmoidf_(rawc[r][1]);
-            c[r][2] = sigmoidf_(rawc[r][2]);
+            sig = comp_softplus(rawd[r] - a.shift);
+            c[r][0] = comp_sigmoid(rawc[r][0]);
+            c[r][1] = comp_sigmoid(rawc[r][1]);
+            c[r][2] = comp_sigmoid(rawc[r][2]);
         } else {
             sig = rawd[r];
             c[r][0] = rawc[r][0]; c[r][1] = rawc[r][1]; c[r][2] = rawc[r][2];
@@ -148,11 +148,11 @@ __device__ __forceinline__ void composite_bwd_ray(const CompositeArgs& a, int64_
         float bb = ((-sig) * del[r]) * a.sa;
         bb = bb * a.sb;
         if (s >= a.S) bb = 0.f;
-        e[r] = expf(bb);
+        e[r] = comp_exp(bb);
         const double incl = wave_inclusive_scan((double)bb);
         const double ex = carry + (incl - (double)bb);
         carry += __shfl(incl, NERF_WAVE - 1, NERF_WAVE);
-        T[r] = (s == 0) ? 1.0f : expf((float)ex);
+        T[r] = (s == 0) ? 1.0f : comp_exp((float)ex);
         w[r] = T[r] * (1.0f - e[r]);
         float gwr = 0.f;
         if (s < a.S) {

@@ -11,6 +11,22 @@
 
 namespace nerf {
 
+#if NERF_COMP_FASTEXP
+// (A/B experiment) e^x from the hardware 2^x with the exponent product split, ~2 ulp
+__device__ __forceinline__ float comp_exp(float x) {
+    const float L = 1.44269502162933349609375f;              // log2(e) rounded to fp32
+    const float p = x * L;
+    const float lo = __builtin_fmaf(x, L, -p) + x * 1.925963033500011e-08f;   // x (log2 e - L)
+    return __builtin_amdgcn_exp2f(p) * __builtin_fmaf(lo, 0.693147182464599609375f, 1.0f);
+}
+__device__ __forceinline__ float comp_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + comp_exp(-x)); }
+__device__ __forceinline__ float comp_softplus(float x) { return x > 8.0f ? x : log1pf(comp_exp(x)); }
+#else
+__device__ __forceinline__ float comp_exp(float x) { return expf(x); }
+__device__ __forceinline__ float comp_sigmoid(float x) { return sigmoidf_(x); }
+__device__ __forceinline__ float comp_softplus(float x) { return softplus_thr8(x); }
+#endif
+
 // rd / del / rc: raw density, interval length, raw (act) or activated colour of the lane's samples
 // (anything past S is ignored).  Outputs: w[r] (valid for s < S), rgb (every lane: the wave sum).
 // COEF: also the per-sample backward coefficients of the act = 1 form (include/nerf_amd.h,
@@ -30,10 +46,10 @@ __device__ __forceinline__ void composite_ray(int S, float sa, float sb, int act
         float sig = rd[r];
         c[r][0] = rc[r][0]; c[r][1] = rc[r][1]; c[r][2] = rc[r][2];
         if (act && s < S) {
-            sig = softplus_thr8(sig - shift);
-            c[r][0] = sigmoidf_(c[r][0]);
-            c[r][1] = sigmoidf_(c[r][1]);
-            c[r][2] = sigmoidf_(c[r][2]);
+            sig = comp_softplus(sig - shift);
+            c[r][0] = comp_sigmoid(c[r][0]);
+            c[r][1] = comp_sigmoid(c[r][1]);
+            c[r][2] = comp_sigmoid(c[r][2]);
         }
         // ((-sigma * delta) * 3) * MAGIC — two fp32 multiplies, as the reference.
         float bb = ((-sig) * del[r]) * sa;
@@ -42,8 +58,8 @@ __device__ __forceinline__ void composite_ray(int S, float sa, float sb, int act
         const double incl = wave_inclusive_scan_dpp((double)bb);
         const double ex = carry + (incl - (double)bb);      // exclusive prefix
         carry += wave_last_d(incl);
-        T[r] = (s == 0) ? 1.0f : expf((float)ex);
-        e[r] = expf(bb);
+        T[r] = (s == 0) ? 1.0f : comp_exp((float)ex);
+        e[r] = comp_exp(bb);
         w[r] = T[r] * (1.0f - e[r]);
         if (s < S) {
             acc0 += w[r] * c[r][0];

@@ -81,6 +81,9 @@ __global__ __launch_bounds__(256) void encode_fwd_kernel(EncArgs a, int Q, int R
 #ifndef NERF_ENC_ROWS
 #define NERF_ENC_ROWS 64
 #endif
+#ifndef NERF_ENC_NT
+#define NERF_ENC_NT 0
+#endif
 constexpr int kEncRows = NERF_ENC_ROWS;
 constexpr int kEncMaxLd = 128;
 
@@ -152,8 +155,14 @@ __global__ __launch_bounds__(256) void encode_fwd_lds_kernel(EncArgs a) {
     for (int i = t; i < stores; i += 256) {
         const int r = pow2 ? i >> qsh : i / Q;
         const int qd = i - r * Q;
+#if NERF_ENC_NT
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v v = *reinterpret_cast<const f4v*>(img + r * lds_ld + 4 * qd);
+        __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(a.out + (n0 + r) * a.ld + 4 * qd));
+#else
         const float4 v = *reinterpret_cast<const float4*>(img + r * lds_ld + 4 * qd);
         *reinterpret_cast<float4*>(a.out + (n0 + r) * a.ld + 4 * qd) = v;
+#endif
     }
 }
 

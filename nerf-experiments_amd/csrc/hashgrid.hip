@@ -984,6 +984,94 @@ __global__ __launch_bounds__(256) void hashgrid_finish_kernel(unsigned long long
     }
 }
 
+// ------------------------------------------------------------------- position gradient
+// dL/dp of the features' positions through the multilinear weights (3d-ingp/model.py:58-121 as
+// SURVEY §8(a) a9 restates it: w_k = prod_d (1 - |x_hat_d - c_kd|) on the unclipped corner c_k,
+// x_hat = (p / 8 + 0.5) r; autograd of torch.abs takes sign(0) = 0; the corners and rows are
+// constants of p).  With G_k = sum_f g[l F + f] table[l][row_k][f]:
+//   dL/dx_hat_d = sum_k G_k (-sign(x_hat_d - c_kd)) prod_{e != d} (1 - |x_hat_e - c_ke|),
+//   dL/dp_d     = sum_l (dL/dx_hat_d r_l) / 8  (r_l without normalisation),
+// levels and corners added in order (fp32, fixed order: deterministic).  One thread per sample.
+__global__ __launch_bounds__(256) void hashgrid_bwd_pos_kernel(HashArgs a, const float* __restrict__ table,
+                                                               const float* __restrict__ g, int64_t g_ld,
+                                                               float* __restrict__ dpos, int accumulate) {
+#pragma clang fp contract(off)
+    const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (n >= a.n) return;
+    const int L = a.p.levels, F = a.p.features, T = a.p.table_size;
+    float p[3];
+    sample_position(a, n, p);
+    float acc[3] = {0.0f, 0.0f, 0.0f};
+    for (int l = 0; l < L; ++l) {
+        const int r = a.p.res[l];
+        const Corners c = level_corners(p, a.p.normalize, r, T, a.p.primes);
+        // per dimension: the factor 1 - |u| and its derivative -sign(u), u = x_hat - corner, for the
+        // corner offsets 0 / 1 (the corner coordinates as level_corners forms them: int64 floor)
+        float fac[3][2], dfac[3][2];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const float xh = (a.p.normalize ? (p[j] / 8.0f + 0.5f) : p[j]) * (float)r;
+            const long long b = (long long)floorf(xh);
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const float u = xh - (float)(b + e);
+                fac[j][e] = 1.0f - fabsf(u);
+                dfac[j][e] = u > 0.0f ? -1.0f : (u < 0.0f ? 1.0f : 0.0f);
+            }
+        }
+        const float* tab = table + a.off[l] * F;
+        const float* gl = g + n * g_ld + (int64_t)l * F;
+        float gx[3] = {0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int ex = (k >> 2) & 1, ey = (k >> 1) & 1, ez = k & 1;   // z fastest
+            float G = 0.0f;
+            for (int f = 0; f < F; ++f) G = G + gl[f] * tab[(int64_t)c.idx[k] * F + f];
+            gx[0] = gx[0] + G * (dfac[0][ex] * (fac[1][ey] * fac[2][ez]));
+            gx[1] = gx[1] + G * (dfac[1][ey] * (fac[0][ex] * fac[2][ez]));
+            gx[2] = gx[2] + G * (dfac[2][ez] * (fac[0][ex] * fac[1][ey]));
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const float gr = gx[j] * (float)r;
+            acc[j] = acc[j] + (a.p.normalize ? gr / 8.0f : gr);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) dpos[n * 3 + j] = accumulate ? dpos[n * 3 + j] + acc[j] : acc[j];
+}
+
+// Ray form: p = o + t_q d, so dL/do = sum_s dL/dp_s and dL/dd = sum_s t_q,s dL/dp_s over each ray's
+// samples — one wave per ray, lane-strided partial sums then a fixed-order wave sum.
+__global__ __launch_bounds__(256) void hashgrid_pos_rays_kernel(HashArgs a, const float* __restrict__ dpos,
+                                                                int64_t n_rays, float* __restrict__ d_o,
+                                                                float* __restrict__ d_d, int accumulate) {
+#pragma clang fp contract(off)
+    const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (ray >= n_rays) return;
+    float so[3] = {0.0f, 0.0f, 0.0f}, sd[3] = {0.0f, 0.0f, 0.0f};
+    for (int s = lane; s < a.spr; s += 64) {
+        const int64_t n = ray * a.spr + s;
+        if (n >= a.n) break;
+        const float tq = (a.p.query == 0) ? a.t0[n] : (a.t0[n] + a.t1[n]) / 2.0f;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const float gp = dpos[n * 3 + j];
+            so[j] = so[j] + gp;
+            sd[j] = sd[j] + gp * tq;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const float to = wave_sum_f(so[j]), td = wave_sum_f(sd[j]);
+        if (lane == 0) {
+            if (d_o) d_o[ray * 3 + j] = accumulate ? d_o[ray * 3 + j] + to : to;
+            if (d_d) d_d[ray * 3 + j] = accumulate ? d_d[ray * 3 + j] + td : td;
+        }
+    }
+}
+
 bool valid_params(const nerf_hashgrid_params* p) {
     if (p == nullptr || p->levels < 1 || p->levels > NERF_HASHGRID_MAX_LEVELS) return false;
     if (p->features < 1 || p->features > NERF_HASHGRID_MAX_FEATURES || p->table_size < 1) return false;
@@ -1046,6 +1134,39 @@ extern "C" int nerf_hashgrid_fwd(const nerf_hashgrid_params* params, const float
                            out, out_ld);
     }
     NERF_CHECK_LAUNCH();
+    return NERF_OK;
+}
+
+extern "C" int nerf_hashgrid_bwd_pos(const nerf_hashgrid_params* params, const float* x, const float* ray_o,
+                                     const float* ray_d, const float* t_start, const float* t_end, int64_t n_samples,
+                                     int32_t samples_per_ray, const float* table, const float* grad_out, int64_t g_ld,
+                                     float* grad_x, float* grad_o, float* grad_d, int32_t accumulate, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+    NERF_REQUIRE(valid_params(params) && table != nullptr && grad_out != nullptr && n_samples >= 0);
+    NERF_REQUIRE(g_ld >= (int64_t)params->levels * params->features);
+    if (x != nullptr) {
+        NERF_REQUIRE(grad_x != nullptr && grad_o == nullptr && grad_d == nullptr);
+    } else {
+        NERF_REQUIRE(ray_o && ray_d && t_start && samples_per_ray >= 1 && (params->query == 0 || t_end));
+        NERF_REQUIRE(grad_x == nullptr && (grad_o != nullptr || grad_d != nullptr));
+        NERF_REQUIRE(n_samples % samples_per_ray == 0);
+        if (workspace == nullptr || workspace_bytes < (size_t)n_samples * 3 * sizeof(float)) return NERF_ERR_WORKSPACE;
+        NERF_REQUIRE(aligned16(workspace));
+    }
+    if (n_samples == 0) return NERF_OK;
+    NERF_REQUIRE((n_samples + 255) / 256 < (1ll << 31));
+    const HashArgs a = make_args(params, x, ray_o, ray_d, t_start, t_end, n_samples, samples_per_ray);
+    hipStream_t st = as_stream(stream);
+    float* dpos = x != nullptr ? grad_x : static_cast<float*>(workspace);
+    hipLaunchKernelGGL(hashgrid_bwd_pos_kernel, dim3((unsigned)((n_samples + 255) / 256)), dim3(256), 0, st, a, table,
+                       grad_out, g_ld, dpos, x != nullptr ? accumulate : 0);
+    NERF_CHECK_LAUNCH();
+    if (x == nullptr) {
+        const int64_t rays = n_samples / samples_per_ray;
+        hipLaunchKernelGGL(hashgrid_pos_rays_kernel, dim3((unsigned)((rays + 3) / 4)), dim3(256), 0, st, a, dpos, rays,
+                           grad_o, grad_d, accumulate);
+        NERF_CHECK_LAUNCH();
+    }
     return NERF_OK;
 }
 

@@ -240,6 +240,8 @@ _SIGNATURES = {
     "nerf_hashgrid_table_rows": (c_i64, [ctypes.POINTER(NerfHashgridParams), c_i32]),
     "nerf_hashgrid_bwd": (c_i32, [ctypes.POINTER(NerfHashgridParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
                                   c_vp, c_i64, c_vp, c_i32, c_vp, c_sz, c_vp]),
+    "nerf_hashgrid_bwd_pos": (c_i32, [ctypes.POINTER(NerfHashgridParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
+                                      c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i32, c_vp, c_sz, c_vp]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES.keys())
@@ -265,7 +267,7 @@ def load(path: str | None = None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.nerf_abi_version() != 8:
+    if lib.nerf_abi_version() != 9:
         raise RuntimeError("nerf_amd: ABI version mismatch between Python binding and libnerf_amd.so")
     for which, st in enumerate(STRUCTS):
         if lib.nerf_struct_size(which) != ctypes.sizeof(st):

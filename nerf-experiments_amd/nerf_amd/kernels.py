@@ -724,6 +724,39 @@ def hashgrid_workspace_bytes(params, n_samples: int | None = None) -> int:
     return int(size)
 
 
+def hashgrid_bwd_pos(params, table: torch.Tensor, grad_out: torch.Tensor, *, x=None, ray_o=None, ray_d=None,
+                     t_start=None, t_end=None, n_samples: int, samples_per_ray: int = 1, want_o: bool = True,
+                     want_d: bool = True):
+    """Position gradient through the hash grid (nerf_hashgrid_bwd_pos): grad_x [n, 3] for explicit
+    positions, else (grad_o, grad_d) [n_rays, 3] (None where not wanted) for ray-mode samples."""
+    _require_cuda_f32("grad_out", grad_out)
+    _hashgrid_table_check("table", params, table)
+    if grad_out.dim() != 2 or grad_out.stride(1) != 1 or grad_out.shape[0] < n_samples \
+            or grad_out.shape[1] < params.levels * params.features:
+        raise ValueError(f"grad_out must be a row-major [>= {n_samples}, >= {params.levels * params.features}] "
+                         f"tensor (got {tuple(grad_out.shape)})")
+    _hashgrid_inputs(params, n_samples, x, ray_o, ray_d, t_start, t_end, samples_per_ray)
+    dev = grad_out.device
+    lib = _lib.load()
+    if x is not None:
+        gx = torch.empty(n_samples, 3, device=dev, dtype=torch.float32)
+        st = lib.nerf_hashgrid_bwd_pos(ctypes.byref(params), _ptr(x), None, None, None, None, n_samples, 1,
+                                       table.data_ptr(), grad_out.data_ptr(), grad_out.stride(0), gx.data_ptr(),
+                                       None, None, 0, None, 0, _stream(dev))
+        _lib.check(st, "nerf_hashgrid_bwd_pos")
+        return gx
+    rays = n_samples // samples_per_ray
+    go = torch.empty(rays, 3, device=dev, dtype=torch.float32) if want_o else None
+    gd = torch.empty(rays, 3, device=dev, dtype=torch.float32) if want_d else None
+    ws = torch.empty(max(1, n_samples * 3), device=dev, dtype=torch.float32)
+    st = lib.nerf_hashgrid_bwd_pos(ctypes.byref(params), None, _ptr(ray_o), _ptr(ray_d), _ptr(t_start), _ptr(t_end),
+                                   n_samples, samples_per_ray, table.data_ptr(), grad_out.data_ptr(),
+                                   grad_out.stride(0), None, _ptr(go), _ptr(gd), 0, ws.data_ptr(),
+                                   ws.numel() * 4, _stream(dev))
+    _lib.check(st, "nerf_hashgrid_bwd_pos")
+    return go, gd
+
+
 def hashgrid_bwd(params, grad_out: torch.Tensor, grad_table: torch.Tensor, workspace: torch.Tensor, *, x=None,
                  ray_o=None, ray_d=None, t_start=None, t_end=None, n_samples: int, samples_per_ray: int = 1,
                  accumulate: bool = False) -> None:

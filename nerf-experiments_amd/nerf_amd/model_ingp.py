@@ -16,8 +16,8 @@ the renderer):
   ``forward(x)`` = the levels' features of x / 8 + 0.5, concatenated (model.py:92-121).  The level
   Parameters are views of one packed buffer (re-established after ``.to()`` / ``load_state_dict``
   or any reassignment), so one kernel launch reads every level; the table gradient is the
-  deterministic fixed-point nerf_hashgrid_bwd.  Positions receive no gradient (the renderer's
-  rays are data).
+  deterministic fixed-point nerf_hashgrid_bwd; positions (x, or the rays' origins / directions)
+  receive theirs through the multilinear weights (nerf_hashgrid_bwd_pos, round 5).
 * ``FourierFeatures(levels)`` — 3d-ingp's own encoding: [cos(x 2^k) | sin(x 2^k)], scale 1
   (model.py:124-148; nerf_encode_fwd kind 0).
 * ``NerfModelINGP(n_hidden, hidden_dim, position_encoder, direction_encoder)`` — ``model_density``
@@ -63,15 +63,6 @@ def ingp_resolutions(n_levels: int = 16, resolution_min: int = 16, resolution_ma
     """floor(resolution_min * b^l) in the reference's fp32 tensor arithmetic (2d-ingp/model.py:101-103)."""
     b = 1 if n_levels == 1 else math.exp((math.log(resolution_max) - math.log(resolution_min)) / (n_levels - 1))
     return [int(r) for r in th.floor(resolution_min * b ** th.arange(n_levels))]
-
-
-def _refuse_position_grad(*ts) -> None:
-    """The table gradient is implemented, the position gradient is not: the reference's trilinear
-    weights 1 - |x r - corner| would carry one (3d-ingp/model.py:58-121), so a caller that needs it
-    (pose refinement through a hash grid) is refused instead of silently getting none."""
-    if th.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts):
-        raise ValueError("INGPEncoding: no position gradient through the hash grid on this path; "
-                         "pass detached positions / rays")
 
 
 # Hash-grid features generated inside the fused field-MLP forward (NERF_FUSE_HASH=1).  Off by default:
@@ -126,14 +117,15 @@ class _HashGridFn(th.autograd.Function):
         ctx.params = params
         ctx.rows = rows
         ctx.meta = (samples_per_ray, n, packed.shape)
-        ctx.save_for_backward(*(t if t is not None else th.empty(0) for t in (x, ray_o, ray_d, t_start, t_end)))
+        ctx.save_for_backward(*(t if t is not None else th.empty(0) for t in (x, ray_o, ray_d, t_start, t_end, packed)))
         return out
 
     @staticmethod
     def backward(ctx, g):
         spr, n, shape = ctx.meta
-        x, o, d, t0, t1 = (t if t.numel() else None for t in ctx.saved_tensors)
+        x, o, d, t0, t1, packed = (t if t.numel() else None for t in ctx.saved_tensors)
         grads = [None] * len(ctx.rows)
+        gx = go = gd = None
         if g is not None and any(ctx.needs_input_grad[12:]):
             gp = th.empty(shape, device=g.device, dtype=th.float32)
             ws = th.empty((K.hashgrid_workspace_bytes(ctx.params, n) + 7) // 8, dtype=th.int64, device=g.device)
@@ -143,7 +135,16 @@ class _HashGridFn(th.autograd.Function):
             for l, r in enumerate(ctx.rows):
                 grads[l] = gp[off:off + r]
                 off += r
-        return (None,) * 12 + tuple(grads)
+        # the positions' gradient through the multilinear weights (nerf_hashgrid_bwd_pos), for
+        # explicit positions x or the rays' origins / directions
+        if g is not None and n > 0 and any(ctx.needs_input_grad[4:7]):
+            if x is not None:
+                gx = K.hashgrid_bwd_pos(ctx.params, packed, g.contiguous(), x=x, n_samples=n)
+            else:
+                go, gd = K.hashgrid_bwd_pos(ctx.params, packed, g.contiguous(), ray_o=o, ray_d=d, t_start=t0,
+                                            t_end=t1, n_samples=n, samples_per_ray=spr,
+                                            want_o=ctx.needs_input_grad[5], want_d=ctx.needs_input_grad[6])
+        return (None,) * 4 + (gx, go, gd) + (None,) * 5 + tuple(grads)
 
 
 class INGPTable(nn.Module):
@@ -257,16 +258,15 @@ class INGPEncoding(nn.Module):
         only ray-mode positions are generated inside the fused MLP)."""
         if x.dim() != 2 or x.shape[1] != 3:
             raise ValueError(f"x must be [N, 3] (got {tuple(x.shape)})")
-        _refuse_position_grad(x)
         x = x.contiguous()
         return self._run(x, None, None, None, None, 1, 1, x.shape[0])
 
     def encode_rays(self, ray_origs, ray_dirs, t_start, t_end, pixel_width, samples_per_ray: int, query: int,
                     pw_mode: int = 0, defer: bool = False) -> th.Tensor:
-        """Features of the samples o + t_q d generated in-kernel (rays that require grad are refused);
-        defer: the rows may be generated by the consuming fused field-MLP forward itself (only for a
-        tensor handed straight to the field MLP, as PositionalEncoding.encode_rays)."""
-        _refuse_position_grad(ray_origs, ray_dirs)
+        """Features of the samples o + t_q d generated in-kernel (rays that require grad get their
+        gradient through the multilinear weights, nerf_hashgrid_bwd_pos); defer: the rows may be
+        generated by the consuming fused field-MLP forward itself (only for a tensor handed straight
+        to the field MLP, as PositionalEncoding.encode_rays)."""
         n = t_start.numel()
         return self._run(None, ray_origs.contiguous(), ray_dirs.contiguous(),
                          t_start.detach().contiguous(), t_end.detach().contiguous(), samples_per_ray, query, n,

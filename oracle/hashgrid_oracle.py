@@ -162,6 +162,36 @@ def encode_backward(x: np.ndarray, grad_out: np.ndarray, res: list[int], table_s
     return grads
 
 
+def encode_position_grad(x: np.ndarray, tables: list[np.ndarray], res: list[int], table_size: int,
+                         grad_out: np.ndarray, primes=PRIMES, normalize: bool = True) -> np.ndarray:
+    """d sum(encode(x) * grad_out) / dx [N, 3] in float64: per level, torch autograd w.r.t. x_hat at
+    the fp32 x_hat the forward evaluates ((x / 8 + 0.5) r, or x r), through weights
+    prod_d (1 - |x_hat_d - c_d|) on the unclipped corner (corners floor(x_hat) + offsets and the
+    rows of level_corners are constants; abs backward sign(0) = 0), then dx_hat/dx = r / 8 (or r).
+    The reference computes this gradient with autograd through its fp32 ops (3d-ingp/model.py:58-121
+    as SURVEY §8(a) a9 restates it) — parity unpinned, as the 3-D hash grid itself."""
+    import torch
+    F = tables[0].shape[1]
+    gx = np.zeros((x.shape[0], 3), dtype=np.float64)
+    for l, (t, r) in enumerate(zip(tables, res)):
+        idx, _ = level_corners(x, r, table_size, primes, normalize)
+        u32 = normalised(x) if normalize else x.astype(np.float32)
+        xh32 = u32 * np.float32(r)
+        xh = torch.tensor(xh32.astype(np.float64), requires_grad=True)
+        base = torch.floor(torch.tensor(xh32.astype(np.float64)))
+        g = torch.tensor(grad_out[:, l * F:(l + 1) * F].astype(np.float64))
+        tt = torch.tensor(t.astype(np.float64))
+        total = torch.zeros((), dtype=torch.float64)
+        for k, off in enumerate(CORNERS_3D):
+            c = base + torch.tensor(off, dtype=torch.float64)
+            d = 1.0 - torch.abs(xh - c)
+            w = (d[:, 0] * d[:, 1]) * d[:, 2]
+            total = total + (w.unsqueeze(1) * tt[torch.from_numpy(idx[:, k])] * g).sum()
+        total.backward()
+        gx += xh.grad.numpy() * (r / 8.0 if normalize else float(r))
+    return gx
+
+
 def pack(tables: list[np.ndarray]) -> np.ndarray:
     """The kernels' packed layout: the levels' tables back to back, [sum rows, F]."""
     return np.concatenate(tables, axis=0)
