@@ -87,6 +87,12 @@ __global__ __launch_bounds__(256) void encode_fwd_kernel(EncArgs a, int Q, int R
 constexpr int kEncRows = NERF_ENC_ROWS;
 constexpr int kEncMaxLd = 128;
 
+// NERF_ENC_PERSIST (default 1): a grid of at most 8 blocks per CU walks the 64-row tiles (the
+// one-tile-per-block grid dispatched ~1 M blocks of ~1 us each at a full frame: the workgroup
+// dispatch, not HBM, paced the kernel at 3.5 TB/s); 0: one tile per block
+#ifndef NERF_ENC_PERSIST
+#define NERF_ENC_PERSIST 1
+#endif
 __global__ __launch_bounds__(256) void encode_fwd_lds_kernel(EncArgs a) {
 #pragma clang fp contract(off)
     extern __shared__ float img[];      // kEncRows x (ld + 4) floats (dynamic: sized to the row)
@@ -97,72 +103,76 @@ __global__ __launch_bounds__(256) void encode_fwd_lds_kernel(EncArgs a) {
     const int id = a.p.include_identity ? 3 : 0;
     const int ld = (int)a.ld;
     const int lds_ld = ld + 4;          // 16-byte aligned rows, staggered banks
-    const int64_t n0 = (int64_t)blockIdx.x * kEncRows;
-    const int rows = a.n - n0 < kEncRows ? (int)(a.n - n0) : kEncRows;
-    if (t < rows) {
-        const int64_t n = n0 + t;
-        float p[3], dv[3];
-        load_pos_dir(a, n, p, dv);
-        float* row = img + t * lds_ld;
-        if (a.p.kind == 1) {
-            const IpeSample q = ipe_sample(a.p, p, dv, a.t0[n], a.t1[n], a.pw ? pixel_width_at(a, n) : 0.f);
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                spm[t][d] = q.pm[d];
-                svb[t][d] = q.vb[d];
-            }
-        } else {
-#pragma unroll
-            for (int d = 0; d < 3; ++d) spm[t][d] = p[d];
-        }
-        for (int c = 0; c < id; ++c) row[c] = spm[t][c];
-        for (int c = a.out_dim; c < ld; ++c) row[c] = 0.0f;
-    }
-    __syncthreads();
-    // phase 1: thread t owns argument column j = t % TPR (fixed d, k, scale, mask for the whole
-    // block) and walks the rows r = t / TPR, + 256/TPR, ...: no per-task index arithmetic
+    const int64_t ntiles = (a.n + kEncRows - 1) / kEncRows;
     const int tl = 3 * L;
     const int TPR = tl <= 32 ? 32 : 64;
     const int j = t & (TPR - 1);
-    if (j < tl) {
-        const int dd = j >= 2 * L ? 2 : (j >= L ? 1 : 0);
-        const int k = j - dd * L;
-        const float s = a.p.scale * (float)(1u << k);
-        const float m = a.p.use_mask ? a.p.mask[k] : 1.0f;
-        const float sc4 = (float)(1u << (2 * k));
-        for (int r = t / TPR; r < rows; r += 256 / TPR) {
-            float sn, cs;
-            sincos_enc(spm[r][dd] * s, &sn, &cs);
-            if (a.p.kind == 1) {
-                const float w = expf((-(svb[r][dd] * sc4)) / 2.0f);
-                cs = cs * w;
-                sn = sn * w;
-            }
-            if (a.p.use_mask) {
-                cs = m * cs;
-                sn = m * sn;
-            }
-            float* row = img + r * lds_ld;
-            row[id + j] = cs;
-            row[id + tl + j] = sn;
-        }
-    }
-    __syncthreads();
+    const int dd = j >= 2 * L ? 2 : (j >= L ? 1 : 0);
+    const int k = j < tl ? j - dd * L : 0;                 // (threads past the tasks: unused)
+    const float s = a.p.scale * (float)(1u << k);
+    const float m = a.p.use_mask ? a.p.mask[k] : 1.0f;
+    const float sc4 = (float)(1u << (2 * k));
     const int Q = ld >> 2;
-    const int stores = rows * Q;
     const bool pow2 = (Q & (Q - 1)) == 0;
     const int qsh = __builtin_ctz((unsigned)Q);
-    for (int i = t; i < stores; i += 256) {
-        const int r = pow2 ? i >> qsh : i / Q;
-        const int qd = i - r * Q;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += (NERF_ENC_PERSIST ? (int64_t)gridDim.x : ntiles)) {
+        const int64_t n0 = tile * kEncRows;
+        const int rows = a.n - n0 < kEncRows ? (int)(a.n - n0) : kEncRows;
+        if (t < rows) {
+            const int64_t n = n0 + t;
+            float p[3], dv[3];
+            load_pos_dir(a, n, p, dv);
+            float* row = img + t * lds_ld;
+            if (a.p.kind == 1) {
+                const IpeSample q = ipe_sample(a.p, p, dv, a.t0[n], a.t1[n], a.pw ? pixel_width_at(a, n) : 0.f);
+#pragma unroll
+                for (int d = 0; d < 3; ++d) {
+                    spm[t][d] = q.pm[d];
+                    svb[t][d] = q.vb[d];
+                }
+            } else {
+#pragma unroll
+                for (int d = 0; d < 3; ++d) spm[t][d] = p[d];
+            }
+            for (int c = 0; c < id; ++c) row[c] = spm[t][c];
+            for (int c = a.out_dim; c < ld; ++c) row[c] = 0.0f;
+        }
+        __syncthreads();
+        // phase 1: thread t owns argument column j = t % TPR (fixed d, k, scale, mask for the whole
+        // block) and walks the rows r = t / TPR, + 256/TPR, ...: no per-task index arithmetic
+        if (j < tl) {
+            for (int r = t / TPR; r < rows; r += 256 / TPR) {
+                float sn, cs;
+                sincos_enc(spm[r][dd] * s, &sn, &cs);
+                if (a.p.kind == 1) {
+                    const float w = expf((-(svb[r][dd] * sc4)) / 2.0f);
+                    cs = cs * w;
+                    sn = sn * w;
+                }
+                if (a.p.use_mask) {
+                    cs = m * cs;
+                    sn = m * sn;
+                }
+                float* row = img + r * lds_ld;
+                row[id + j] = cs;
+                row[id + tl + j] = sn;
+            }
+        }
+        __syncthreads();
+        const int stores = rows * Q;
+        for (int i = t; i < stores; i += 256) {
+            const int r = pow2 ? i >> qsh : i / Q;
+            const int qd = i - r * Q;
 #if NERF_ENC_NT
-        typedef float f4v __attribute__((ext_vector_type(4)));
-        const f4v v = *reinterpret_cast<const f4v*>(img + r * lds_ld + 4 * qd);
-        __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(a.out + (n0 + r) * a.ld + 4 * qd));
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            const f4v v = *reinterpret_cast<const f4v*>(img + r * lds_ld + 4 * qd);
+            __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(a.out + (n0 + r) * a.ld + 4 * qd));
 #else
-        const float4 v = *reinterpret_cast<const float4*>(img + r * lds_ld + 4 * qd);
-        *reinterpret_cast<float4*>(a.out + (n0 + r) * a.ld + 4 * qd) = v;
+            const float4 v = *reinterpret_cast<const float4*>(img + r * lds_ld + 4 * qd);
+            *reinterpret_cast<float4*>(a.out + (n0 + r) * a.ld + 4 * qd) = v;
 #endif
+        }
+        if (NERF_ENC_PERSIST) __syncthreads();      // the image is rewritten by the next tile
     }
 }
 
@@ -379,6 +389,17 @@ __global__ __launch_bounds__(256) void encode_bwd_rays_kernel(EncArgs a, const f
     }
 }
 
+int enc_num_cus() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+    }
+    return n;
+}
+
 int out_dim_of(const nerf_pe_params& p) { return (2 * p.levels + (p.include_identity ? 1 : 0)) * 3; }
 
 }  // namespace
@@ -406,7 +427,8 @@ extern "C" int nerf_encode_fwd(const nerf_pe_params* params, const float* x, con
     EncArgs a{p, x, xdir, ray_o, ray_d, t_start, t_end, pixel_width, n_samples,
               samples_per_ray > 0 ? samples_per_ray : 1, n_rays, out, out_ld, od, vec};
     if (vec && out_ld <= kEncMaxLd) {
-        const int64_t blocks = (n_samples + kEncRows - 1) / kEncRows;
+        int64_t blocks = (n_samples + kEncRows - 1) / kEncRows;
+        if (NERF_ENC_PERSIST) blocks = blocks < 8 * enc_num_cus() ? blocks : 8 * enc_num_cus();
         const size_t lds = (size_t)kEncRows * (size_t)(out_ld + 4) * sizeof(float);
         hipLaunchKernelGGL(encode_fwd_lds_kernel, dim3((unsigned)blocks), dim3(256), lds, as_stream(stream), a);
     } else {
