@@ -11,8 +11,17 @@
 
 namespace nerf {
 
+// NERF_COMP_FASTEXP=1 (off): e^x from the hardware 2^x with the exponent product split (~2 ulp),
+// sigmoid through the hardware reciprocal, in the compositing (stand-alone and fused).  At a full
+// 800 x 800 frame composite_fwd 2.84 -> 3.17-3.26 TB/s, composite_bwd 2.84 -> 2.93-3.00 (profiles/
+// r05e, r05f); off because the parity bars of the compositing are set on the libm results and the
+// training step composites inside the fused MLP launches, where these kernels do not run.  Neither a
+// second ray's loads in flight nor two rays composited per iteration changed the rates (r05f, r05h):
+// the kernel waits on its instruction dependencies (SQ_WAIT_INST_ANY 53 % of wave cycles, r05g).
+#ifndef NERF_COMP_FASTEXP
+#define NERF_COMP_FASTEXP 0
+#endif
 #if NERF_COMP_FASTEXP
-// (A/B experiment) e^x from the hardware 2^x with the exponent product split, ~2 ulp
 __device__ __forceinline__ float comp_exp(float x) {
     const float L = 1.44269502162933349609375f;              // log2(e) rounded to fp32
     const float p = x * L;

@@ -17,6 +17,8 @@
 // libm sincosf made the kernel VALU-bound.  Wider / unaligned rows: one thread per 4 columns.
 // Floating-point contraction is off so every other fp32 operation rounds exactly where the
 // reference's does.
+#include <stddef.h>
+
 #include "common.h"
 #include "encode_common.h"
 
@@ -87,11 +89,12 @@ __global__ __launch_bounds__(256) void encode_fwd_kernel(EncArgs a, int Q, int R
 constexpr int kEncRows = NERF_ENC_ROWS;
 constexpr int kEncMaxLd = 128;
 
-// NERF_ENC_PERSIST (default 1): a grid of at most 8 blocks per CU walks the 64-row tiles (the
-// one-tile-per-block grid dispatched ~1 M blocks of ~1 us each at a full frame: the workgroup
-// dispatch, not HBM, paced the kernel at 3.5 TB/s); 0: one tile per block
+// NERF_ENC_PERSIST=1: a grid of at most 8 blocks per CU walks the 64-row tiles instead of one tile
+// per block — measured slower at a full 800 x 800 frame (2.62 vs 3.50 TB/s, profiles/r05e), and so
+// was a barrier-free form with each wave encoding its own 16 rows in a private LDS image (2.70 TB/s,
+// profiles/r05f): the dispatch of ~1 M short blocks does not pace this kernel
 #ifndef NERF_ENC_PERSIST
-#define NERF_ENC_PERSIST 1
+#define NERF_ENC_PERSIST 0
 #endif
 __global__ __launch_bounds__(256) void encode_fwd_lds_kernel(EncArgs a) {
 #pragma clang fp contract(off)

@@ -169,48 +169,6 @@ def _wgrad_rays(blocks, N4: int, lp, workspace, gW, gb, acc, split) -> None:
     K.linear_wgrad_reduce(Bt, N4, kray, lp.N, ws2, lp.col_map[kmain:kmain + kray], gW, None, accumulate=acc)
 
 
-# A layer wider than one 256-column tile (NerfModel's skip layer: [z (256) | encoding (64)] = 320
-# columns) as two single-tile launches over column groups, each the transposed-read kernel (the
-# multi-tile kernel ran such a layer at 0.58 ms per mip step), their reduces writing disjoint
-# weight columns (NERF_WGRAD_KSPLIT=0: the multi-tile kernel)
-WGRAD_KSPLIT = os.environ.get("NERF_WGRAD_KSPLIT", "1") != "0"
-
-
-def _k_split(blocks, N4: int):
-    """(segment count of the first column group) when the layer's inputs split into a first group of
-    exactly 256 padded columns and a rest of at most 256, every input per sample; None otherwise."""
-    if not WGRAD_KSPLIT or N4 > 256 or N4 <= 128:
-        return None
-    segs = blocks[0][1]
-    if any(rd != 1 for _, _, rd in segs):
-        return None
-    widths = [K.pad32(k) for _, k, _ in segs]
-    acc = 0
-    for i, w in enumerate(widths):
-        acc += w
-        if acc == 256:
-            rest = sum(widths[i + 1:])
-            return i + 1 if 0 < rest <= 256 else None
-        if acc > 256:
-            return None
-    return None
-
-
-def _wgrad_ksplit(blocks, N4: int, nrow: int, lp, workspace, gW, gb, acc, n1: int) -> None:
-    """The weight gradient of `blocks` (one or two passes' rows) over its two column groups (_k_split)."""
-    Mt = sum(M for _, _, M in blocks)
-    k1 = sum(K.pad32(k) for _, k, _ in blocks[0][1][:n1])
-    k2 = sum(K.pad32(k) for _, k, _ in blocks[0][1][n1:])
-    for part, (kcols, cmap, g_b) in enumerate(((k1, lp.col_map[:k1], gb), (k2, lp.col_map[k1:k1 + k2], None))):
-        sub = [(dZ, segs[:n1] if part == 0 else segs[n1:], M) for dZ, segs, M in blocks]
-        ws = _wgrad_workspace(workspace, Mt, N4, kcols)
-        if len(sub) > 1:
-            K.linear_wgrad_x3_rows(sub, nrow, ws)
-        else:
-            K.linear_wgrad_x3(sub[0][0], nrow, sub[0][1], sub[0][2], ws)
-        K.linear_wgrad_reduce(Mt, N4, kcols, lp.N, ws, cmap, gW, g_b, accumulate=acc)
-
-
 def _flush_wgrad(entry, sink) -> None:
     """A stashed pass whose partner never ran its backward (BucketedGradAllReduce.finish()): its
     weight gradient alone, landed as the sink expects."""
@@ -220,11 +178,8 @@ def _flush_wgrad(entry, sink) -> None:
     gb, _ = sink.target(b)
     ws = torch.empty((K.linear_wgrad_workspace_bytes(M, N4, lp.Kp) + 3) // 4, device=dZ.device, dtype=torch.float32)
     rsplit = _ray_split([(dZ, segs, M)], N4) if nrow == N4 else None
-    ksplit = _k_split([(dZ, segs, M)], N4) if nrow == N4 and rsplit is None else None
     if rsplit is not None:          # the route the unmerged backward takes: the same result, bitwise
         _wgrad_rays([(dZ, segs, M)], N4, lp, ws, gW, gb, acc, rsplit)
-    elif ksplit is not None:
-        _wgrad_ksplit([(dZ, segs, M)], N4, nrow, lp, ws, gW, gb, acc, ksplit)
     else:
         K.linear_wgrad_x3(dZ, nrow, segs, M, ws)
         K.linear_wgrad_reduce(M, N4, lp.Kp, lp.N, ws, lp.col_map, gW, gb, accumulate=acc)
@@ -726,16 +681,12 @@ class MLPFunction(torch.autograd.Function):
                         raise RuntimeError("direct gradient sink: weight and bias of one layer out of step")
                 else:
                     gW, gb, acc = torch.empty_like(w), torch.empty_like(lp.module.bias), False
-                rsplit = ksplit = None
+                rsplit = None
                 wblocks = [(prev[0], prev[1], prev[2]), (dZ, segs, M)] if prev is not None else [(dZ, segs, M)]
                 if ctx.prec == "x3" and nrow == N4:
                     rsplit = _ray_split(wblocks, N4)
-                    if rsplit is None:
-                        ksplit = _k_split(wblocks, N4)
                 if rsplit is not None:
                     _wgrad_rays(wblocks, N4, lp, workspace, gW, gb, acc, rsplit)
-                elif ksplit is not None:
-                    _wgrad_ksplit(wblocks, N4, nrow, lp, workspace, gW, gb, acc, ksplit)
                 elif prev is not None:
                     pdZ, psegs, pM = prev[0], prev[1], prev[2]
                     ws = _wgrad_workspace(workspace, M + pM, N4, lp.Kp)

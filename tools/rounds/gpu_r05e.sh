@@ -18,7 +18,7 @@ for lib in nerf_amd/libnerf_amd.so var/lib_encold.so var/lib_encnt.so var/lib_co
   python3 -c "import json;d=json.load(open('$O/frame_$(basename $lib .so).json'));f=d['roofline_hbm_frame'];print('$lib', f['frac'], {k:round(v['gbs']) for k,v in f['per_kernel'].items()})"
 done
 for rep in 1 2; do
-  for lib in nerf_amd/libnerf_amd.so var/lib_prio.so; do
+  for lib in nerf_amd/libnerf_amd.so var/lib_prio.so var/lib_sb2.so; do
     NERF_AMD_LIB=nerf-experiments_amd/$lib timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-frame-roofline --steps 100 --warmup 10 > $O/bench_$(basename $lib .so)_$rep.json 2>/dev/null || exit 1
     python3 -c "import json;d=json.load(open('$O/bench_$(basename $lib .so)_$rep.json'));k=d['kernel_functions'];print('$lib', d['ms_per_step'], k['mlp_fused_kernel<0>']['ms_per_step'], k['mlp_fused_kernel<1>']['ms_per_step'])"
   done
