@@ -32,6 +32,7 @@
 // is stored; waits are counted (asm fragment reads, a per-layer DMA table in VGPRs) so the
 // prefetch is never drained.
 #include <stddef.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <type_traits>
@@ -246,10 +247,12 @@ struct Ctx {
     bf16x8 gh[SB], gl[SB];
 };
 
-__device__ __forceinline__ int dma_units(Ctx& c, int l) { return LF(int, chunk_units, l); }
+template <class CT>
+__device__ __forceinline__ int dma_units(CT& c, int l) { return LF(int, chunk_units, l); }
 
 // first layer at or after l (cyclically) with a register-fed part (kernel prologue only)
-__device__ __forceinline__ int next_ring_layer(Ctx& c, int l) {
+template <class CT>
+__device__ __forceinline__ int next_ring_layer(CT& c, int l) {
     for (int i = 0; i < c.n_layers; ++i, l = (l + 1 == c.n_layers ? 0 : l + 1))
         if (dma_units(c, l) > 0) return l;
     return -1;
@@ -342,11 +345,12 @@ static_assert(SPW * (GEN_LD + 8) * 4 <= XIMG_BYTES, "generator scratch");
 // The per-sample inputs of encoding e for lanes < SPW (sample base + lane): o xyz, d xyz, t0, t1,
 // pixel width for ray-mode positions; x xyz for per-ray directions.  Loads only, so that the
 // tile's inputs of both encodings are in flight together (one memory round trip per tile).
-__device__ __forceinline__ void gen_load(const Ctx& c, int e, int base, float (&v)[9]) {
+template <int NS, class CT>
+__device__ __forceinline__ void gen_load(const CT& c, int e, int base, float (&v)[9]) {
 #pragma unroll
     for (int j = 0; j < 9; ++j) v[j] = 0.f;
     const int m = base + c.lane;
-    if (c.lane >= SPW || m >= c.M) return;
+    if (c.lane >= NS || m >= c.M) return;
     const int per_ray = EF(int, per_ray, e);
     const unsigned S = (unsigned)EF(int, samples_per_ray, e);
     const float* ray_d = EF(cfptr_t, ray_d, e);
@@ -372,13 +376,14 @@ __device__ __forceinline__ void gen_load(const Ctx& c, int e, int base, float (&
 // hashgrid_fwd_tile_kernel computes them (hashgrid_common.h: the same corner arithmetic, the 8
 // corners' feature loads issued before the sums, products rounded then added in corner order):
 // the samples' positions first (lanes < SPW), then one level per trip.
-__device__ __forceinline__ void gen_hash_rows(const Ctx& c, int base, const float (&v)[9]) {
+template <int NS, class CT>
+__device__ __forceinline__ void gen_hash_rows(const CT& c, int base, const float (&v)[9]) {
 #pragma clang fp contract(off)
-    float* R = reinterpret_cast<float*>(c.ximg);          // [SPW][GEN_LD]
-    float* P = R + SPW * GEN_LD;                            // [SPW][8]: position xyz
+    float* R = reinterpret_cast<float*>(c.ximg);          // [NS][GEN_LD]
+    float* P = R + NS * GEN_LD;                             // [NS][8]: position xyz
     const int L = HG(int32_t, levels), F = HG(int32_t, features), T = HG(int32_t, table_size);
     const int cols = L * F;
-    if (c.lane < SPW) {
+    if (c.lane < NS) {
         float p[3] = {0.f, 0.f, 0.f};
         if (base + c.lane < c.M) {
             // as sample_position (hashgrid.hip): o + tq d
@@ -412,7 +417,7 @@ __device__ __forceinline__ void gen_hash_rows(const Ctx& c, int base, const floa
     const float* table = *(const __attribute__((address_space(4))) cfptr_t*)(c.kargs + offsetof(FusedArgs, hg_table));
     for (int l = 0; l < L; ++l) {
         const int rl = res[l], ol = offs[l];
-        if (c.lane < SPW) {
+        if (c.lane < NS) {
             const int r = c.lane;
             const float p[3] = {P[r * 8 + 0], P[r * 8 + 1], P[r * 8 + 2]};
             const Corners cn = level_corners(p, normalize, rl, T, pr);
@@ -436,19 +441,20 @@ __device__ __forceinline__ void gen_hash_rows(const Ctx& c, int base, const floa
 }
 
 // Rows of encoding e from its inputs (gen_load) into the wave's LDS scratch.
-__device__ __forceinline__ void gen_rows_lds(const Ctx& c, int e, int base, const float (&v)[9]) {
+template <int NS, class CT>
+__device__ __forceinline__ void gen_rows_lds(const CT& c, int e, int base, const float (&v)[9]) {
 #pragma clang fp contract(off)
-    float* R = reinterpret_cast<float*>(c.ximg);          // [SPW][GEN_LD]
-    float* P = R + SPW * GEN_LD;                            // [SPW][8]: pm xyz, vb xyz
+    float* R = reinterpret_cast<float*>(c.ximg);          // [NS][GEN_LD]
+    float* P = R + NS * GEN_LD;                             // [NS][8]: pm xyz, vb xyz
     const __attribute__((address_space(4))) nerf_pe_params& prm = EF(nerf_pe_params, params, e);
     if (prm.kind == 2) {
-        gen_hash_rows(c, base, v);
+        gen_hash_rows<NS>(c, base, v);
         return;
     }
     const int per_ray = EF(int, per_ray, e);
     const int out_dim = EF(int, out_dim, e);
     const int L = prm.levels, id = prm.include_identity ? 3 : 0;
-    if (c.lane < SPW) {
+    if (c.lane < NS) {
         float pm[3] = {0.f, 0.f, 0.f}, vb[3] = {0.f, 0.f, 0.f};
         if (base + c.lane < c.M) {
             // as load_pos_dir (encode_common.h): x, or o + tq d
@@ -481,7 +487,7 @@ __device__ __forceinline__ void gen_rows_lds(const Ctx& c, int e, int base, cons
     const GenArgs a{prm, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1, 1};
     // (same wave: its LDS operations complete in order, so the terms above are visible below)
     const int na = 3 * L;
-    for (int i = c.lane; i < SPW * na; i += 64) {
+    for (int i = c.lane; i < NS * na; i += 64) {
         const int r = i / na, j = i - r * na;
         const int dd = j >= 2 * L ? 2 : (j >= L ? 1 : 0);
         const int k = j - dd * L;
@@ -507,14 +513,15 @@ __device__ __forceinline__ void gen_rows_lds(const Ctx& c, int e, int base, cons
 // The generated rows of the wave's samples into the encoding's rows in HBM (read back by later
 // layers of the launch and by the weight gradients; a per-ray encoding by the ray's first sample):
 // each instruction stores 1 KB of consecutive 16-byte row pieces.
-__device__ __forceinline__ void gen_store(const Ctx& c, int e, int base) {
+template <int NS, class CT>
+__device__ __forceinline__ void gen_store(const CT& c, int e, int base) {
     const float* R = reinterpret_cast<const float*>(c.ximg);
     float* out = EF(fptr_t, out, e);
     const int per_ray = EF(int, per_ray, e);
     const unsigned S = (unsigned)EF(int, samples_per_ray, e);
     const int ld = (int)EF(int64_t, ld, e);
     const int q4 = ld >> 2;                                   // 16-byte pieces per row (ld <= 64)
-    for (int i = c.lane; i < SPW * q4; i += 64) {
+    for (int i = c.lane; i < NS * q4; i += 64) {
         const int r = i / q4, q = i - r * q4;
         const int m = base + r;
         if (m < c.M && (!per_ray || (unsigned)m % S == 0u)) {
@@ -525,7 +532,8 @@ __device__ __forceinline__ void gen_store(const Ctx& c, int e, int base) {
 }
 
 // Columns col .. col + 7 of generated row r (gen_rows_lds), split into the bf16 hi/lo operand halves.
-__device__ __forceinline__ void gen_block(const Ctx& c, int r, int col, bf16x8& h, bf16x8& lo) {
+template <class CT>
+__device__ __forceinline__ void gen_block(const CT& c, int r, int col, bf16x8& h, bf16x8& lo) {
     const float* R = reinterpret_cast<const float*>(c.ximg) + r * GEN_LD + col;
     const f4 v0 = *reinterpret_cast<const f4*>(R), v1 = *reinterpret_cast<const f4*>(R + 4);
     split8(__builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7), h, lo);
@@ -1232,9 +1240,9 @@ constexpr int COMP_SMAX = 2 * TILE;
 constexpr int COMP_DEL = COMP_SMAX * 16;
 static_assert(COMP_OFF >= SB * 2048 && COMP_OFF + COMP_SMAX * 20 <= XIMG_BYTES, "composite scratch");
 
-template <int R>
-__device__ __forceinline__ void composite_wave(Ctx& c, int64_t ray, int S) {
-    const char* reg = c.ximg + COMP_OFF;
+template <int R, class CT>
+__device__ __forceinline__ void composite_wave(CT& c, int64_t ray, int S, int roff = 0) {
+    const char* reg = c.ximg + COMP_OFF + roff;
     float rd[R], del[R], rc[R][3];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -1410,8 +1418,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
             // loaded together, then each into the wave's LDS scratch and out to its HBM rows; the one
             // the first layer reads last, so that its rows are still in LDS
             float v0[9], v1[9];
-            if (a.gen_mask & 1) gen_load(c, 0, base, v0);
-            if (a.gen_mask & 2) gen_load(c, 1, base, v1);
+            if (a.gen_mask & 1) gen_load<SPW>(c, 0, base, v0);
+            if (a.gen_mask & 2) gen_load<SPW>(c, 1, base, v1);
 #pragma nounroll
             for (int i = 0; i < 2; ++i) {
                 const int e = a.gen_lds == 0 ? 1 - i : i;
@@ -1419,14 +1427,14 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
                     float v[9];
 #pragma unroll
                     for (int j = 0; j < 9; ++j) v[j] = e == 0 ? v0[j] : v1[j];
-                    gen_rows_lds(c, e, base, v);
+                    gen_rows_lds<SPW>(c, e, base, v);
                     if (e == a.gen_reg) {
                         // the later layer's block from the wave's own rows (same wave: LDS in order)
 #pragma unroll
                         for (int sb = 0; sb < SB; ++sb)
                             gen_block(c, 16 * sb + (c.lane & 15), 8 * (c.lane >> 4), c.gh[sb], c.gl[sb]);
                     }
-                    gen_store(c, e, base);
+                    gen_store<SPW>(c, e, base);
                 }
             }
         }
@@ -1447,6 +1455,620 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
     if (c.dsink == 1234.5f) LF(fptr_t, out, 0)[threadIdx.x] = c.dsink;   // keeps the MFMAs live
 #endif
 }
+// =====================================================================================================
+// The forward on 32-sample waves (NERF_FUSED_W32): v_mfma_f32_32x32x16_bf16, one wave per SIMD.
+//
+// Same image, descriptors and outputs as mlp_fused_kernel<MODE_FWD> (bitwise the same outputs is
+// not the contract: the sums run in another order; the ReLU bits and rows are the forward's).  A
+// 16x16x32 MFMA holds its SIMD's vector issue for 8 of its 16 cycles, a 32x32x16 one for 8 of 32
+// (MI355X_MICROARCH.md, cycle constants), so the same epilogue, fragment reads and weight stream
+// find three times the issue slots beside the matrix pipe: the 16-sample kernel is issue-bound
+// (3.5 VALU + 1.85 SALU + 0.74 LDS instructions per MFMA, MFMA busy ~31 %, profiles/r05g).
+//
+// A wave owns 32 samples (4 waves, 128-sample tile as before) and a chunk is 32 output rows:
+//   out^T[32 C + r][s] = W[32 C + r][:] . x^T[:][s],  A = weights (lane (r, h)), B = activations.
+// Its accumulator holds, in lane (s, h) (s = lane & 31, h = lane >> 5), rows 8 q + 4 h + i of
+// sample s in register 4 q + i.  The 16-row image layout is read as is: k-step (kb, gp) of a chunk
+// (kb: 32-deep k-block, gp = 0, 1) takes, for lane (r, h), the 16 bytes of 16-row-layout lane
+// (r & 15) + 16 (2 gp + h) of the 16-row chunk 2 C + (r >> 4) — element j is W[32 C + r][32 kb +
+// 16 (j >> 2) + 8 gp + 4 h + (j & 3)] — so the B operand of lane (s, h) is registers 4 gp .. 4 gp + 3
+// and 8 + 4 gp .. 8 + 4 gp + 3 of the previous layer's chunk kb, lane-local.  HBM-fed blocks: k-step
+// (kh, gp) takes the same lanes of fragment kh, element j = column 32 kh + 16 gp + 8 h + j.
+//
+// Weights stream through LDS in half chunks (16 KB: 4 k-blocks of both 16-row chunks), one slot
+// ahead in a 2-slot ring, each wave loading its 4 KB share into registers at the start of a slot and
+// writing it into the other slot at its end (register staging: an LDS-DMA piece costs its wave
+// 60-185 issue cycles, a load + ds_write_b128 pair ~17).  LDS: 32 KB ring + 4 x 32 KB operand
+// images (the next layer's operand, written by the epilogue, read back at the end of the layer).
+// The previous chunk's epilogue (ReLU, stores, mask bits, split + image writes) runs in six parts
+// between the first slot's k-steps; biases start the accumulation (no bias add).
+namespace w32 {
+constexpr int NW = 4;                        // waves, one per SIMD
+constexpr int WGS = 64 * NW;
+constexpr int SPW = 32;                      // samples per wave
+constexpr int TILE = NW * SPW;
+constexpr int XIMG = 32 * 1024;              // per wave: [k-step t][hi | lo][64 lanes][16 B]
+constexpr int RSLOT = 16 * 1024;             // half a chunk's register-fed weights
+constexpr int NRS = 2;
+constexpr int WPW = RSLOT / 1024 / NW;       // 1 KB pieces per wave and slot
+static_assert(TILE == ::TILE, "tile size shared with the 16-sample kernel (composite scratch)");
+static_assert(SPW * (GEN_LD + 8) * 4 <= XIMG, "generator scratch");
+static_assert(COMP_OFF >= 4096 && COMP_OFF + COMP_SMAX * 20 <= XIMG, "composite scratch");
+static_assert(COMP_DEL >= 2048 + 64 * 16, "two rays of S <= 64 samples per composite region");
+static_assert(WPW == 4, "s_write waits for four pieces");
+}  // namespace w32
+
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f16v mfma32(bf16x8 a, bf16x8 b, f16v c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+struct C32 {
+    kchar_t* kargs;
+    char* smem;
+    char* ximg;           // this wave's operand image / generator and composite scratch
+    __amdgpu_buffer_rsrc_t rimg;
+    int wave, lane, M, n_layers;
+    int cur;              // ring slot of the next register-fed half chunk
+    // stream cursor over the register-fed half chunks (layer, 32-row chunk, half), repeating per tile
+    int d_src, d_kbr, d_n16, d_C, d_h2, d_layer;
+    int d_remaining;
+    // per-layer table, lane l = layer l (v_readlane: no scalar loads inside the chunk loop)
+    int t_off, t_kbr, t_n16, t_next;
+    // the lane's offset inside this wave's pieces (i & 1): k-block (wave >> 1) + 2 (i & 1), half wave & 1
+    unsigned w_voff[2];
+    // the current layer's register-fed input (B operand) per 16-deep k-step
+    bf16x8 xh[16], xl[16];
+    f4 head;              // the last layer's rows 0..3 (lanes h = 0)
+    float sig, cdist;
+    f4 phead;
+    float pcdist;
+    bf16x8 gh[2], gl[2];  // the captured per-ray block (gen_reg), k-steps gp = 0, 1
+};
+
+__device__ __forceinline__ void s_seek(C32& c, int l) {
+    c.d_layer = l;
+    c.d_src = __builtin_amdgcn_readlane(c.t_off, l);
+    c.d_kbr = __builtin_amdgcn_readlane(c.t_kbr, l);
+    c.d_n16 = __builtin_amdgcn_readlane(c.t_n16, l);
+    c.d_C = 0;
+    c.d_h2 = 0;
+}
+
+// This wave's pieces of the stream's current half chunk into registers, then the cursor advances
+// (past the end of the stream the last one is loaded again: every slot issues WPW loads).  Piece u
+// = wave + NW i: 16-row chunk 2 C + (u >> 3), k-block 4 h2 + ((u >> 1) & 3), half u & 1; it lands
+// at u KB of the slot, so that lane (r, h) of k-step (kbl, gp) reads 8 KB (r >> 4) + 2 KB kbl +
+// 1 KB hl + 512 gp + 16 ((r & 15) + 16 h).
+__device__ __forceinline__ void s_load(C32& c, bf16x8 (&w)[w32::WPW]) {
+    // pieces i = 0, 1 of 16-row chunk 2 C, i = 2, 3 of 2 C + 1 (past the layer's chunks: offsets
+    // beyond the image, loading zeros); the k-block / half part of the offset is the lane's constant
+    const int base0 = c.d_src + (2 * c.d_C * c.d_kbr + 4 * c.d_h2) * 2048;
+    const int base1 = 2 * c.d_C + 1 < c.d_n16 ? base0 + c.d_kbr * 2048 : (int)OOB;
+#ifndef NERF_FUSED_DIAG_NODMA          // diagnostic builds only: time the kernel without its weight stream
+#pragma unroll
+    for (int i = 0; i < w32::WPW; ++i)
+        asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen"
+                     : "=v"(w[i])
+                     : "v"(c.w_voff[i & 1]), "s"(c.rimg), "s"(i < 2 ? base0 : base1));
+#else
+#pragma unroll
+    for (int i = 0; i < w32::WPW; ++i) asm volatile("; %0 %1 %2" : "=v"(w[i]) : "s"(base0), "s"(base1));
+#endif
+    if (c.d_remaining > 1) {
+        --c.d_remaining;
+        if (++c.d_h2 == (c.d_kbr >> 2)) {
+            c.d_h2 = 0;
+            if (++c.d_C == ((c.d_n16 + 1) >> 1)) s_seek(c, __builtin_amdgcn_readlane(c.t_next, c.d_layer));
+        }
+    }
+}
+
+// ... into ring slot `slot` once landed (N younger vector-memory operations may be in flight)
+template <int N>
+__device__ __forceinline__ void s_write(C32& c, int slot, bf16x8 (&w)[w32::WPW]) {
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : "n"(N));
+    char* base = c.smem + slot * w32::RSLOT + c.lane * 16;
+#pragma unroll
+    for (int i = 0; i < w32::WPW; ++i) *reinterpret_cast<bf16x8*>(base + (c.wave + w32::NW * i) * 1024) = w[i];
+}
+
+struct L32 {
+    int floor_i;          // ReLU as an integer max on the fp32 bits: 0, or INT_MIN for no ReLU
+    int col_chunk;        // 32-row chunk holding the column output (-1: none)
+    int nb;               // 16-row chunks carrying mask bits: min(n16, 16)
+    int img;              // 32-row chunks written into the next layer's operand image
+    unsigned row_off;     // byte offset of the lane's sample row + 16 h (OOB past M)
+    int colok;            // ldo - 4 h: rows 32 C + 8 q + 4 h are stored while 32 C + 8 q < colok
+    unsigned sample_off;  // sample * 4 for lanes h = 0 (OOB otherwise / past M)
+    unsigned mrow_off;    // sample * 32 + 8 h (OOB past M)
+    unsigned bias_off;    // + 16 h
+    __amdgpu_buffer_rsrc_t ro, rm, rc;
+    unsigned mw[2], m0[2];  // mask words of lane groups g = 2 gs + h: accumulating / first half
+};
+
+// Epilogue part P of 32-row chunk cp (-1: none, stores dropped) on its values v (biases included):
+// 0 ReLU (+ the density for compositing), 1 stores, 2 / 3 ReLU mask bits of lane group g = 2 (P - 2)
+// + h, 4 / 5 the hi/lo split of k-step 2 cp + (P - 4) of the next layer into the operand image.
+template <int P>
+__device__ __forceinline__ void w32_epi(C32& c, L32& st, int cp, f16v& v) {
+    if constexpr (P == 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float x = v[r];
+            v[r] = __builtin_bit_cast(float, max(__builtin_bit_cast(int, x), st.floor_i));
+        }
+        if (cp >= 0 && cp == st.col_chunk) c.sig = v[0];
+    } else if constexpr (P == 1) {
+        // asm stores: counted by the slot's weight wait (s_write), so never merged or dropped (as
+        // builtins, the dropped stores of chunk -1, all at one offset, were merged into one)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const unsigned off =
+                cp >= 0 && 32 * cp + 8 * q < st.colok ? st.row_off + 128u * (unsigned)cp + 32u * q : OOB;
+            const f4 x = {v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+#ifndef NERF_FUSED_DIAG_NOSTORE   // diagnostic: no layer-output stores
+            asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen nt" ::"v"(x), "v"(off), "s"(st.ro));
+#else
+            asm volatile("; %0 %1" ::"v"(x), "v"(off));
+#endif
+        }
+        const unsigned coff = cp >= 0 && cp == st.col_chunk ? st.sample_off : OOB;
+        const float x0 = v[0];
+        asm volatile("buffer_store_dword %0, %1, %2, 0 offen" ::"v"(x0), "v"(coff), "s"(st.rc));
+    } else if constexpr (P == 2 || P == 3) {
+        // NERF_FUSED_MASK: 16-row chunk ch's rows 4 g + i at bit 4 (7 - (ch & 7)) + i of word ch >> 3
+        // of lane group g; chunk cp holds 16-row chunks 2 cp (q = gs) and 2 cp + 1 (q = gs + 2)
+        constexpr int gs = P - 2;
+        if (cp >= 0 && 2 * cp < st.nb) {
+            unsigned t = st.mw[gs];
+#pragma unroll
+            for (int r = 3; r >= 0; --r) t = shift_in_dead(t, v[4 * gs + r]);
+            if (2 * cp + 1 < st.nb) {
+#pragma unroll
+                for (int r = 3; r >= 0; --r) t = shift_in_dead(t, v[4 * (gs + 2) + r]);
+            }
+            if (2 * cp + 1 == 7 && st.nb >= 8) {
+                st.m0[gs] = t;
+                t = 0;
+            }
+            st.mw[gs] = t;
+        }
+    } else {
+        constexpr int gp = P - 4;
+        if (cp >= 0 && cp < st.img) {
+            typedef unsigned u4 __attribute__((ext_vector_type(4)));
+            unsigned h0, l0, h1, l1, h2, l2, h3, l3;
+            split2(v[4 * gp], v[4 * gp + 1], h0, l0);
+            split2(v[4 * gp + 2], v[4 * gp + 3], h1, l1);
+            split2(v[8 + 4 * gp], v[8 + 4 * gp + 1], h2, l2);
+            split2(v[8 + 4 * gp + 2], v[8 + 4 * gp + 3], h3, l3);
+            char* d = c.ximg + (2 * cp + gp) * 2048 + c.lane * 16;
+            *reinterpret_cast<u4*>(d) = u4{h0, h1, h2, h3};
+            *reinterpret_cast<u4*>(d + 1024) = u4{l0, l1, l2, l3};
+        }
+    }
+}
+
+template <int OFF>
+__device__ __forceinline__ void w32_frag(bf16x8 (&f)[2], unsigned sa) {
+    lds_frag<OFF>(f[0], sa);
+    lds_frag<OFF + 1024>(f[1], sa);
+}
+// k-step I of a slot: k-block I >> 1 of the slot, gp = I & 1
+template <int I>
+constexpr int w32_off() { return (I >> 1) * 2048 + (I & 1) * 512; }
+
+// The 8 k-steps of one slot (global k-steps T0 .. T0 + 7), fragments FA steps ahead; in the first
+// slot of a chunk the previous chunk's epilogue parts 0-5 at steps 1-6.
+template <int T0, int I>
+__device__ __forceinline__ void w32_steps(C32& c, L32& st, unsigned sa, bf16x8 (&fr)[FA][2], f16v& a, f16v& pv,
+                                          int cp) {
+    if constexpr (I < 8) {
+        constexpr int t = T0 + I;
+        bf16x8(&f)[2] = fr[I % FA];
+        constexpr int later = (I + FA - 1 < 7 ? I + FA - 1 : 7) - I;
+        lds_wait<2 * later>(f[0], f[1]);
+        a = mfma32(f[1], c.xh[t], a);
+        a = mfma32(f[0], c.xl[t], a);
+        a = mfma32(f[0], c.xh[t], a);
+        if constexpr (I + FA < 8) w32_frag<w32_off<I + FA>()>(f, sa);
+        if constexpr (T0 == 0 && I >= 1 && I <= 6) w32_epi<I - 1>(c, st, cp, pv);
+        __builtin_amdgcn_sched_barrier(0);
+        w32_steps<T0, I + 1>(c, st, sa, fr, a, pv, cp);
+    }
+}
+
+template <int I>
+__device__ __forceinline__ void w32_first_reads(bf16x8 (&fr)[FA][2], unsigned sa) {
+    if constexpr (I < FA) {
+        w32_frag<w32_off<I>()>(fr[I], sa);
+        w32_first_reads<I + 1>(fr, sa);
+    }
+}
+
+__device__ __forceinline__ void w32_bias(f4 (&b)[4], const C32& c, unsigned off) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) buf_load16(b[q], off + 32u * q, c.rimg);
+}
+template <int N>
+__device__ __forceinline__ void w32_bias_wait(f4 (&b)[4]) {
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]) : "n"(N));
+}
+__device__ __forceinline__ f16v w32_acc(const f4 (&b)[4]) {
+    const f8 lo = __builtin_shufflevector(b[0], b[1], 0, 1, 2, 3, 4, 5, 6, 7);
+    const f8 hi = __builtin_shufflevector(b[2], b[3], 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+}
+
+// One layer of shape (KBR register-fed, KBH HBM-fed 32-deep k-blocks) on 32-row chunks.
+template <int KBR, int KBH>
+__device__ __forceinline__ void w32_layer(C32& c, int l, int base) {
+    constexpr int HPC = KBR / 4;                 // ring slots per chunk
+    const int s = c.lane & 31, h = c.lane >> 5;
+    const int N = LF(int, N, l);
+    const int n16 = n16_of(N);
+    const int NC = (N + 31) >> 5;
+    L32 st;
+    const int ldo = (int)LF(int64_t, ldo, l);
+    st.floor_i = LF(int, relu, l) != 0 ? 0 : (int)0x80000000;
+    st.colok = ldo - 4 * h;
+    st.nb = n16 < 16 ? n16 : 16;
+    st.img = l + 1 < c.n_layers ? (NC < 8 ? NC : 8) : 1;
+    const int sample = base + s;
+    const bool row_ok = sample < c.M;
+    st.row_off = row_ok ? (unsigned)sample * (unsigned)ldo * 4u + 16u * h : OOB;
+    st.sample_off = row_ok && h == 0 ? (unsigned)sample * 4u : OOB;
+    st.mrow_off = row_ok ? (unsigned)sample * 32u + 8u * h : OOB;
+    st.mw[0] = st.mw[1] = st.m0[0] = st.m0[1] = 0;
+    st.ro = __builtin_amdgcn_make_buffer_rsrc(LF(fptr_t, out, l), 0, c.M * ldo * 4, RSRC_W3);
+    st.bias_off = (unsigned)LF(int64_t, bias_off, l) + 16u * h;
+    uint8_t* mptr = LF(u8ptr_t, mask, l);
+    st.rm = __builtin_amdgcn_make_buffer_rsrc(mptr, 0, mptr != nullptr ? c.M * 32 : 0, RSRC_W3);
+    float* cptr = LF(fptr_t, col_out, l);
+    st.col_chunk = cptr != nullptr ? LF(int, col_idx, l) / 32 : -1;
+    st.rc = __builtin_amdgcn_make_buffer_rsrc(cptr, 0, cptr ? c.M * 4 : 0, RSRC_W3);
+
+    // ---- HBM-fed input k-steps: lane (s, h) of k-step (kh, gp) holds columns 32 kh + 16 gp + 8 h .. +7
+    constexpr int KTH = KBH > 0 ? 2 * KBH : 1;
+    bf16x8 hh[KTH], hl[KTH];
+    if constexpr (KBH > 0) {
+        const int kb0 = LFI(int, seg_kb, 0, l);
+#pragma unroll
+        for (int kh = 0; kh < KBH; ++kh) {
+            const int sg = kh < kb0 ? 0 : 1;
+            const int khl = sg ? kh - kb0 : kh;
+            const int gen = sg ? LFI(int, seg_gen, 1, l) : LFI(int, seg_gen, 0, l);
+            if (gen != 0) {
+                if constexpr (KBR == 0) {         // the first layer: generated at the tile start, still in LDS
+#pragma unroll
+                    for (int gp = 0; gp < 2; ++gp)
+                        gen_block(c, s, 32 * khl + 16 * gp + 8 * h, hh[2 * kh + gp], hl[2 * kh + gp]);
+                } else {                          // a later layer: the block captured at the tile start
+#pragma unroll
+                    for (int gp = 0; gp < 2; ++gp) {
+                        hh[2 * kh + gp] = c.gh[gp];
+                        hl[2 * kh + gp] = c.gl[gp];
+                    }
+                }
+                continue;
+            }
+            const float* p = sg ? LFI(cfptr_t, seg_ptr, 1, l) : LFI(cfptr_t, seg_ptr, 0, l);
+            const int64_t ld = sg ? LFI(int64_t, seg_ld, 1, l) : LFI(int64_t, seg_ld, 0, l);
+            const int k = sg ? LFI(int, seg_k, 1, l) : LFI(int, seg_k, 0, l);
+            const int rd = sg ? LFI(int, seg_rd, 1, l) : LFI(int, seg_rd, 0, l);
+            const int rows = sg ? LFI(int, seg_rows, 1, l) : LFI(int, seg_rows, 0, l);
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, (int)((int64_t)rows * ld * 4), RSRC_W3);
+            const unsigned m = (unsigned)(row_ok ? sample : 0);
+            const unsigned row = rd == 1 ? m : m / (unsigned)rd;
+#pragma unroll
+            for (int gp = 0; gp < 2; ++gp) {
+                const int col = 32 * khl + 16 * gp + 8 * h;
+                const unsigned rbase = (unsigned)(((int64_t)row * ld + col) * 4);
+                const f4 x0 = __builtin_amdgcn_raw_buffer_load_b128(rs, col < k ? rbase : OOB, 0, 0);
+                const f4 x1 = __builtin_amdgcn_raw_buffer_load_b128(rs, col + 4 < k ? rbase + 16 : OOB, 0, 0);
+                split8(__builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7), hh[2 * kh + gp], hl[2 * kh + gp]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < KTH; ++i) asm volatile("" : "+v"(hh[i]), "+v"(hl[i]));
+    }
+    // HBM-fed weight fragments: lane (r, h) of k-step (kh, gp) reads 16-row-layout lane (r & 15) + 32 gp
+    // + 16 h of fragment kh of 16-row chunk 2 C + (r >> 4)
+    const int p16 = s >> 4;
+    const unsigned hbm_lane = (unsigned)LF(int, hbm_off, l) + (unsigned)(p16 * KBH * 2048) + (unsigned)(((s & 15) + 16 * h) * 16);
+    f4 bc[4], bn[4];
+    w32_bias(bc, c, st.bias_off);
+    f16v pv = {};
+    if constexpr (KBR == 0) {
+        // the first layer: no ring; its fragments (and biases) one chunk ahead by builtin loads
+        typedef bf16x8 fragk_t[KTH][2];
+        auto frag_load = [&](fragk_t& f, int C) __attribute__((always_inline)) {
+            const bool ok = 2 * C + p16 < n16;
+#pragma unroll
+            for (int kh = 0; kh < KBH; ++kh)
+#pragma unroll
+                for (int gp = 0; gp < 2; ++gp)
+#pragma unroll
+                    for (int hl_ = 0; hl_ < 2; ++hl_)
+                        f[2 * kh + gp][hl_] = __builtin_bit_cast(
+                            bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                        c.rimg,
+                                        ok ? hbm_lane + (unsigned)((2 * C * KBH + kh) * 2048 + hl_ * 1024 + gp * 512) : OOB,
+                                        0, 0));
+        };
+        w32_bias_wait<0>(bc);
+        fragk_t hA, hB;
+        frag_load(hA, 0);
+        auto step = [&](int C, fragk_t& cur, fragk_t& nxt) __attribute__((always_inline)) {
+            frag_load(nxt, C + 1 < NC ? C + 1 : C);
+            f16v a = w32_acc(bc);
+            if (C + 1 < NC) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    bc[q] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                       c.rimg, st.bias_off + 128u * (unsigned)(C + 1) + 32u * q, 0, 0));
+            }
+#pragma unroll
+            for (int t = 0; t < 2 * KBH; ++t) {
+                a = mfma32(cur[t][1], hh[t], a);
+                a = mfma32(cur[t][0], hl[t], a);
+                a = mfma32(cur[t][0], hh[t], a);
+            }
+            w32_epi<0>(c, st, C - 1, pv);
+            w32_epi<1>(c, st, C - 1, pv);
+            w32_epi<2>(c, st, C - 1, pv);
+            w32_epi<3>(c, st, C - 1, pv);
+            w32_epi<4>(c, st, C - 1, pv);
+            w32_epi<5>(c, st, C - 1, pv);
+            pv = a;
+        };
+        for (int C = 0; C < NC; C += 2) {
+            step(C, hA, hB);
+            if (C + 1 < NC) step(C + 1, hB, hA);
+        }
+    } else {
+        w32_bias_wait<0>(bc);
+        const unsigned lane_rd = (unsigned)(p16 * 8192 + ((s & 15) + 16 * h) * 16);
+        for (int C = 0; C < NC; ++C) {
+            f16v a = w32_acc(bc);
+            bf16x8 hf[KTH][2];
+            // vector-memory ops of the chunk's first slot issued after its weight loads: the next
+            // chunk's biases, the HBM-fed fragments, the previous chunk's 5 stores
+            constexpr int AFTER_W = 4 + 4 * KBH + 5;
+            auto slot = [&](auto h2_tag) __attribute__((always_inline)) {
+                constexpr int H2 = decltype(h2_tag)::value;
+#ifndef NERF_FUSED_DIAG_NOBARRIER      // diagnostic builds only (timing without the per-slot barrier)
+                barrier();
+#endif
+                const unsigned sa = lds_addr(c.smem) + (unsigned)(c.cur * w32::RSLOT) + lane_rd;
+                bf16x8 fr[FA][2];
+                w32_first_reads<0>(fr, sa);
+                bf16x8 wr[w32::WPW];
+                s_load(c, wr);
+                if constexpr (H2 == 0) {
+                    w32_bias(bn, c, st.bias_off + 128u * (unsigned)(C + 1 < NC ? C + 1 : C));
+                    const bool ok = 2 * C + p16 < n16;
+#pragma unroll
+                    for (int kh = 0; kh < KBH; ++kh)
+#pragma unroll
+                        for (int gp = 0; gp < 2; ++gp)
+#pragma unroll
+                            for (int hl_ = 0; hl_ < 2; ++hl_)
+                                buf_load16(hf[2 * kh + gp][hl_],
+                                           ok ? hbm_lane + (unsigned)((2 * C * KBH + kh) * 2048 + hl_ * 1024 + gp * 512)
+                                              : OOB,
+                                           c.rimg);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                w32_steps<8 * H2, 0>(c, st, sa, fr, a, pv, C - 1);
+                s_write<H2 == 0 ? AFTER_W : 0>(c, c.cur ^ 1, wr);
+                c.cur ^= 1;
+            };
+            slot(std::integral_constant<int, 0>{});
+            if constexpr (HPC > 1) slot(std::integral_constant<int, 1>{});
+            if constexpr (KBH > 0) {
+#pragma unroll
+                for (int t = 0; t < 2 * KBH; ++t) frag_vwait<(HPC > 1 ? 0 : 5)>(hf[t][0], hf[t][1]);
+#pragma unroll
+                for (int t = 0; t < 2 * KBH; ++t) {
+                    a = mfma32(hf[t][1], hh[t], a);
+                    a = mfma32(hf[t][0], hl[t], a);
+                    a = mfma32(hf[t][0], hh[t], a);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            w32_bias_wait<(HPC > 1 ? 0 : 5)>(bn);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) bc[q] = bn[q];
+            pv = a;
+        }
+    }
+    // the last chunk's epilogue
+    w32_epi<0>(c, st, NC - 1, pv);
+    w32_epi<1>(c, st, NC - 1, pv);
+    w32_epi<2>(c, st, NC - 1, pv);
+    w32_epi<3>(c, st, NC - 1, pv);
+    w32_epi<4>(c, st, NC - 1, pv);
+    w32_epi<5>(c, st, NC - 1, pv);
+    {
+        // the lane's mask words, each 16-row chunk's nibble at 4 (7 - (ch & 7)) whatever the count
+        if (st.nb < 8) {
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+                st.m0[g] = st.mw[g] << (4 * (8 - st.nb));
+                st.mw[g] = 0;
+            }
+        } else if (st.nb > 8) {
+#pragma unroll
+            for (int g = 0; g < 2; ++g) st.mw[g] <<= 4 * (16 - st.nb);
+        }
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+            __builtin_amdgcn_raw_buffer_store_b64(u2{st.m0[g], st.mw[g]}, st.rm, st.mrow_off == OOB ? OOB : st.mrow_off + 16u * g,
+                                                  0, 0);
+    }
+    c.head = f4{pv[0], pv[1], pv[2], pv[3]};
+    if (l + 1 == c.n_layers) return;
+    // the next layer's operand: the wave's image back into registers (same wave: LDS ops in order)
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        c.xh[t] = *reinterpret_cast<const bf16x8*>(c.ximg + t * 2048 + c.lane * 16);
+        c.xl[t] = *reinterpret_cast<const bf16x8*>(c.ximg + t * 2048 + 1024 + c.lane * 16);
+    }
+}
+
+__device__ __forceinline__ void w32_composite_tile(C32& c, int tile) {
+    const int S = CF(int32_t, samples_per_ray);
+    const bool col_sigma = CF(int32_t, sigma_layer) >= 0;
+    char* regions = c.smem + w32::NRS * w32::RSLOT;
+    if (S > w32::TILE) {
+        if ((tile & 1) == 0) {
+            c.phead = c.head;
+            if (col_sigma) c.phead[3] = c.sig;
+            c.pcdist = c.cdist;
+            return;
+        }
+        if (c.lane < 32) {
+            char* reg = regions + COMP_OFF;       // wave 0's region
+            const int j = c.wave * w32::SPW + c.lane;
+            f4 hd = c.head;
+            if (col_sigma) hd[3] = c.sig;
+            *reinterpret_cast<f4*>(reg + j * 16) = c.phead;
+            *reinterpret_cast<float*>(reg + COMP_DEL + j * 4) = c.pcdist;
+            *reinterpret_cast<f4*>(reg + (w32::TILE + j) * 16) = hd;
+            *reinterpret_cast<float*>(reg + COMP_DEL + (w32::TILE + j) * 4) = c.cdist;
+        }
+        barrier();
+        asm volatile("" ::: "memory");
+        if (c.wave == 0) composite_wave<(2 * w32::TILE) / 64>(c, (int64_t)(tile >> 1), S);
+        return;
+    }
+    // ray r of the tile in wave (r % NW)'s region, at 2 KB (r / NW) (S = 16: 8 rays on 4 waves)
+    if (c.lane < 32) {
+        const int j = c.wave * w32::SPW + c.lane;
+        if (tile * w32::TILE + j < c.M) {
+            const int r = j / S, o = j - r * S;
+            char* reg = regions + (r % w32::NW) * w32::XIMG + COMP_OFF + (r / w32::NW) * 2048;
+            f4 hd = c.head;
+            if (col_sigma) hd[3] = c.sig;
+            *reinterpret_cast<f4*>(reg + o * 16) = hd;
+            *reinterpret_cast<float*>(reg + COMP_DEL + o * 4) = c.cdist;
+        }
+    }
+    barrier();
+    asm volatile("" ::: "memory");
+    const int rpt = w32::TILE / S;
+#pragma nounroll
+    for (int k = 0; k < 2; ++k) {
+        const int r = c.wave + w32::NW * k;
+        const int64_t ray = (int64_t)tile * rpt + r;
+        if (r < rpt && ray * S < c.M) {
+            if (S > 64)
+                composite_wave<2>(c, ray, S);
+            else
+                composite_wave<1>(c, ray, S, 2048 * k);
+        }
+    }
+}
+
+__global__ __launch_bounds__(w32::WGS) __attribute__((amdgpu_waves_per_eu(1, 1))) void mlp_fused32_kernel(FusedArgs a) {
+    __shared__ __attribute__((aligned(16))) char smem[w32::NRS * w32::RSLOT + w32::NW * w32::XIMG];
+    C32 c;
+    c.kargs = (kchar_t*)__builtin_amdgcn_kernarg_segment_ptr();
+    c.smem = smem;
+    c.rimg = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(a.img), 0, a.img_bytes, RSRC_W3);
+    c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    c.ximg = smem + w32::NRS * w32::RSLOT + c.wave * w32::XIMG;
+    c.lane = threadIdx.x & 63;
+    c.M = a.M;
+    c.n_layers = a.n_layers;
+    if ((int)blockIdx.x >= a.ntiles) return;
+    const int ngroups = a.ntiles / a.span;
+    const int my_tiles = a.span * ((ngroups - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x);
+    int per_tile = 0;
+    for (int l = 0; l < a.n_layers; ++l)
+        if (dma_units(c, l) > 0) per_tile += ((LF(int, N, l) + 31) >> 5) * (dma_units(c, l) / 8);
+    c.d_remaining = my_tiles * per_tile;
+    {
+        const int l = c.lane < c.n_layers ? c.lane : 0;
+        c.t_off = (int)LF(int64_t, img_off, l);
+        c.t_kbr = dma_units(c, l) / 2;
+        c.t_n16 = n16_of(LF(int, N, l));
+        c.t_next = next_ring_layer(c, l + 1 == c.n_layers ? 0 : l + 1);
+    }
+    const int l0 = next_ring_layer(c, 0);
+    c.cur = 0;
+    c.w_voff[0] = (unsigned)((c.wave >> 1) * 2048 + (c.wave & 1) * 1024 + c.lane * 16);
+    c.w_voff[1] = c.w_voff[0] + 4096u;
+    if (l0 >= 0) {
+        s_seek(c, l0);
+        bf16x8 wr[w32::WPW];
+        s_load(c, wr);
+        s_write<0>(c, 0, wr);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        c.xh[t] = bf16x8{};
+        c.xl[t] = bf16x8{};
+    }
+#pragma unroll
+    for (int gp = 0; gp < 2; ++gp) {
+        c.gh[gp] = bf16x8{};
+        c.gl[gp] = bf16x8{};
+    }
+    c.sig = 0.f;
+    c.head = f4{0.f, 0.f, 0.f, 0.f};
+    const int span_log = a.span >> 1;
+    for (int it = 0; it < my_tiles; ++it) {
+        const int tile = (((int)blockIdx.x + (it >> span_log) * (int)gridDim.x) << span_log) + (it & span_log);
+        const int base = tile * w32::TILE + c.wave * w32::SPW;
+        if (a.comp_on) {
+            const float* dist = CF(cfptr_t, dist);
+            const int m = base + c.lane;
+            c.cdist = c.lane < 32 && m < c.M ? dist[m] : 0.f;
+        }
+        if (a.gen_mask != 0) {
+            float v0[9], v1[9];
+            if (a.gen_mask & 1) gen_load<w32::SPW>(c, 0, base, v0);
+            if (a.gen_mask & 2) gen_load<w32::SPW>(c, 1, base, v1);
+#pragma nounroll
+            for (int i = 0; i < 2; ++i) {
+                const int e = a.gen_lds == 0 ? 1 - i : i;
+                if ((a.gen_mask >> e) & 1) {
+                    float v[9];
+#pragma unroll
+                    for (int j = 0; j < 9; ++j) v[j] = e == 0 ? v0[j] : v1[j];
+                    gen_rows_lds<w32::SPW>(c, e, base, v);
+                    if (e == a.gen_reg) {
+#pragma unroll
+                        for (int gp = 0; gp < 2; ++gp)
+                            gen_block(c, c.lane & 31, 16 * gp + 8 * (c.lane >> 5), c.gh[gp], c.gl[gp]);
+                    }
+                    gen_store<w32::SPW>(c, e, base);
+                }
+            }
+        }
+        for (int l = 0; l < a.n_layers; ++l) {
+            switch (LF(int, type, l)) {
+                case 1: w32_layer<0, 1>(c, l, base); break;
+                case 2: w32_layer<0, 2>(c, l, base); break;
+                case 3: w32_layer<4, 0>(c, l, base); break;
+                case 6: w32_layer<8, 0>(c, l, base); break;
+                case 7: w32_layer<8, 1>(c, l, base); break;
+                case 8: w32_layer<8, 2>(c, l, base); break;
+                default: break;                          // rejected on the host
+            }
+        }
+        if (a.comp_on) w32_composite_tile(c, tile);
+    }
+}
+
 #undef LF
 #undef LFI
 #undef EF
@@ -1480,6 +2102,13 @@ __global__ __launch_bounds__(256) void fused_pack_kernel(PackArgs p, const int32
     } else {
         reinterpret_cast<float*>(img)[~d] = v;
     }
+}
+
+// NERF_FUSED_W32=1: the forward on 32-sample waves (mlp_fused32_kernel); read at every launch, so
+// that one process can compare the two kernels
+bool fused_w32() {
+    const char* e = getenv("NERF_FUSED_W32");
+    return e != nullptr && e[0] == '1';
 }
 
 int num_cus() {
@@ -1718,6 +2347,14 @@ int fused_launch(const nerf_fused_layer* layers, int32_t n_layers, const void* i
     }
     const int ngroups = a.ntiles / a.span;
     const int grid = ngroups < num_cus() ? ngroups : num_cus();
+    // the forward on 32-sample waves (mlp_fused32_kernel; its composite takes S >= 16: a tile's rays
+    // on two per wave at most)
+    const bool w32_ok = !dgrad && (comp == nullptr || comp->samples_per_ray * 2 * w32::NW >= w32::TILE);
+    if (w32_ok && fused_w32()) {
+        hipLaunchKernelGGL(mlp_fused32_kernel, dim3(grid), dim3(w32::WGS), 0, as_stream(stream), a);
+        NERF_CHECK_LAUNCH();
+        return NERF_OK;
+    }
     if (dgrad)
         hipLaunchKernelGGL(mlp_fused_kernel<MODE_DGRAD>, dim3(grid), dim3(WG), 0, as_stream(stream), a);
     else
