@@ -333,7 +333,7 @@ struct GenArgs {
     int64_t n_rays;
 };
 
-// Rows of encoding e for the wave's samples base .. base + SPW - 1, written into LDS (the wave's
+// Rows of encoding e for the wave's NS samples base .. base + NS - 1, written into LDS (the wave's
 // operand-image region, unused before a layer's chunk loop): row r, columns [0, 64) (zeros past
 // out_dim), as nerf_encode_fwd computes them (the same encode_common.h functions, fp contraction
 // off: bitwise equal).  The wave shares the work like encode_fwd_lds_kernel: per-sample terms
@@ -342,7 +342,7 @@ struct GenArgs {
 // outputs are dropped).
 constexpr int GEN_LD = 68;                    // floats per LDS row: 64 columns + 16-B pad
 static_assert(SPW * (GEN_LD + 8) * 4 <= XIMG_BYTES, "generator scratch");
-// The per-sample inputs of encoding e for lanes < SPW (sample base + lane): o xyz, d xyz, t0, t1,
+// The per-sample inputs of encoding e for lanes < NS (sample base + lane): o xyz, d xyz, t0, t1,
 // pixel width for ray-mode positions; x xyz for per-ray directions.  Loads only, so that the
 // tile's inputs of both encodings are in flight together (one memory round trip per tile).
 template <int NS, class CT>
@@ -375,7 +375,7 @@ __device__ __forceinline__ void gen_load(const CT& c, int e, int base, float (&v
 // Hash-grid features (params.kind 2) of the wave's samples into its LDS scratch, as
 // hashgrid_fwd_tile_kernel computes them (hashgrid_common.h: the same corner arithmetic, the 8
 // corners' feature loads issued before the sums, products rounded then added in corner order):
-// the samples' positions first (lanes < SPW), then one level per trip.
+// the samples' positions first (lanes < NS), then one level per trip.
 template <int NS, class CT>
 __device__ __forceinline__ void gen_hash_rows(const CT& c, int base, const float (&v)[9]) {
 #pragma clang fp contract(off)
@@ -398,7 +398,7 @@ __device__ __forceinline__ void gen_hash_rows(const CT& c, int base, const float
         for (int col = cols; col < 64; ++col) row[col] = 0.f;
     }
     // (same wave: its LDS operations complete in order, so the positions above are visible below)
-    // One level per trip, its resolution and row offset uniform (scalar loads), lane s < SPW on
+    // One level per trip, its resolution and row offset uniform (scalar loads), lane s < NS on
     // sample s: bitwise the stand-alone kernel and repeatable on both corner forms
     // (tests/test_hashgrid.py).  Round 4 also ran four levels per trip (16-lane groups, per-lane
     // level parameters); with the int64 corner arithmetic of that time it dropped corner 2's term
