@@ -1,0 +1,7 @@
+#!/bin/bash
+# full GPU suite at HEAD
+set -u
+O=gpurun_out/r05q; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.txt 2>&1 || { tail -40 $O/gpu_tests.txt; exit 1; }
+tail -2 $O/gpu_tests.txt
