@@ -750,9 +750,11 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
                 __builtin_amdgcn_raw_buffer_store_b128(v, st.ro2, off2, 0, ST_AUX_DG);
             } else if (!sec) {
 #if NERF_FUSED_PAIR >= 4
-                // the pair's two half lines back to back (no lane exchange)
-                const unsigned oa = 16 * (ch - 1) < st.colok ? st.row_off[sb] + 64u * (unsigned)(ch - 1) : OOB;
-                const unsigned ob = 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
+                // the pair's two half lines back to back (no lane exchange); chunk -1 (the odd slot
+                // before chunk 0) drops both (unguarded, its negative offsets wrapped to the bytes just
+                // before the row: the previous sample's columns, overwritten with the stash)
+                const unsigned oa = ch > 0 && 16 * (ch - 1) < st.colok ? st.row_off[sb] + 64u * (unsigned)(ch - 1) : OOB;
+                const unsigned ob = ch >= 0 && 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
                 __builtin_amdgcn_raw_buffer_store_b128(st.stash[sb], st.ro, oa, 0, ST_AUX_DG);
                 __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, ob, 0, ST_AUX_DG);
 #else
