@@ -839,6 +839,18 @@ __host__ __device__ constexpr int epi_placed() {                 // parts placed
     return KBR - EPI0 < EPI_NP ? (KBR - EPI0 > 0 ? KBR - EPI0 : 0) : EPI_NP;
 }
 
+// the first k-step of an 8-block chunk carrying the previous chunk's epilogue (its bias waited
+// there): forward 3, chain 4.  One box, three rotating repetitions (profiles/r05x), ms per step
+// forward / chain: 1: 3.84 / 3.44, 2: 3.83 / 3.42, 3: 3.77 / 3.41, 4: 3.89 / 3.39
+#ifndef NERF_FUSED_EPI0_FWD
+#define NERF_FUSED_EPI0_FWD 3
+#endif
+#ifndef NERF_FUSED_EPI0_DG
+#define NERF_FUSED_EPI0_DG 4
+#endif
+template <int MODE>
+constexpr int epi0_of() { return MODE == 0 ? NERF_FUSED_EPI0_FWD : NERF_FUSED_EPI0_DG; }
+
 // the chunk loop of the layers with a register-fed part unrolled by two (compile-time pair parity)
 #ifndef NERF_FUSED_UNROLL2
 #define NERF_FUSED_UNROLL2 1
@@ -875,7 +887,7 @@ __device__ __forceinline__ void first_reads(bf16x8 (&fr)[FA][2], unsigned sa) {
 template <int MODE, int KBR, int KBH, int KB_I, int EPAR = -1>
 __device__ __forceinline__ void reg_steps(Ctx& c, LayerState& st, unsigned sa, bf16x8 (&fr)[FA][2], f4 (&a)[SB],
                                           f4 (&pv)[SB], f4& pb, int ch) {
-    constexpr int EPI0 = KBR >= 8 ? 4 : (KBR >= 4 ? 1 : 0);
+    constexpr int EPI0 = KBR >= 8 ? epi0_of<MODE>() : (KBR >= 4 ? 1 : 0);
     if constexpr (KB_I < KBR) {
         bf16x8(&f)[2] = fr[KB_I % FA];
         // this step's fragments have landed (the reads of the steps after it may still be in flight)
@@ -909,7 +921,7 @@ __device__ __forceinline__ void reg_steps(Ctx& c, LayerState& st, unsigned sa, b
 // 16-row output chunks.
 template <int MODE, int KBR, int KBH>
 __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
-    constexpr int EPI0 = KBR >= 8 ? 4 : (KBR >= 4 ? 1 : 0);   // first stage carrying an epilogue part
+    constexpr int EPI0 = KBR >= 8 ? epi0_of<MODE>() : (KBR >= 4 ? 1 : 0);   // first stage carrying an epilogue part
     const int g = c.lane >> 4;
     const int N = LF(int, N, l);
     const int NC = n16_of(N);
