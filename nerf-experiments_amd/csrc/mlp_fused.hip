@@ -86,6 +86,16 @@ constexpr int ST_AUX_DG = NERF_FUSED_STORE_AUX_DG;
 // starts: the predecessor's 4 epilogue stores (absent outputs included, as dropped stores) and the
 // bias load at the start of the chunk itself
 constexpr int AFTER_DMA_VM = 1 + 2 * SB;
+// The input-gradient chain has no biases.  It used to load the (zero) bias row anyway, to keep the
+// forward's counts; that load, issued at every chunk start after the previous chunk's dY stores and
+// waited for at the epilogue, made every chunk wait for those stores (NERF_FUSED_DG_BIASLOAD=1
+// restores it for A/B).  Without it the chain's chunk-start wait leaves only its stores in flight.
+#ifndef NERF_FUSED_DG_BIASLOAD
+#define NERF_FUSED_DG_BIASLOAD 0
+#endif
+constexpr bool DG_BIASLOAD = NERF_FUSED_DG_BIASLOAD != 0;
+template <int MODE>
+constexpr int after_dma_vm() { return MODE == 0 || DG_BIASLOAD ? AFTER_DMA_VM : 2 * SB; }
 // Layer-output stores in chunk pairs: a 16-row chunk is 64 B of each sample row, half a 128-B line.
 // The even chunk's values wait in registers for the odd one's.  NERF_FUSED_PAIR: 0 none; 1 the
 // input-gradient chain only, as two stores each covering whole lines of 8 samples (lanes s and s ^ 8
@@ -909,7 +919,8 @@ __device__ __forceinline__ void reg_steps(Ctx& c, LayerState& st, unsigned sa, b
         }
         // (placing the epilogue parts of the two waves of a SIMD at different stages, 0-2 and 4-6,
         // measured slower: chain 3.78 -> 4.03-4.09 ms, forward 3.86 -> 3.94-4.00 per mip step)
-        if constexpr (KB_I == EPI0) bias_wait<(KBR > 0 ? DMA_PER_WAVE : 0) + 2 * KBH>(pb);
+        if constexpr (KB_I == EPI0 && (MODE == MODE_FWD || DG_BIASLOAD))
+            bias_wait<(KBR > 0 ? DMA_PER_WAVE : 0) + 2 * KBH>(pb);
         if constexpr (KB_I >= EPI0 && KB_I < EPI0 + epi_placed<KBR, EPI0>())
             epi_part<MODE, EPAR>(c, st, epi_part_of(KB_I - EPI0), ch - 1, pv, pb);
         __builtin_amdgcn_sched_barrier(0);
@@ -1115,11 +1126,11 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
         constexpr int EP = decltype(ep_tag)::value;
         // the previous chunk's biases (rows 4 g .. 4 g + 3), for its epilogue in this chunk, issued
         // before this chunk's DMA so that waiting for it does not wait for the DMA
-        f4 pb;
+        f4 pb = {0.f, 0.f, 0.f, 0.f};
         if constexpr (MODE == MODE_FWD)
             buf_load16(pb, st.bias_off + 64u * (unsigned)(ch > 0 ? ch - 1 : 0), c.rimg);
-        else
-            buf_load16(pb, st.bias_off, c.rimg);     // (zero biases: the load only keeps the count)
+        else if constexpr (DG_BIASLOAD)
+            buf_load16(pb, st.bias_off, c.rimg);     // (zero biases: the load only kept the count)
         const unsigned sa = lds_addr(c.smem + c.cur * SLOT_BYTES + c.lane * 16);
         bf16x8 fr[FA][2];
 #if NERF_FUSED_WREG
@@ -1138,7 +1149,7 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
             // this chunk's DMA share has landed (issued at the start of the previous register-fed
             // chunk and followed by >= AFTER_DMA_VM vector-memory ops), then everyone else's; the
             // other slot is free
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AFTER_DMA_VM) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(after_dma_vm<MODE>()) : "memory");
 #ifndef NERF_FUSED_DIAG_NOBARRIER      // diagnostic builds only (timing without the per-chunk barrier)
             barrier();
 #endif
@@ -1199,9 +1210,11 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
 #endif
     }
     {
-        f4 lb;
-        buf_load16(lb, st.bias_off + (MODE == MODE_FWD ? 64u * (unsigned)(NC - 1) : 0u), c.rimg);
-        bias_wait<0>(lb);
+        f4 lb = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (MODE == MODE_FWD || DG_BIASLOAD) {
+            buf_load16(lb, st.bias_off + (MODE == MODE_FWD ? 64u * (unsigned)(NC - 1) : 0u), c.rimg);
+            bias_wait<0>(lb);
+        }
 #pragma unroll
         for (int p = 0; p < 4; ++p) epi_part<MODE>(c, st, p, NC - 1, pv, lb);
     }
