@@ -1310,6 +1310,9 @@ __device__ __forceinline__ void composite_wave(CT& c, int64_t ray, int S, int ro
 }
 
 __device__ __forceinline__ void composite_tile(Ctx& c, int tile) {
+#ifdef NERF_FUSED_DIAG_NOCOMP          // diagnostic builds only: timing without the tile-end compositing
+    return;
+#endif
     const int S = CF(int32_t, samples_per_ray);
     const bool col_sigma = CF(int32_t, sigma_layer) >= 0;
     if (S > TILE) {
@@ -1440,7 +1443,11 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
                 c.cdist[sb] = c.lane < 16 && m < c.M ? dist[m] : 0.f;
             }
         }
+#ifndef NERF_FUSED_DIAG_NOGEN           // diagnostic builds only: timing without the tile-start encodings
         if (MODE == MODE_FWD && a.gen_mask != 0) {
+#else
+        if (false) {
+#endif
             // the tile's in-kernel encodings (one code copy for every layer type): the inputs of both
             // loaded together, then each into the wave's LDS scratch and out to its HBM rows; the one
             // the first layer reads last, so that its rows are still in LDS
