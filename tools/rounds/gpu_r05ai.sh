@@ -1,0 +1,15 @@
+#!/bin/bash
+# cache policy of the fused kernels' output stores: chain (AUX_DG 3 = sc0|nt, 18 = sc1|nt) and forward (AUX 3 / 18) vs production
+set -u
+O=gpurun_out/r05ai; mkdir -p $O
+export TMPDIR=/tmp
+L=nerf-experiments_amd
+run() {
+  t=$1_$2
+  NERF_AMD_LIB=$L/var/lib_$1.so timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-frame-roofline --steps 60 --warmup 10 \
+    > $O/bench_$t.json 2> $O/bench_$t.err || { tail -20 $O/bench_$t.err; exit 1; }
+  python3 -c "import json;d=json.load(open('$O/bench_$t.json'));k=d['kernel_functions'];print('$t', round(d['ms_per_step'],3), round(d['final_loss'],9), {n:round(v['ms_per_step'],3) for n,v in k.items() if 'fused' in n})"
+}
+for v in prod dg3 dg18 fw3 fw18; do run $v 1 || exit 1; done
+for v in fw18 dg18 prod fw3 dg3; do run $v 2 || exit 1; done
+for v in dg3 fw3 fw18 prod dg18; do run $v 3 || exit 1; done
