@@ -23,7 +23,8 @@
 #if defined(NERF_FUSED_DIAG_NOFRAG) || defined(NERF_FUSED_DIAG_MFMAONLY) || defined(NERF_FUSED_DIAG_NOMASK) || \
     defined(NERF_FUSED_DIAG_NOSPLIT) || defined(NERF_FUSED_DIAG_NOSTORE) || defined(NERF_FUSED_DIAG_NOMASKIN) || \
     defined(NERF_FUSED_DIAG_DROPSTORE) || defined(NERF_FUSED_DIAG_NODMA) || defined(NERF_FUSED_DIAG_NOEPI) || \
-    defined(NERF_FUSED_DIAG_NOBARRIER) || defined(NERF_FUSED_DIAG_NOCOMP) || defined(NERF_FUSED_DIAG_NOGEN)
+    defined(NERF_FUSED_DIAG_NOBARRIER) || defined(NERF_FUSED_DIAG_NOCOMP) || defined(NERF_FUSED_DIAG_NOGEN) || \
+    defined(NERF_FUSED_DIAG_COMP2) || defined(NERF_FUSED_DIAG_GEN2) || defined(NERF_FUSED_DIAG_BAR2)
 #define NERF_TU_DIAG_FUSED NERF_BUILD_DIAG_FUSED
 #else
 #define NERF_TU_DIAG_FUSED 0

@@ -1153,6 +1153,9 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
 #ifndef NERF_FUSED_DIAG_NOBARRIER      // diagnostic builds only (timing without the per-chunk barrier)
             barrier();
 #endif
+#ifdef NERF_FUSED_DIAG_BAR2             // diagnostic builds only: a second barrier (the cost of one at aligned waves)
+            barrier();
+#endif
             first_reads<KBR, 0>(fr, sa);
             issue_dma(c, c.cur ^ 1);                 // the next register-fed chunk, a whole chunk ahead
             __builtin_amdgcn_sched_barrier(0);      // keep the DMA ahead of this chunk's vmem ops (vmcnt)
@@ -1454,9 +1457,15 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
             float v0[9], v1[9];
             if (a.gen_mask & 1) gen_load<SPW>(c, 0, base, v0);
             if (a.gen_mask & 2) gen_load<SPW>(c, 1, base, v1);
+#ifdef NERF_FUSED_DIAG_GEN2             // diagnostic builds only: the encodings twice (same outputs)
+#pragma nounroll
+            for (int i = 0; i < 4; ++i) {
+                const int e = a.gen_lds == 0 ? 1 - (i & 1) : (i & 1);
+#else
 #pragma nounroll
             for (int i = 0; i < 2; ++i) {
                 const int e = a.gen_lds == 0 ? 1 - i : i;
+#endif
                 if ((a.gen_mask >> e) & 1) {
                     float v[9];
 #pragma unroll
@@ -1484,6 +1493,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
             }
         }
         if (MODE == MODE_FWD && a.comp_on) composite_tile(c, tile);
+#ifdef NERF_FUSED_DIAG_COMP2            // diagnostic builds only: the compositing twice (same outputs, its cost at unchanged data)
+        if (MODE == MODE_FWD && a.comp_on) composite_tile(c, tile);
+#endif
     }
 #ifdef NERF_FUSED_DIAG_MFMAONLY
     if (c.dsink == 1234.5f) LF(fptr_t, out, 0)[threadIdx.x] = c.dsink;   // keeps the MFMAs live
