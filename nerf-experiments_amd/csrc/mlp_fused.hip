@@ -861,6 +861,11 @@ __host__ __device__ constexpr int epi_placed() {                 // parts placed
 template <int MODE>
 constexpr int epi0_of() { return MODE == 0 ? NERF_FUSED_EPI0_FWD : NERF_FUSED_EPI0_DG; }
 
+// the tile-start encodings' inputs loaded one tile ahead (0: at the tile start)
+#ifndef NERF_FUSED_GEN_PREFETCH
+#define NERF_FUSED_GEN_PREFETCH 1
+#endif
+
 // the chunk loop of the layers with a register-fed part unrolled by two (compile-time pair parity)
 #ifndef NERF_FUSED_UNROLL2
 #define NERF_FUSED_UNROLL2 1
@@ -1434,8 +1439,19 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
     }
     // tile groups of `span` consecutive tiles (one group: one tile, unless rays span two)
     const int span_log = a.span >> 1;                 // span 1 or 2
+    auto tile_of = [&](int it) { return (((int)blockIdx.x + (it >> span_log) * (int)gridDim.x) << span_log) + (it & span_log); };
+#if NERF_FUSED_GEN_PREFETCH
+    // the encodings' inputs of the next tile, loaded before this tile's compositing (their memory
+    // round trip no longer opens every tile)
+    float gv0[9], gv1[9];
+    if (MODE == MODE_FWD && a.gen_mask != 0 && my_tiles > 0) {
+        const int nb = tile_of(0) * TILE + c.wave * SPW;
+        if (a.gen_mask & 1) gen_load<SPW>(c, 0, nb, gv0);
+        if (a.gen_mask & 2) gen_load<SPW>(c, 1, nb, gv1);
+    }
+#endif
     for (int it = 0; it < my_tiles; ++it) {
-        const int tile = (((int)blockIdx.x + (it >> span_log) * (int)gridDim.x) << span_log) + (it & span_log);
+        const int tile = tile_of(it);
         const int base = tile * TILE + c.wave * SPW;
         if (MODE == MODE_FWD && a.comp_on) {
             // the samples' interval lengths for the tile-end compositing (long landed by then)
@@ -1454,9 +1470,18 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
             // the tile's in-kernel encodings (one code copy for every layer type): the inputs of both
             // loaded together, then each into the wave's LDS scratch and out to its HBM rows; the one
             // the first layer reads last, so that its rows are still in LDS
+#if NERF_FUSED_GEN_PREFETCH
+            float v0[9], v1[9];
+#pragma unroll
+            for (int j = 0; j < 9; ++j) {
+                v0[j] = gv0[j];
+                v1[j] = gv1[j];
+            }
+#else
             float v0[9], v1[9];
             if (a.gen_mask & 1) gen_load<SPW>(c, 0, base, v0);
             if (a.gen_mask & 2) gen_load<SPW>(c, 1, base, v1);
+#endif
 #ifdef NERF_FUSED_DIAG_GEN2             // diagnostic builds only: the encodings twice (same outputs)
 #pragma nounroll
             for (int i = 0; i < 4; ++i) {
@@ -1492,6 +1517,13 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
                 default: break;                          // rejected on the host
             }
         }
+#if NERF_FUSED_GEN_PREFETCH
+        if (MODE == MODE_FWD && a.gen_mask != 0 && it + 1 < my_tiles) {
+            const int nb = tile_of(it + 1) * TILE + c.wave * SPW;
+            if (a.gen_mask & 1) gen_load<SPW>(c, 0, nb, gv0);
+            if (a.gen_mask & 2) gen_load<SPW>(c, 1, nb, gv1);
+        }
+#endif
         if (MODE == MODE_FWD && a.comp_on) composite_tile(c, tile);
 #ifdef NERF_FUSED_DIAG_COMP2            // diagnostic builds only: the compositing twice (same outputs, its cost at unchanged data)
         if (MODE == MODE_FWD && a.comp_on) composite_tile(c, tile);
