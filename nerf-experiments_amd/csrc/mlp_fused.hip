@@ -110,6 +110,18 @@ constexpr int after_dma_vm() { return MODE == 0 || DG_BIASLOAD ? AFTER_DMA_VM : 
 #define NERF_FUSED_PAIR 3
 #endif
 
+// the input-gradient chain's composite coefficient rows loaded one tile ahead, at the start of the
+// tile's NERF_FUSED_COMP_PF_BACK-th layer from the end (its first layer if it has fewer).  Off: four
+// rotating repetitions on one box, chain ms per step 3.388 / 3.398 / 3.393 (2 / 1 / 4 layers from
+// the end) vs 3.383 without (profiles/r05ap) — that round trip was not exposed, and the held rows
+// cost the chain 15 VGPRs
+#ifndef NERF_FUSED_COMP_PREFETCH
+#define NERF_FUSED_COMP_PREFETCH 0
+#endif
+#ifndef NERF_FUSED_COMP_PF_BACK
+#define NERF_FUSED_COMP_PF_BACK 2
+#endif
+
 struct FusedArgs {
     nerf_fused_layer L[NERF_FUSED_MAX_LAYERS];
     nerf_fused_encoding enc[2];
@@ -255,6 +267,12 @@ struct Ctx {
     // the split k-block of encoding gen_reg for the wave's own samples, captured from the LDS rows at
     // the tile start and held across the layers (a later layer's generated segment, seg_gen on l > 0)
     bf16x8 gh[SB], gl[SB];
+    // input-gradient chain: the composite coefficient rows (coef [M][8]) and grad_rgb of the wave's
+    // samples of tile base `cbase`, loaded one tile ahead from `ccoef` (NERF_FUSED_COMP_PREFETCH)
+    f4 cq0[SB], cq1[SB];
+    float cg[SB][3];
+    const float* ccoef;
+    int cbase;
 };
 
 template <class CT>
@@ -553,7 +571,30 @@ __device__ __forceinline__ void gen_block(const CT& c, int r, int col, bf16x8& h
 // gradient; include/nerf_amd.h nerf_fused_composite): per sample the coefficient row (coef [M][8])
 // times its ray's grad_rgb, stored for the weight gradients and split into the B operand of the
 // step's k-block (lanes g = 0 hold columns 0..7, the others zeros).
-__device__ __forceinline__ void comp_grad_block(const Ctx& c, int gen, const float* coef, const int (&sample)[SB],
+// The coefficient rows and grad_rgb of the wave's samples of the tile at `base`, into c.cq / c.cg
+// (zeros for lanes g > 0 and rows past M, which comp_grad_block does not read).
+__device__ __forceinline__ void comp_prefetch(Ctx& c, const float* coef, int base) {
+    const unsigned S = (unsigned)CF(int32_t, samples_per_ray);
+    const float* grgb = CF(cfptr_t, grad_rgb);
+#pragma unroll
+    for (int sb = 0; sb < SB; ++sb) {
+        const int m = base + 16 * sb + (c.lane & 15);
+        c.cq0[sb] = c.cq1[sb] = f4{0.f, 0.f, 0.f, 0.f};
+        c.cg[sb][0] = c.cg[sb][1] = c.cg[sb][2] = 0.f;
+        if ((c.lane >> 4) == 0 && m < c.M) {
+            const unsigned ray = (unsigned)m / S;
+            c.cq0[sb] = *reinterpret_cast<const f4*>(coef + (size_t)m * 8);
+            c.cq1[sb] = *reinterpret_cast<const f4*>(coef + (size_t)m * 8 + 4);
+            c.cg[sb][0] = grgb[ray * 3 + 0];
+            c.cg[sb][1] = grgb[ray * 3 + 1];
+            c.cg[sb][2] = grgb[ray * 3 + 2];
+        }
+    }
+    c.ccoef = coef;
+    c.cbase = base;
+}
+
+__device__ __forceinline__ void comp_grad_block(const Ctx& c, int gen, const float* coef, int base, const int (&sample)[SB],
                                                 const bool (&row_ok)[SB], bf16x8 (&h)[SB], bf16x8 (&lo)[SB]) {
 #pragma clang fp contract(off)
     const unsigned S = (unsigned)CF(int32_t, samples_per_ray);
@@ -561,15 +602,28 @@ __device__ __forceinline__ void comp_grad_block(const Ctx& c, int gen, const flo
     const bool dens_head = CF(int32_t, sigma_layer) < 0;
     float* out = gen == 3 ? CF(fptr_t, grad_head) : CF(fptr_t, grad_sigma);
     const int64_t ldo = gen == 3 ? CF(int64_t, ld_head) : CF(int64_t, ld_sigma);
+    const bool pre = NERF_FUSED_COMP_PREFETCH && coef == c.ccoef && base == c.cbase;   // wave-uniform
 #pragma unroll
     for (int sb = 0; sb < SB; ++sb) {
         f4 x0 = {0.f, 0.f, 0.f, 0.f};
         if ((c.lane >> 4) == 0 && row_ok[sb]) {
             const unsigned m = (unsigned)sample[sb];
             const unsigned ray = m / S;
-            const f4 q0 = *reinterpret_cast<const f4*>(coef + (size_t)m * 8);
-            const f4 q1 = *reinterpret_cast<const f4*>(coef + (size_t)m * 8 + 4);
-            const float g0 = grgb[ray * 3 + 0], g1 = grgb[ray * 3 + 1], g2 = grgb[ray * 3 + 2];
+            f4 q0, q1;
+            float g0, g1, g2;
+            if (pre) {
+                q0 = c.cq0[sb];
+                q1 = c.cq1[sb];
+                g0 = c.cg[sb][0];
+                g1 = c.cg[sb][1];
+                g2 = c.cg[sb][2];
+            } else {
+                q0 = *reinterpret_cast<const f4*>(coef + (size_t)m * 8);
+                q1 = *reinterpret_cast<const f4*>(coef + (size_t)m * 8 + 4);
+                g0 = grgb[ray * 3 + 0];
+                g1 = grgb[ray * 3 + 1];
+                g2 = grgb[ray * 3 + 2];
+            }
             const float ds = (g0 * q1[0] + g1 * q1[1]) + g2 * q1[2];
             if (gen == 3)
                 x0 = f4{g0 * q0[0], g1 * q0[1], g2 * q0[2], dens_head ? ds : 0.f};
@@ -865,6 +919,12 @@ constexpr int epi0_of() { return MODE == 0 ? NERF_FUSED_EPI0_FWD : NERF_FUSED_EP
 #ifndef NERF_FUSED_GEN_PREFETCH
 #define NERF_FUSED_GEN_PREFETCH 1
 #endif
+// where: 0 before the tile-end compositing, k > 0 at the start of the tile's k-th layer from the end
+// (its first layer if it has fewer).  Four rotating repetitions on one box (profiles/r05ao), forward
+// ms per step: 0: 3.749, 1: 3.762, 2: 3.723, 3: 3.744
+#ifndef NERF_FUSED_GEN_PF_BACK
+#define NERF_FUSED_GEN_PF_BACK 2
+#endif
 
 // the chunk loop of the layers with a register-fed part unrolled by two (compile-time pair parity)
 #ifndef NERF_FUSED_UNROLL2
@@ -1019,7 +1079,7 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
             const int khl = sg ? kh - kb0 : kh;
             const int gen = sg ? LFI(int, seg_gen, 1, l) : LFI(int, seg_gen, 0, l);
             if (MODE == MODE_DGRAD && gen >= 3) {       // the fused composite's head / density gradient
-                comp_grad_block(c, gen, sg ? LFI(cfptr_t, seg_ptr, 1, l) : LFI(cfptr_t, seg_ptr, 0, l), sample,
+                comp_grad_block(c, gen, sg ? LFI(cfptr_t, seg_ptr, 1, l) : LFI(cfptr_t, seg_ptr, 0, l), base, sample,
                                 row_ok, hh[kh], hl[kh]);
                 continue;
             }
@@ -1440,8 +1500,19 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
     // tile groups of `span` consecutive tiles (one group: one tile, unless rays span two)
     const int span_log = a.span >> 1;                 // span 1 or 2
     auto tile_of = [&](int it) { return (((int)blockIdx.x + (it >> span_log) * (int)gridDim.x) << span_log) + (it & span_log); };
+    c.ccoef = nullptr;
+    c.cbase = -1;
+    const float* pf_coef = nullptr;                   // the chain's first composite-fed segment
+    if (MODE == MODE_DGRAD && NERF_FUSED_COMP_PREFETCH) {
+        for (int l = a.n_layers - 1; l >= 0; --l)
+            for (int sg = 1; sg >= 0; --sg)
+                if (LFI(int, seg_gen, sg, l) >= 3 &&
+                    (sg == 0 ? LFI(int, seg_kb, 0, l) > 0 : LFI(int, seg_kb, 0, l) < LF(int, type, l) % 3))
+                    pf_coef = LFI(cfptr_t, seg_ptr, sg, l);
+        if (pf_coef != nullptr && my_tiles > 0) comp_prefetch(c, pf_coef, tile_of(0) * TILE + c.wave * SPW);
+    }
 #if NERF_FUSED_GEN_PREFETCH
-    // the encodings' inputs of the next tile, loaded before this tile's compositing (their memory
+    // the encodings' inputs of the next tile, loaded while this tile's last layers run (their memory
     // round trip no longer opens every tile)
     float gv0[9], gv1[9];
     if (MODE == MODE_FWD && a.gen_mask != 0 && my_tiles > 0) {
@@ -1507,6 +1578,17 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
             }
         }
         for (int l = 0; l < a.n_layers; ++l) {
+            if (MODE == MODE_DGRAD && pf_coef != nullptr && it + 1 < my_tiles &&
+                l == (a.n_layers > NERF_FUSED_COMP_PF_BACK ? a.n_layers - NERF_FUSED_COMP_PF_BACK : 0))
+                comp_prefetch(c, pf_coef, tile_of(it + 1) * TILE + c.wave * SPW);
+#if NERF_FUSED_GEN_PREFETCH && NERF_FUSED_GEN_PF_BACK > 0
+            if (MODE == MODE_FWD && a.gen_mask != 0 && it + 1 < my_tiles &&
+                l == (a.n_layers > NERF_FUSED_GEN_PF_BACK ? a.n_layers - NERF_FUSED_GEN_PF_BACK : 0)) {
+                const int nb = tile_of(it + 1) * TILE + c.wave * SPW;
+                if (a.gen_mask & 1) gen_load<SPW>(c, 0, nb, gv0);
+                if (a.gen_mask & 2) gen_load<SPW>(c, 1, nb, gv1);
+            }
+#endif
             switch (LF(int, type, l)) {
                 case 1: fused_layer<MODE, 0, 1>(c, l, base); break;
                 case 2: fused_layer<MODE, 0, 2>(c, l, base); break;
@@ -1517,7 +1599,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
                 default: break;                          // rejected on the host
             }
         }
-#if NERF_FUSED_GEN_PREFETCH
+#if NERF_FUSED_GEN_PREFETCH && NERF_FUSED_GEN_PF_BACK == 0
         if (MODE == MODE_FWD && a.gen_mask != 0 && it + 1 < my_tiles) {
             const int nb = tile_of(it + 1) * TILE + c.wave * SPW;
             if (a.gen_mask & 1) gen_load<SPW>(c, 0, nb, gv0);
