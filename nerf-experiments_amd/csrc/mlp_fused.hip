@@ -110,6 +110,12 @@ constexpr int after_dma_vm() { return MODE == 0 || DG_BIASLOAD ? AFTER_DMA_VM : 
 #define NERF_FUSED_PAIR 3
 #endif
 
+// the tile-start encodings' sincos / weight tasks dealt per sample (0: a flat task loop over the
+// wave's samples x 3 L, a division per task)
+#ifndef NERF_FUSED_GEN_TASKS
+#define NERF_FUSED_GEN_TASKS 1
+#endif
+
 // the input-gradient chain's composite coefficient rows loaded one tile ahead, at the start of the
 // tile's NERF_FUSED_COMP_PF_BACK-th layer from the end (its first layer if it has fewer).  Off: four
 // rotating repetitions on one box, chain ms per step 3.388 / 3.398 / 3.393 (2 / 1 / 4 layers from
@@ -512,9 +518,45 @@ __device__ __forceinline__ void gen_rows_lds(const CT& c, int e, int base, const
         for (int col = 0; col < id; ++col) row[col] = pm[col];
         for (int col = out_dim; col < 64; ++col) row[col] = 0.f;
     }
-    const GenArgs a{prm, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1, 1};
     // (same wave: its LDS operations complete in order, so the terms above are visible below)
     const int na = 3 * L;
+#if NERF_FUSED_GEN_TASKS
+    // lane (r, g) = (lane % NS, lane / NS) takes sample r's tasks j = g, g + 64 / NS, ...: the
+    // sample's terms read once, no division, the mask value of level k from lane k (ds_bpermute;
+    // lanes 0-15 have g = 0 and so take part in every trip)
+    {
+        constexpr int G = 64 / NS;
+        const int r = c.lane % NS, g = c.lane / NS;
+        const float* pr = P + r * 8;
+        const float pmr[3] = {pr[0], pr[1], pr[2]}, vbr[3] = {pr[3], pr[4], pr[5]};
+        const float mreg = prm.use_mask ? prm.mask[c.lane & 15] : 1.f;
+        const float scale = prm.scale;
+        const int kind = prm.kind, use_mask = prm.use_mask;
+        float* row = R + r * GEN_LD + id;
+        for (int j = g; j < na; j += G) {
+            const int dd = j >= 2 * L ? 2 : (j >= L ? 1 : 0);
+            const int k = j - dd * L;
+            const float sc = scale * (float)(1u << k);
+            float sn, cs;
+            sincos_enc(sel3(pmr, dd) * sc, &sn, &cs);
+            if (kind == 1) {
+                // mip-NeRF weight exp(-(var_d * 4^k) / 2) (positional_encodings.py:213-232)
+                const float w = expf((-(sel3(vbr, dd) * (float)(1u << (2 * k)))) / 2.0f);
+                cs = cs * w;
+                sn = sn * w;
+            }
+            if (use_mask) {
+                const float mk = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(k << 2, __builtin_bit_cast(int, mreg)));
+                cs = mk * cs;
+                sn = mk * sn;
+            }
+            row[j] = cs;
+            row[na + j] = sn;
+        }
+        return;
+    }
+#endif
+    const GenArgs a{prm, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1, 1};
     for (int i = c.lane; i < NS * na; i += 64) {
         const int r = i / na, j = i - r * na;
         const int dd = j >= 2 * L ? 2 : (j >= L ? 1 : 0);
