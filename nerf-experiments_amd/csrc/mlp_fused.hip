@@ -110,6 +110,13 @@ constexpr int after_dma_vm() { return MODE == 0 || DG_BIASLOAD ? AFTER_DMA_VM : 
 #define NERF_FUSED_PAIR 3
 #endif
 
+// the generated encoding rows stored nontemporal (read back only by later layers' HBM-fed loads
+// and the weight gradients).  Off: forward 3.841 vs 3.820 ms per step, four alternating
+// repetitions (profiles/r05au)
+#ifndef NERF_FUSED_GEN_NT
+#define NERF_FUSED_GEN_NT 0
+#endif
+
 // the tile-start encodings' sincos / weight tasks dealt per sample (0: a flat task loop over the
 // wave's samples x 3 L, a division per task)
 #ifndef NERF_FUSED_GEN_TASKS
@@ -596,7 +603,12 @@ __device__ __forceinline__ void gen_store(const CT& c, int e, int base) {
         const int m = base + r;
         if (m < c.M && (!per_ray || (unsigned)m % S == 0u)) {
             const int64_t n = per_ray ? (int64_t)((unsigned)m / S) : (int64_t)m;
+#if NERF_FUSED_GEN_NT
+            __builtin_nontemporal_store(*reinterpret_cast<const f4*>(R + r * GEN_LD + 4 * q),
+                                        reinterpret_cast<f4*>(out + n * ld + 4 * q));
+#else
             *reinterpret_cast<f4*>(out + n * ld + 4 * q) = *reinterpret_cast<const f4*>(R + r * GEN_LD + 4 * q);
+#endif
         }
     }
 }
