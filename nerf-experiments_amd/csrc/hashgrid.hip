@@ -1163,6 +1163,7 @@ extern "C" int nerf_hashgrid_bwd_pos(const nerf_hashgrid_params* params, const f
     NERF_CHECK_LAUNCH();
     if (x == nullptr) {
         const int64_t rays = n_samples / samples_per_ray;
+        NERF_REQUIRE((rays + 3) / 4 < (1ll << 31));
         hipLaunchKernelGGL(hashgrid_pos_rays_kernel, dim3((unsigned)((rays + 3) / 4)), dim3(256), 0, st, a, dpos, rays,
                            grad_o, grad_d, accumulate);
         NERF_CHECK_LAUNCH();

@@ -2,9 +2,8 @@
 // (a7, barf/model_interpolation_architecture.py:96-141; contract in include/nerf_amd.h).
 //
 // Layer-by-layer GEMMs move each 256-wide fp32 activation through HBM twice (written by
-// one launch, read by the next: 536 MB per layer at 262 144 samples).  Here a wave owns 16 * SB
-// samples (NERF_FUSED_SB, default 1: 8 waves of 16 samples, two per SIMD; SB = 2: 4 waves of 32)
-// and keeps their layer input in registers across the whole network:
+// one launch, read by the next: 536 MB per layer at 262 144 samples).  Here a wave owns 16 samples
+// (8 waves, two per SIMD) and keeps their layer input in registers across the whole network:
 //
 //   out^T[n][s] = W[n][:] . x^T[:][s]    A operand = weights (rows n), B = activations (cols s)
 //
@@ -17,7 +16,7 @@
 //
 // A chunk is 16 output rows: its MFMA steps interleave the previous chunk's epilogue (bias, ReLU,
 // fp32 stores, mask bits, hi/lo split) in four parts, whose split halves go to the wave's
-// SB x 16 KB LDS image of the next layer's operand; at the end of the layer that image is read
+// 16 KB LDS image of the next layer's operand; at the end of the layer that image is read
 // back into the operand registers (compile-time indices: no register array is ever indexed at run
 // time).  MODE_DGRAD runs the backward's input-gradient chain with the same loop: W^T images, the
 // forward's ReLU bits applied to each incoming gradient row, dY of every layer stored.
@@ -56,12 +55,9 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 
 constexpr int SLOT_BYTES = 16 * 1024;      // register-fed part of a 16-row chunk: <= 8 k-blocks x 2 KB
 constexpr int NSLOT = 2;
-#ifndef NERF_FUSED_SB
-#define NERF_FUSED_SB 1
-#endif
-constexpr int SB = NERF_FUSED_SB;          // 16-sample column blocks per wave
+constexpr int SB = 1;                      // 16-sample column blocks per wave
 constexpr int XIMG_BYTES = SB * 16 * 1024; // per wave: the next layer's operand, [kb][sb][hi|lo][lane] 16 B
-constexpr int WG = 512 / SB;               // 8 waves (two per SIMD) of 16 samples, or 4 of 32
+constexpr int WG = 512 / SB;               // 8 waves (two per SIMD) of 16 samples
 constexpr int NWAVE = WG / 64;
 constexpr int SPW = 16 * SB;               // samples per wave
 constexpr int TILE = NWAVE * SPW;          // samples per workgroup tile
@@ -73,67 +69,21 @@ constexpr int RSRC_W3 = 0x00020000;
 // every counted wait for a chunk's weight DMA also waits for the stores issued before it; with
 // the default policy those stores held the forward at 4.56 ms per mip step, nontemporal 3.49 ms
 // (the input-gradient chain 4.39 -> 3.74), results bitwise unchanged
-#ifndef NERF_FUSED_STORE_AUX
-#define NERF_FUSED_STORE_AUX 2
-#endif
-constexpr int ST_AUX = NERF_FUSED_STORE_AUX;
-// the input-gradient chain's stores (dY rows) on their own knob
-#ifndef NERF_FUSED_STORE_AUX_DG
-#define NERF_FUSED_STORE_AUX_DG NERF_FUSED_STORE_AUX
-#endif
-constexpr int ST_AUX_DG = NERF_FUSED_STORE_AUX_DG;
+constexpr int ST_AUX = 2;
 // vector-memory ops issued after a chunk's DMA (at the start of its predecessor) before the chunk
-// starts: the predecessor's 4 epilogue stores (absent outputs included, as dropped stores) and the
-// bias load at the start of the chunk itself
-constexpr int AFTER_DMA_VM = 1 + 2 * SB;
-// The input-gradient chain has no biases.  It used to load the (zero) bias row anyway, to keep the
-// forward's counts; that load, issued at every chunk start after the previous chunk's dY stores and
-// waited for at the epilogue, made every chunk wait for those stores (NERF_FUSED_DG_BIASLOAD=1
-// restores it for A/B).  Without it the chain's chunk-start wait leaves only its stores in flight.
-#ifndef NERF_FUSED_DG_BIASLOAD
-#define NERF_FUSED_DG_BIASLOAD 0
-#endif
-constexpr bool DG_BIASLOAD = NERF_FUSED_DG_BIASLOAD != 0;
+// starts: the predecessor's 2 epilogue stores (absent outputs included, as dropped stores) and, in
+// the forward, the bias load at the start of the chunk itself.  The input-gradient chain has no
+// biases and loads none: a zero-bias load there, waited for at the epilogue, made every chunk wait
+// for the previous chunk's dY stores (profiles/r05ac).
 template <int MODE>
-constexpr int after_dma_vm() { return MODE == 0 || DG_BIASLOAD ? AFTER_DMA_VM : 2 * SB; }
+constexpr int after_dma_vm() { return MODE == 0 ? 1 + 2 * SB : 2 * SB; }
 // Layer-output stores in chunk pairs: a 16-row chunk is 64 B of each sample row, half a 128-B line.
-// The even chunk's values wait in registers for the odd one's.  NERF_FUSED_PAIR: 0 none; 1 the
-// input-gradient chain only, as two stores each covering whole lines of 8 samples (lanes s and s ^ 8
-// trade halves by a DPP row rotate: chain 3.73 -> 3.55 ms per mip step); 2 that in the forward too
-// (WRITE_SIZE 1.0x, but the DPP / select work costs the forward ~0.2 ms); 3 (default) the chain as 1
-// and the forward's pair as its two half-line stores back to back, no lane exchange: forward
-// WRITE_SIZE 7.25 -> 6.47 GB per fine launch, forward +0.13 ms, chain -0.12 ms and weight gradients
-// -0.08 ms (fewer half-written lines left dirty for them): step -0.08 ms (profiles/r03m); 4 the
-// chain's pairs back to back as well (measured +0.1 ms in the chain, profiles/r03s).  Every
-// chunk still issues 2 stores per column block (counted waits assume at least that many).
-#ifndef NERF_FUSED_PAIR
-#define NERF_FUSED_PAIR 3
-#endif
-
-// the generated encoding rows stored nontemporal (read back only by later layers' HBM-fed loads
-// and the weight gradients).  Off: forward 3.841 vs 3.820 ms per step, four alternating
-// repetitions (profiles/r05au)
-#ifndef NERF_FUSED_GEN_NT
-#define NERF_FUSED_GEN_NT 0
-#endif
-
-// the tile-start encodings' sincos / weight tasks dealt per sample (0: a flat task loop over the
-// wave's samples x 3 L, a division per task)
-#ifndef NERF_FUSED_GEN_TASKS
-#define NERF_FUSED_GEN_TASKS 1
-#endif
-
-// the input-gradient chain's composite coefficient rows loaded one tile ahead, at the start of the
-// tile's NERF_FUSED_COMP_PF_BACK-th layer from the end (its first layer if it has fewer).  Off: four
-// rotating repetitions on one box, chain ms per step 3.388 / 3.398 / 3.393 (2 / 1 / 4 layers from
-// the end) vs 3.383 without (profiles/r05ap) — that round trip was not exposed, and the held rows
-// cost the chain 15 VGPRs
-#ifndef NERF_FUSED_COMP_PREFETCH
-#define NERF_FUSED_COMP_PREFETCH 0
-#endif
-#ifndef NERF_FUSED_COMP_PF_BACK
-#define NERF_FUSED_COMP_PF_BACK 2
-#endif
+// The even chunk's values wait in registers for the odd one's.  The input-gradient chain writes each
+// pair as two stores each covering whole lines of 8 samples (lanes s and s ^ 8 trade halves by a DPP
+// row rotate: chain 3.73 -> 3.55 ms per mip step); the forward writes its pair as the two half-line
+// stores back to back, no lane exchange (the exchange cost the forward ~0.2 ms; back to back:
+// WRITE_SIZE 7.25 -> 6.47 GB per fine launch, step -0.08 ms, profiles/r03m).  Every chunk still
+// issues 2 stores per column block (counted waits assume at least that many).
 
 struct FusedArgs {
     nerf_fused_layer L[NERF_FUSED_MAX_LAYERS];
@@ -280,12 +230,6 @@ struct Ctx {
     // the split k-block of encoding gen_reg for the wave's own samples, captured from the LDS rows at
     // the tile start and held across the layers (a later layer's generated segment, seg_gen on l > 0)
     bf16x8 gh[SB], gl[SB];
-    // input-gradient chain: the composite coefficient rows (coef [M][8]) and grad_rgb of the wave's
-    // samples of tile base `cbase`, loaded one tile ahead from `ccoef` (NERF_FUSED_COMP_PREFETCH)
-    f4 cq0[SB], cq1[SB];
-    float cg[SB][3];
-    const float* ccoef;
-    int cbase;
 };
 
 template <class CT>
@@ -312,14 +256,8 @@ __device__ __forceinline__ void dma_seek(Ctx& c, int l) {
 // ones repeat pieces, and past the end of the stream the last chunk is fetched again), so that the
 // count of vector-memory ops in a chunk is the same on every path
 constexpr int DMA_PER_WAVE = 2 * KBMAX / NWAVE;
-// NERF_FUSED_WREG=1: the same pieces by plain buffer loads into VGPRs at the chunk start and
-// ds_write_b128 into the ring slot at the chunk end, instead of LDS-DMA (a DMA piece costs its wave
-// 60-185 issue cycles beside MFMAs and LDS reads, MI355X_MICROARCH.md; a load + ds_write_b128 pair
-// ~17).  Measured slower on the mip step: 12.53 vs 12.22 ms, forward 3.93 / 3.97 vs 3.84 ms and
-// chain 3.73 vs 3.53 ms (two interleaved repetitions on one box, profiles/r04e), so off by default.
-#ifndef NERF_FUSED_WREG
-#define NERF_FUSED_WREG 0
-#endif
+// (The same pieces by plain buffer loads into VGPRs and ds_write_b128 into the slot measured slower:
+// step 12.53 vs 12.22 ms, profiles/r04e.)
 __device__ __forceinline__ void dma_advance(Ctx& c) {
     if (c.d_remaining > 1) {
         c.d_off += c.d_units * 1024;
@@ -327,28 +265,6 @@ __device__ __forceinline__ void dma_advance(Ctx& c) {
         --c.d_remaining;
     }
 }
-#if NERF_FUSED_WREG
-// the next register-fed chunk's pieces of this wave into registers (unit u of piece i: the DMA's)
-__device__ __forceinline__ void wload(Ctx& c, bf16x8 (&w)[DMA_PER_WAVE], unsigned (&dst)[DMA_PER_WAVE]) {
-#pragma unroll
-    for (int i = 0; i < DMA_PER_WAVE; ++i) {
-        const int u = (c.wave + NWAVE * i) & (c.d_units - 1);
-        asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(w[i])
-                     : "v"((unsigned)(c.lane * 16 + c.d_off + u * 1024)), "s"(c.rimg));
-        dst[i] = (unsigned)(u * 1024 + c.lane * 16);
-    }
-    dma_advance(c);
-}
-// ... and into ring slot `slot` once landed (N younger vector-memory ops may still be in flight)
-template <int N>
-__device__ __forceinline__ void wwrite(Ctx& c, int slot, bf16x8 (&w)[DMA_PER_WAVE], const unsigned (&dst)[DMA_PER_WAVE]) {
-    static_assert(DMA_PER_WAVE == 2, "wwrite waits for two pieces");
-    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(w[0]), "+v"(w[1]) : "n"(N));
-    char* base = c.smem + slot * SLOT_BYTES;
-#pragma unroll
-    for (int i = 0; i < DMA_PER_WAVE; ++i) *reinterpret_cast<bf16x8*>(base + dst[i]) = w[i];
-}
-#endif
 __device__ __forceinline__ void issue_dma(Ctx& c, int slot) {
     char* dst = c.smem + slot * SLOT_BYTES;
 #ifndef NERF_FUSED_DIAG_NODMA          // diagnostic builds only: time the kernel without its weight stream
@@ -527,11 +443,13 @@ __device__ __forceinline__ void gen_rows_lds(const CT& c, int e, int base, const
     }
     // (same wave: its LDS operations complete in order, so the terms above are visible below)
     const int na = 3 * L;
-#if NERF_FUSED_GEN_TASKS
     // lane (r, g) = (lane % NS, lane / NS) takes sample r's tasks j = g, g + 64 / NS, ...: the
     // sample's terms read once, no division, the mask value of level k from lane k (ds_bpermute;
     // lanes 0-15 have g = 0 and so take part in every trip)
     {
+        // the mask value of level k is read from lane k: lanes 0-15 hold levels 0-15 (encoding_ok caps
+        // levels at 16, the 64-column LDS row at 10) and must all be in group g = 0
+        static_assert(NS >= 16 && NS <= 64 && 64 % NS == 0, "mask lanes 0-15 in the g = 0 group");
         constexpr int G = 64 / NS;
         const int r = c.lane % NS, g = c.lane / NS;
         const float* pr = P + r * 8;
@@ -560,30 +478,6 @@ __device__ __forceinline__ void gen_rows_lds(const CT& c, int e, int base, const
             row[j] = cs;
             row[na + j] = sn;
         }
-        return;
-    }
-#endif
-    const GenArgs a{prm, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1, 1};
-    for (int i = c.lane; i < NS * na; i += 64) {
-        const int r = i / na, j = i - r * na;
-        const int dd = j >= 2 * L ? 2 : (j >= L ? 1 : 0);
-        const int k = j - dd * L;
-        const float sc = a.p.scale * (float)(1u << k);
-        float sn, cs;
-        sincos_enc(P[r * 8 + dd] * sc, &sn, &cs);
-        if (a.p.kind == 1) {
-            // mip-NeRF weight exp(-(var_d * 4^k) / 2) (positional_encodings.py:213-232)
-            const float w = expf((-(P[r * 8 + 3 + dd] * (float)(1u << (2 * k)))) / 2.0f);
-            cs = cs * w;
-            sn = sn * w;
-        }
-        if (a.p.use_mask) {
-            const float mk = a.p.mask[k];
-            cs = mk * cs;
-            sn = mk * sn;
-        }
-        R[r * GEN_LD + id + j] = cs;
-        R[r * GEN_LD + id + na + j] = sn;
     }
 }
 
@@ -603,12 +497,7 @@ __device__ __forceinline__ void gen_store(const CT& c, int e, int base) {
         const int m = base + r;
         if (m < c.M && (!per_ray || (unsigned)m % S == 0u)) {
             const int64_t n = per_ray ? (int64_t)((unsigned)m / S) : (int64_t)m;
-#if NERF_FUSED_GEN_NT
-            __builtin_nontemporal_store(*reinterpret_cast<const f4*>(R + r * GEN_LD + 4 * q),
-                                        reinterpret_cast<f4*>(out + n * ld + 4 * q));
-#else
             *reinterpret_cast<f4*>(out + n * ld + 4 * q) = *reinterpret_cast<const f4*>(R + r * GEN_LD + 4 * q);
-#endif
         }
     }
 }
@@ -625,30 +514,7 @@ __device__ __forceinline__ void gen_block(const CT& c, int r, int col, bf16x8& h
 // gradient; include/nerf_amd.h nerf_fused_composite): per sample the coefficient row (coef [M][8])
 // times its ray's grad_rgb, stored for the weight gradients and split into the B operand of the
 // step's k-block (lanes g = 0 hold columns 0..7, the others zeros).
-// The coefficient rows and grad_rgb of the wave's samples of the tile at `base`, into c.cq / c.cg
-// (zeros for lanes g > 0 and rows past M, which comp_grad_block does not read).
-__device__ __forceinline__ void comp_prefetch(Ctx& c, const float* coef, int base) {
-    const unsigned S = (unsigned)CF(int32_t, samples_per_ray);
-    const float* grgb = CF(cfptr_t, grad_rgb);
-#pragma unroll
-    for (int sb = 0; sb < SB; ++sb) {
-        const int m = base + 16 * sb + (c.lane & 15);
-        c.cq0[sb] = c.cq1[sb] = f4{0.f, 0.f, 0.f, 0.f};
-        c.cg[sb][0] = c.cg[sb][1] = c.cg[sb][2] = 0.f;
-        if ((c.lane >> 4) == 0 && m < c.M) {
-            const unsigned ray = (unsigned)m / S;
-            c.cq0[sb] = *reinterpret_cast<const f4*>(coef + (size_t)m * 8);
-            c.cq1[sb] = *reinterpret_cast<const f4*>(coef + (size_t)m * 8 + 4);
-            c.cg[sb][0] = grgb[ray * 3 + 0];
-            c.cg[sb][1] = grgb[ray * 3 + 1];
-            c.cg[sb][2] = grgb[ray * 3 + 2];
-        }
-    }
-    c.ccoef = coef;
-    c.cbase = base;
-}
-
-__device__ __forceinline__ void comp_grad_block(const Ctx& c, int gen, const float* coef, int base, const int (&sample)[SB],
+__device__ __forceinline__ void comp_grad_block(const Ctx& c, int gen, const float* coef, const int (&sample)[SB],
                                                 const bool (&row_ok)[SB], bf16x8 (&h)[SB], bf16x8 (&lo)[SB]) {
 #pragma clang fp contract(off)
     const unsigned S = (unsigned)CF(int32_t, samples_per_ray);
@@ -656,28 +522,15 @@ __device__ __forceinline__ void comp_grad_block(const Ctx& c, int gen, const flo
     const bool dens_head = CF(int32_t, sigma_layer) < 0;
     float* out = gen == 3 ? CF(fptr_t, grad_head) : CF(fptr_t, grad_sigma);
     const int64_t ldo = gen == 3 ? CF(int64_t, ld_head) : CF(int64_t, ld_sigma);
-    const bool pre = NERF_FUSED_COMP_PREFETCH && coef == c.ccoef && base == c.cbase;   // wave-uniform
 #pragma unroll
     for (int sb = 0; sb < SB; ++sb) {
         f4 x0 = {0.f, 0.f, 0.f, 0.f};
         if ((c.lane >> 4) == 0 && row_ok[sb]) {
             const unsigned m = (unsigned)sample[sb];
             const unsigned ray = m / S;
-            f4 q0, q1;
-            float g0, g1, g2;
-            if (pre) {
-                q0 = c.cq0[sb];
-                q1 = c.cq1[sb];
-                g0 = c.cg[sb][0];
-                g1 = c.cg[sb][1];
-                g2 = c.cg[sb][2];
-            } else {
-                q0 = *reinterpret_cast<const f4*>(coef + (size_t)m * 8);
-                q1 = *reinterpret_cast<const f4*>(coef + (size_t)m * 8 + 4);
-                g0 = grgb[ray * 3 + 0];
-                g1 = grgb[ray * 3 + 1];
-                g2 = grgb[ray * 3 + 2];
-            }
+            const f4 q0 = *reinterpret_cast<const f4*>(coef + (size_t)m * 8);
+            const f4 q1 = *reinterpret_cast<const f4*>(coef + (size_t)m * 8 + 4);
+            const float g0 = grgb[ray * 3 + 0], g1 = grgb[ray * 3 + 1], g2 = grgb[ray * 3 + 2];
             const float ds = (g0 * q1[0] + g1 * q1[1]) + g2 * q1[2];
             if (gen == 3)
                 x0 = f4{g0 * q0[0], g1 * q0[1], g2 * q0[2], dens_head ? ds : 0.f};
@@ -702,12 +555,10 @@ struct LayerState {
     unsigned mrow_off[SB];    // this lane's 8 bytes of the sample's mask row (OOB past M)
     __amdgpu_buffer_rsrc_t ro, rm, rc, ro2;
     unsigned mw[SB][2];   // this lane's ReLU mask words (NERF_FUSED_MASK layout; [1] accumulates)
-#if NERF_FUSED_PAIR
     f4 stash[SB];             // the even chunk's values, stored with the odd chunk's
     unsigned pa[SB], pb[SB];  // row offsets (+16 g) of the samples this lane writes in the pair's
     unsigned pa2[SB], pb2[SB];  // stores A (samples 0-7 of the block) and B (8-15), in out / out2
     int last_even;            // NC - 1 for an odd chunk count (stored alone), else -1
-#endif
     unsigned mi[SB][2];   // mask_in: this lane's two words of the sample's bits (NERF_FUSED_MASK layout)
     unsigned mcur[SB];    // the word of the current chunk (mi[0], mi[1] from chunk 8, zero past n1)
 };
@@ -724,7 +575,6 @@ __device__ __forceinline__ void split2(float x, float y, unsigned& hi, unsigned&
     lo = __builtin_bit_cast(unsigned, __builtin_convertvector(d, bf16x2));
 }
 
-#if NERF_FUSED_PAIR
 __device__ __forceinline__ bool pair_odd(int ch) { return ch >= 0 && (ch & 1) != 0; }
 
 __device__ __forceinline__ float ror8(float x) {      // lane (s ^ 8) of this lane's 16-lane row
@@ -755,7 +605,6 @@ __device__ __forceinline__ void pair_stores(const Ctx& c, const LayerState& st, 
     oa = inr ? pa + 64u * (unsigned)cl : OOB;
     ob = inr ? pb + 64u * (unsigned)cl : OOB;
 }
-#endif
 
 // Epilogue of 16-row chunk ch (output rows 16 ch .. 16 ch + 15; ch = -1: none, the stores are
 // dropped), in four parts placed between the next chunk's MFMA stages: 0 / 1 = the values of column
@@ -789,7 +638,6 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
             for (int r = 0; r < 4; ++r)
                 v[r] = __builtin_bit_cast(float, max(__builtin_bit_cast(int, v[r] + b[r]), st.floor_i));
             if (ch >= 0 && ch == st.col_chunk) c.sig[sb] = v[0];   // (the raw density, for fused compositing)
-#if NERF_FUSED_PAIR >= 2
             if (EPAR >= 0 ? EPAR == 0 : !pair_odd(ch)) {
                 // even chunk: held for the pair (alone if it is the layer's last); the column output
                 // (col_idx is a multiple of 32: always an even chunk)
@@ -800,31 +648,13 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
                 const unsigned coff = ch == st.col_chunk ? st.sample_off[sb] : OOB;
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), st.rc, coff, 0, 0);
             } else {
-#if NERF_FUSED_PAIR >= 3
                 // the pair's two half lines of every sample back to back (the even chunk's from the stash):
                 // no lane exchange, the halves reach L2 together
                 const unsigned oa = ch > 0 && 16 * (ch - 1) < st.colok ? st.row_off[sb] + 64u * (unsigned)(ch - 1) : OOB;
                 const unsigned ob = ch >= 0 && 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
                 __builtin_amdgcn_raw_buffer_store_b128(st.stash[sb], st.ro, oa, 0, ST_AUX);
                 __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, ob, 0, ST_AUX);
-#else
-                f4 va, vb;
-                unsigned oa, ob;
-                pair_stores(c, st, sb, ch, st.colok, st.pa[sb], st.pb[sb], v, va, vb, oa, ob);
-                __builtin_amdgcn_raw_buffer_store_b128(va, st.ro, oa, 0, ST_AUX);
-                __builtin_amdgcn_raw_buffer_store_b128(vb, st.ro, ob, 0, ST_AUX);
-#endif
             }
-#else
-            const unsigned off = ch >= 0 && 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
-#ifndef NERF_FUSED_DIAG_NOSTORE   // diagnostic: no layer-output stores
-            __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, off, 0, ST_AUX);
-            const unsigned coff = ch == st.col_chunk ? st.sample_off[sb] : OOB;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), st.rc, coff, 0, 0);
-#else
-            (void)off;
-#endif
-#endif
         } else {
             const bool sec = ch >= st.n1;          // an encoding input's rows (out2): not masked
             // column 16 ch + 4 g + r is (dead) bit 4 (7 - (ch & 7)) + r of this lane's word ch >> 3 (zero
@@ -855,7 +685,6 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
             st.colok = st.colok2 = -1 << 20;
             st.pa[sb] = st.pb[sb] = st.pa2[sb] = st.pb2[sb] = st.row_off[sb] = st.row_off2[sb] = OOB;
 #endif
-#if NERF_FUSED_PAIR
             if (EPAR >= 0 ? EPAR == 0 : !pair_odd(ch)) {
                 // even chunk: held for the pair (alone if it is the layer's last); n1 is even, so
                 // both chunks of a pair go to the same output
@@ -864,39 +693,21 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
                 const unsigned off1 = alone && !sec && 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
                 const unsigned off2 =
                     alone && sec && 16 * (ch - st.n1) < st.colok2 ? st.row_off2[sb] + 64u * (unsigned)(ch - st.n1) : OOB;
-                __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, off1, 0, ST_AUX_DG);
-                __builtin_amdgcn_raw_buffer_store_b128(v, st.ro2, off2, 0, ST_AUX_DG);
+                __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, off1, 0, ST_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(v, st.ro2, off2, 0, ST_AUX);
             } else if (!sec) {
-#if NERF_FUSED_PAIR >= 4
-                // the pair's two half lines back to back (no lane exchange); chunk -1 (the odd slot
-                // before chunk 0) drops both (unguarded, its negative offsets wrapped to the bytes just
-                // before the row: the previous sample's columns, overwritten with the stash)
-                const unsigned oa = ch > 0 && 16 * (ch - 1) < st.colok ? st.row_off[sb] + 64u * (unsigned)(ch - 1) : OOB;
-                const unsigned ob = ch >= 0 && 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
-                __builtin_amdgcn_raw_buffer_store_b128(st.stash[sb], st.ro, oa, 0, ST_AUX_DG);
-                __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, ob, 0, ST_AUX_DG);
-#else
                 f4 va, vb;
                 unsigned oa, ob;
                 pair_stores(c, st, sb, ch, st.colok, st.pa[sb], st.pb[sb], v, va, vb, oa, ob);
-                __builtin_amdgcn_raw_buffer_store_b128(va, st.ro, oa, 0, ST_AUX_DG);
-                __builtin_amdgcn_raw_buffer_store_b128(vb, st.ro, ob, 0, ST_AUX_DG);
-#endif
+                __builtin_amdgcn_raw_buffer_store_b128(va, st.ro, oa, 0, ST_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(vb, st.ro, ob, 0, ST_AUX);
             } else {
                 f4 va, vb;
                 unsigned oa, ob;
                 pair_stores(c, st, sb, ch - st.n1, st.colok2, st.pa2[sb], st.pb2[sb], v, va, vb, oa, ob);
-                __builtin_amdgcn_raw_buffer_store_b128(va, st.ro2, oa, 0, ST_AUX_DG);
-                __builtin_amdgcn_raw_buffer_store_b128(vb, st.ro2, ob, 0, ST_AUX_DG);
+                __builtin_amdgcn_raw_buffer_store_b128(va, st.ro2, oa, 0, ST_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(vb, st.ro2, ob, 0, ST_AUX);
             }
-#else
-            // one store to each output, the one not addressed dropped (a select of the two resources
-            // or offsets here becomes a runtime-indexed private array, i.e. scratch)
-            const unsigned off1 = !sec && ch >= 0 && 16 * ch < st.colok ? st.row_off[sb] + 64u * (unsigned)ch : OOB;
-            const unsigned off2 = sec && 16 * (ch - st.n1) < st.colok2 ? st.row_off2[sb] + 64u * (unsigned)(ch - st.n1) : OOB;
-            __builtin_amdgcn_raw_buffer_store_b128(v, st.ro, off1, 0, ST_AUX_DG);
-            __builtin_amdgcn_raw_buffer_store_b128(v, st.ro2, off2, 0, ST_AUX_DG);
-#endif
         }
     } else if (p == 2) {
         if constexpr (MODE == MODE_FWD) {
@@ -943,14 +754,10 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
 
 // Epilogue parts in the MFMA stream: the parts that do anything (1 only with SB = 2) go to
 // consecutive register-fed stages from EPI0 on, part 3 (the hi/lo split into the next layer's
-// operand image) included when the chunk has the stages (NERF_FUSED_P3S = 1; 0: part 3 after the
-// chunk's HBM-fed MFMAs, as parts that do not fit)
-#ifndef NERF_FUSED_P3S
-#define NERF_FUSED_P3S 1
-#endif
-constexpr int EPI_NP = NERF_FUSED_P3S ? (SB > 1 ? 4 : 3) : 3;   // parts placed in stages
-__host__ __device__ constexpr int epi_part_of(int i) {         // i-th placed part
-    return (NERF_FUSED_P3S && SB == 1) ? (i == 0 ? 0 : i + 1) : i;
+// operand image) included; parts that do not fit run after the chunk's HBM-fed MFMAs
+constexpr int EPI_NP = 3;                                      // parts placed in stages
+__host__ __device__ constexpr int epi_part_of(int i) {         // i-th placed part (part 1: SB = 2 only)
+    return i == 0 ? 0 : i + 1;
 }
 template <int KBR, int EPI0>
 __host__ __device__ constexpr int epi_placed() {                 // parts placed in the stages
@@ -960,46 +767,11 @@ __host__ __device__ constexpr int epi_placed() {                 // parts placed
 // the first k-step of an 8-block chunk carrying the previous chunk's epilogue (its bias waited
 // there): forward 3, chain 4.  One box, three rotating repetitions (profiles/r05x), ms per step
 // forward / chain: 1: 3.84 / 3.44, 2: 3.83 / 3.42, 3: 3.77 / 3.41, 4: 3.89 / 3.39
-#ifndef NERF_FUSED_EPI0_FWD
-#define NERF_FUSED_EPI0_FWD 3
-#endif
-#ifndef NERF_FUSED_EPI0_DG
-#define NERF_FUSED_EPI0_DG 4
-#endif
 template <int MODE>
-constexpr int epi0_of() { return MODE == 0 ? NERF_FUSED_EPI0_FWD : NERF_FUSED_EPI0_DG; }
-
-// the tile-start encodings' inputs loaded one tile ahead (0: at the tile start)
-#ifndef NERF_FUSED_GEN_PREFETCH
-#define NERF_FUSED_GEN_PREFETCH 1
-#endif
-// where: 0 before the tile-end compositing, k > 0 at the start of the tile's k-th layer from the end
-// (its first layer if it has fewer).  Four rotating repetitions on one box (profiles/r05ao), forward
-// ms per step: 0: 3.749, 1: 3.762, 2: 3.723, 3: 3.744
-#ifndef NERF_FUSED_GEN_PF_BACK
-#define NERF_FUSED_GEN_PF_BACK 2
-#endif
-
-// the chunk loop of the layers with a register-fed part unrolled by two (compile-time pair parity)
-#ifndef NERF_FUSED_UNROLL2
-#define NERF_FUSED_UNROLL2 1
-#endif
-
-// the first layer's weight fragments one chunk ahead by builtin loads (0: the asm loads + vmcnt(0))
-#ifndef NERF_FUSED_L0_PREFETCH
-#define NERF_FUSED_L0_PREFETCH 1
-#endif
-
-// pin the split HBM-fed operand blocks in registers across a layer's chunk loop (0: hipcc's choice)
-#ifndef NERF_FUSED_PIN_HBM
-#define NERF_FUSED_PIN_HBM 1
-#endif
+constexpr int epi0_of() { return MODE == 0 ? 3 : 4; }
 
 // k-steps of weight fragments read ahead of the step being multiplied
-#ifndef NERF_FUSED_FA
-#define NERF_FUSED_FA 2
-#endif
-constexpr int FA = NERF_FUSED_FA;
+constexpr int FA = 2;
 
 // the chunk's first min(FA, KBR) steps' fragment reads (compile-time LDS offsets)
 template <int KBR, int I>
@@ -1038,7 +810,7 @@ __device__ __forceinline__ void reg_steps(Ctx& c, LayerState& st, unsigned sa, b
         }
         // (placing the epilogue parts of the two waves of a SIMD at different stages, 0-2 and 4-6,
         // measured slower: chain 3.78 -> 4.03-4.09 ms, forward 3.86 -> 3.94-4.00 per mip step)
-        if constexpr (KB_I == EPI0 && (MODE == MODE_FWD || DG_BIASLOAD))
+        if constexpr (KB_I == EPI0 && MODE == MODE_FWD)
             bias_wait<(KBR > 0 ? DMA_PER_WAVE : 0) + 2 * KBH>(pb);
         if constexpr (KB_I >= EPI0 && KB_I < EPI0 + epi_placed<KBR, EPI0>())
             epi_part<MODE, EPAR>(c, st, epi_part_of(KB_I - EPI0), ch - 1, pv, pb);
@@ -1059,9 +831,7 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
     const int ldo = (int)LF(int64_t, ldo, l);
     st.floor_i = LF(int, relu, l) != 0 ? 0 : (int)0x80000000;
     st.colok = ldo - 4 * g;
-#if NERF_FUSED_PAIR
     st.last_even = (NC & 1) ? NC - 1 : -1;
-#endif
     int sample[SB];
     bool row_ok[SB];
 #pragma unroll
@@ -1071,14 +841,12 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
         st.row_off[sb] = row_ok[sb] ? (unsigned)sample[sb] * (unsigned)ldo * 4u + 16u * g : OOB;
         st.sample_off[sb] = row_ok[sb] && g == 0 ? (unsigned)sample[sb] * 4u : OOB;
         st.mrow_off[sb] = row_ok[sb] ? (unsigned)sample[sb] * 32u + 8u * g : OOB;
-#if NERF_FUSED_PAIR
         {
             const int sa = (c.lane & 8) == 0 ? sample[sb] : sample[sb] - 8;   // store A's sample
             const int sbb = sa + 8;                                           // store B's
             st.pa[sb] = sa < c.M ? (unsigned)sa * (unsigned)ldo * 4u + 16u * g : OOB;
             st.pb[sb] = sbb < c.M ? (unsigned)sbb * (unsigned)ldo * 4u + 16u * g : OOB;
         }
-#endif
         st.mw[sb][0] = st.mw[sb][1] = 0;
     }
     st.ro = __builtin_amdgcn_make_buffer_rsrc(LF(fptr_t, out, l), 0, c.M * ldo * 4, RSRC_W3);
@@ -1099,7 +867,6 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
 #pragma unroll
         for (int sb = 0; sb < SB; ++sb)
             st.row_off2[sb] = row_ok[sb] ? (unsigned)sample[sb] * (unsigned)ldo2 * 4u + 16u * g : OOB;
-#if NERF_FUSED_PAIR
 #pragma unroll
         for (int sb = 0; sb < SB; ++sb) {
             const int sa = (c.lane & 8) == 0 ? sample[sb] : sample[sb] - 8;
@@ -1107,7 +874,6 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
             st.pa2[sb] = sa < c.M ? (unsigned)sa * (unsigned)ldo2 * 4u + 16u * g : OOB;
             st.pb2[sb] = sbb < c.M ? (unsigned)sbb * (unsigned)ldo2 * 4u + 16u * g : OOB;
         }
-#endif
         const uint8_t* mi = LF(cu8ptr_t, mask_in, l);
         const __amdgpu_buffer_rsrc_t rmi =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(mi), 0, mi != nullptr ? c.M * 32 : 0, RSRC_W3);
@@ -1133,7 +899,7 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
             const int khl = sg ? kh - kb0 : kh;
             const int gen = sg ? LFI(int, seg_gen, 1, l) : LFI(int, seg_gen, 0, l);
             if (MODE == MODE_DGRAD && gen >= 3) {       // the fused composite's head / density gradient
-                comp_grad_block(c, gen, sg ? LFI(cfptr_t, seg_ptr, 1, l) : LFI(cfptr_t, seg_ptr, 0, l), base, sample,
+                comp_grad_block(c, gen, sg ? LFI(cfptr_t, seg_ptr, 1, l) : LFI(cfptr_t, seg_ptr, 0, l), sample,
                                 row_ok, hh[kh], hl[kh]);
                 continue;
             }
@@ -1170,7 +936,6 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
             }
         }
     }
-#if NERF_FUSED_PIN_HBM
     // the split HBM-fed operand stays in registers for the whole chunk loop: hipcc otherwise keeps
     // the fp32 rows and redoes the split in every chunk (8 conversions + 4 subtracts + 4 shifts per
     // block and chunk: 32-64 VALU per chunk of the skip / head layers)
@@ -1180,12 +945,10 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
 #pragma unroll
             for (int sb = 0; sb < SB; ++sb) asm volatile("" : "+v"(hh[kh][sb]), "+v"(hl[kh][sb]));
     }
-#endif
     const unsigned hbm_frag = (unsigned)LF(int, hbm_off, l) + (unsigned)c.lane * 16u;
 
     // the previous chunk's accumulators (its epilogue runs during the current chunk)
     f4 pv[SB] = {};
-#if NERF_FUSED_L0_PREFETCH
     if constexpr (KBR == 0) {
         // The first layer has no register-fed part and no DMA.  Its weight fragments (and biases)
         // come from L2 one chunk ahead through builtin buffer loads whose waits hipcc counts, so a
@@ -1229,7 +992,6 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
             // the previous chunk's epilogue (all parts: no register-fed stages to place them in)
 #pragma unroll
             for (int i = 0; i < EPI_NP; ++i) epi_part<MODE>(c, st, epi_part_of(i), ch - 1, pv, bprev);
-            if constexpr (!NERF_FUSED_P3S) epi_part<MODE>(c, st, 3, ch - 1, pv, bprev);
 #pragma unroll
             for (int sb = 0; sb < SB; ++sb) pv[sb] = a[sb];
         };
@@ -1238,7 +1000,6 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
             if (ch + 1 < NC) step(ch + 1, hB, hA, bB, bA);
         }
     } else
-#endif
     {
     // one chunk; EP: the compile-time parity of its predecessor (whose epilogue it runs)
     auto chunk = [&](int ch, auto ep_tag) __attribute__((always_inline)) {
@@ -1248,25 +1009,11 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
         f4 pb = {0.f, 0.f, 0.f, 0.f};
         if constexpr (MODE == MODE_FWD)
             buf_load16(pb, st.bias_off + 64u * (unsigned)(ch > 0 ? ch - 1 : 0), c.rimg);
-        else if constexpr (DG_BIASLOAD)
-            buf_load16(pb, st.bias_off, c.rimg);     // (zero biases: the load only kept the count)
         const unsigned sa = lds_addr(c.smem + c.cur * SLOT_BYTES + c.lane * 16);
         bf16x8 fr[FA][2];
-#if NERF_FUSED_WREG
-        bf16x8 wr[DMA_PER_WAVE];
-        unsigned wdst[DMA_PER_WAVE];
-#endif
         if constexpr (KBR > 0) {
-#if NERF_FUSED_WREG
-            // this chunk's pieces were written at the end of the previous register-fed chunk (LDS
-            // ops complete in order; the barrier's lgkmcnt(0) covers them); the other slot is free
-            barrier();
-            first_reads<KBR, 0>(fr, sa);
-            wload(c, wr, wdst);                      // the next register-fed chunk, a whole chunk ahead
-            __builtin_amdgcn_sched_barrier(0);      // keep the loads ahead of this chunk's vmem ops (vmcnt)
-#else
             // this chunk's DMA share has landed (issued at the start of the previous register-fed
-            // chunk and followed by >= AFTER_DMA_VM vector-memory ops), then everyone else's; the
+            // chunk and followed by >= after_dma_vm vector-memory ops), then everyone else's; the
             // other slot is free
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(after_dma_vm<MODE>()) : "memory");
 #ifndef NERF_FUSED_DIAG_NOBARRIER      // diagnostic builds only (timing without the per-chunk barrier)
@@ -1278,7 +1025,6 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
             first_reads<KBR, 0>(fr, sa);
             issue_dma(c, c.cur ^ 1);                 // the next register-fed chunk, a whole chunk ahead
             __builtin_amdgcn_sched_barrier(0);      // keep the DMA ahead of this chunk's vmem ops (vmcnt)
-#endif
         }
         // this chunk's HBM-fed weight fragments, from L2
         bf16x8 hf[KBH > 0 ? KBH : 1][2];
@@ -1309,17 +1055,10 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
         // the parts the stages did not take (all of them for the first layer)
 #pragma unroll
         for (int i = epi_placed<KBR, EPI0>(); i < EPI_NP; ++i) epi_part<MODE, EP>(c, st, epi_part_of(i), ch - 1, pv, pb);
-        if constexpr (!NERF_FUSED_P3S) epi_part<MODE, EP>(c, st, 3, ch - 1, pv, pb);
-#if NERF_FUSED_WREG
-        // the next chunk's pieces into the free slot (younger than their loads: the HBM-fed fragment
-        // loads, waited above, and the 2 SB epilogue stores of parts 0-1)
-        if constexpr (KBR > 0) wwrite<2 * SB>(c, c.cur ^ 1, wr, wdst);
-#endif
         if constexpr (KBR > 0) c.cur ^= 1;
 #pragma unroll
         for (int sb = 0; sb < SB; ++sb) pv[sb] = a[sb];
     };
-#if NERF_FUSED_UNROLL2
     // unrolled by two: chunk ch (even) runs the epilogue of the odd chunk ch - 1 (none for ch = 0:
     // its stores are dropped), chunk ch + 1 that of the even chunk ch — the pair-store parity, the
     // stash and the accumulator hand-over are compile-time, with no branch or register copy per chunk
@@ -1327,14 +1066,11 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
         chunk(ch, std::integral_constant<int, 1>{});
         if (ch + 1 < NC) chunk(ch + 1, std::integral_constant<int, 0>{});
     }
-#else
-    for (int ch = 0; ch < NC; ++ch) chunk(ch, std::integral_constant<int, -1>{});
-#endif
     }
     {
         f4 lb = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (MODE == MODE_FWD || DG_BIASLOAD) {
-            buf_load16(lb, st.bias_off + (MODE == MODE_FWD ? 64u * (unsigned)(NC - 1) : 0u), c.rimg);
+        if constexpr (MODE == MODE_FWD) {
+            buf_load16(lb, st.bias_off + 64u * (unsigned)(NC - 1), c.rimg);
             bias_wait<0>(lb);
         }
 #pragma unroll
@@ -1508,9 +1244,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
     c.n_layers = a.n_layers;
     c.dsink = 0.f;
     if ((int)blockIdx.x >= a.ntiles) return;
-#ifdef NERF_FUSED_PRIO_HALF      // tuning: static issue priority for the second-dispatched half of the waves
-    if (c.wave >= NWAVE / 2) __builtin_amdgcn_s_setprio(1);
-#endif
     const int ngroups = a.ntiles / a.span;
     const int my_tiles = a.span * ((ngroups - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x);
     int per_tile = 0;
@@ -1527,16 +1260,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
     const int l0 = next_ring_layer(c, 0);
     if (l0 >= 0) dma_seek(c, l0);
     c.cur = 0;
-#if NERF_FUSED_WREG
-    if (l0 >= 0) {
-        bf16x8 wr[DMA_PER_WAVE];
-        unsigned wdst[DMA_PER_WAVE];
-        wload(c, wr, wdst);
-        wwrite<0>(c, 0, wr, wdst);
-    }
-#else
     if (l0 >= 0) issue_dma(c, 0);
-#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the first chunk (the steady-state wait assumes predecessors)
     __syncthreads();
 #pragma unroll
@@ -1554,27 +1278,15 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
     // tile groups of `span` consecutive tiles (one group: one tile, unless rays span two)
     const int span_log = a.span >> 1;                 // span 1 or 2
     auto tile_of = [&](int it) { return (((int)blockIdx.x + (it >> span_log) * (int)gridDim.x) << span_log) + (it & span_log); };
-    c.ccoef = nullptr;
-    c.cbase = -1;
-    const float* pf_coef = nullptr;                   // the chain's first composite-fed segment
-    if (MODE == MODE_DGRAD && NERF_FUSED_COMP_PREFETCH) {
-        for (int l = a.n_layers - 1; l >= 0; --l)
-            for (int sg = 1; sg >= 0; --sg)
-                if (LFI(int, seg_gen, sg, l) >= 3 &&
-                    (sg == 0 ? LFI(int, seg_kb, 0, l) > 0 : LFI(int, seg_kb, 0, l) < LF(int, type, l) % 3))
-                    pf_coef = LFI(cfptr_t, seg_ptr, sg, l);
-        if (pf_coef != nullptr && my_tiles > 0) comp_prefetch(c, pf_coef, tile_of(0) * TILE + c.wave * SPW);
-    }
-#if NERF_FUSED_GEN_PREFETCH
-    // the encodings' inputs of the next tile, loaded while this tile's last layers run (their memory
-    // round trip no longer opens every tile)
+    // the encodings' inputs of the next tile, loaded at the start of this tile's second-to-last layer
+    // (their memory round trip no longer opens every tile; at the last / third-to-last layer or before
+    // the compositing measured slower, profiles/r05ao)
     float gv0[9], gv1[9];
     if (MODE == MODE_FWD && a.gen_mask != 0 && my_tiles > 0) {
         const int nb = tile_of(0) * TILE + c.wave * SPW;
         if (a.gen_mask & 1) gen_load<SPW>(c, 0, nb, gv0);
         if (a.gen_mask & 2) gen_load<SPW>(c, 1, nb, gv1);
     }
-#endif
     for (int it = 0; it < my_tiles; ++it) {
         const int tile = tile_of(it);
         const int base = tile * TILE + c.wave * SPW;
@@ -1595,18 +1307,12 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
             // the tile's in-kernel encodings (one code copy for every layer type): the inputs of both
             // loaded together, then each into the wave's LDS scratch and out to its HBM rows; the one
             // the first layer reads last, so that its rows are still in LDS
-#if NERF_FUSED_GEN_PREFETCH
             float v0[9], v1[9];
 #pragma unroll
             for (int j = 0; j < 9; ++j) {
                 v0[j] = gv0[j];
                 v1[j] = gv1[j];
             }
-#else
-            float v0[9], v1[9];
-            if (a.gen_mask & 1) gen_load<SPW>(c, 0, base, v0);
-            if (a.gen_mask & 2) gen_load<SPW>(c, 1, base, v1);
-#endif
 #ifdef NERF_FUSED_DIAG_GEN2             // diagnostic builds only: the encodings twice (same outputs)
 #pragma nounroll
             for (int i = 0; i < 4; ++i) {
@@ -1632,17 +1338,12 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
             }
         }
         for (int l = 0; l < a.n_layers; ++l) {
-            if (MODE == MODE_DGRAD && pf_coef != nullptr && it + 1 < my_tiles &&
-                l == (a.n_layers > NERF_FUSED_COMP_PF_BACK ? a.n_layers - NERF_FUSED_COMP_PF_BACK : 0))
-                comp_prefetch(c, pf_coef, tile_of(it + 1) * TILE + c.wave * SPW);
-#if NERF_FUSED_GEN_PREFETCH && NERF_FUSED_GEN_PF_BACK > 0
             if (MODE == MODE_FWD && a.gen_mask != 0 && it + 1 < my_tiles &&
-                l == (a.n_layers > NERF_FUSED_GEN_PF_BACK ? a.n_layers - NERF_FUSED_GEN_PF_BACK : 0)) {
+                l == (a.n_layers > 2 ? a.n_layers - 2 : 0)) {
                 const int nb = tile_of(it + 1) * TILE + c.wave * SPW;
                 if (a.gen_mask & 1) gen_load<SPW>(c, 0, nb, gv0);
                 if (a.gen_mask & 2) gen_load<SPW>(c, 1, nb, gv1);
             }
-#endif
             switch (LF(int, type, l)) {
                 case 1: fused_layer<MODE, 0, 1>(c, l, base); break;
                 case 2: fused_layer<MODE, 0, 2>(c, l, base); break;
@@ -1653,13 +1354,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
                 default: break;                          // rejected on the host
             }
         }
-#if NERF_FUSED_GEN_PREFETCH && NERF_FUSED_GEN_PF_BACK == 0
-        if (MODE == MODE_FWD && a.gen_mask != 0 && it + 1 < my_tiles) {
-            const int nb = tile_of(it + 1) * TILE + c.wave * SPW;
-            if (a.gen_mask & 1) gen_load<SPW>(c, 0, nb, gv0);
-            if (a.gen_mask & 2) gen_load<SPW>(c, 1, nb, gv1);
-        }
-#endif
         if (MODE == MODE_FWD && a.comp_on) composite_tile(c, tile);
 #ifdef NERF_FUSED_DIAG_COMP2            // diagnostic builds only: the compositing twice (same outputs, its cost at unchanged data)
         if (MODE == MODE_FWD && a.comp_on) composite_tile(c, tile);
@@ -1669,620 +1363,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
     if (c.dsink == 1234.5f) LF(fptr_t, out, 0)[threadIdx.x] = c.dsink;   // keeps the MFMAs live
 #endif
 }
-// =====================================================================================================
-// The forward on 32-sample waves (NERF_FUSED_W32): v_mfma_f32_32x32x16_bf16, one wave per SIMD.
-//
-// Same image, descriptors and outputs as mlp_fused_kernel<MODE_FWD> (bitwise the same outputs is
-// not the contract: the sums run in another order; the ReLU bits and rows are the forward's).  A
-// 16x16x32 MFMA holds its SIMD's vector issue for 8 of its 16 cycles, a 32x32x16 one for 8 of 32
-// (MI355X_MICROARCH.md, cycle constants), so the same epilogue, fragment reads and weight stream
-// find three times the issue slots beside the matrix pipe: the 16-sample kernel is issue-bound
-// (3.5 VALU + 1.85 SALU + 0.74 LDS instructions per MFMA, MFMA busy ~31 %, profiles/r05g).
-//
-// A wave owns 32 samples (4 waves, 128-sample tile as before) and a chunk is 32 output rows:
-//   out^T[32 C + r][s] = W[32 C + r][:] . x^T[:][s],  A = weights (lane (r, h)), B = activations.
-// Its accumulator holds, in lane (s, h) (s = lane & 31, h = lane >> 5), rows 8 q + 4 h + i of
-// sample s in register 4 q + i.  The 16-row image layout is read as is: k-step (kb, gp) of a chunk
-// (kb: 32-deep k-block, gp = 0, 1) takes, for lane (r, h), the 16 bytes of 16-row-layout lane
-// (r & 15) + 16 (2 gp + h) of the 16-row chunk 2 C + (r >> 4) — element j is W[32 C + r][32 kb +
-// 16 (j >> 2) + 8 gp + 4 h + (j & 3)] — so the B operand of lane (s, h) is registers 4 gp .. 4 gp + 3
-// and 8 + 4 gp .. 8 + 4 gp + 3 of the previous layer's chunk kb, lane-local.  HBM-fed blocks: k-step
-// (kh, gp) takes the same lanes of fragment kh, element j = column 32 kh + 16 gp + 8 h + j.
-//
-// Weights stream through LDS in half chunks (16 KB: 4 k-blocks of both 16-row chunks), one slot
-// ahead in a 2-slot ring, each wave loading its 4 KB share into registers at the start of a slot and
-// writing it into the other slot at its end (register staging: an LDS-DMA piece costs its wave
-// 60-185 issue cycles, a load + ds_write_b128 pair ~17).  LDS: 32 KB ring + 4 x 32 KB operand
-// images (the next layer's operand, written by the epilogue, read back at the end of the layer).
-// The previous chunk's epilogue (ReLU, stores, mask bits, split + image writes) runs in six parts
-// between the first slot's k-steps; biases start the accumulation (no bias add).
-namespace w32 {
-constexpr int NW = 4;                        // waves, one per SIMD
-constexpr int WGS = 64 * NW;
-constexpr int SPW = 32;                      // samples per wave
-constexpr int TILE = NW * SPW;
-constexpr int XIMG = 32 * 1024;              // per wave: [k-step t][hi | lo][64 lanes][16 B]
-constexpr int RSLOT = 16 * 1024;             // half a chunk's register-fed weights
-constexpr int NRS = 2;
-constexpr int WPW = RSLOT / 1024 / NW;       // 1 KB pieces per wave and slot
-static_assert(TILE == ::TILE, "tile size shared with the 16-sample kernel (composite scratch)");
-static_assert(SPW * (GEN_LD + 8) * 4 <= XIMG, "generator scratch");
-static_assert(COMP_OFF >= 4096 && COMP_OFF + COMP_SMAX * 20 <= XIMG, "composite scratch");
-static_assert(COMP_DEL >= 2048 + 64 * 16, "two rays of S <= 64 samples per composite region");
-static_assert(WPW == 4, "s_write waits for four pieces");
-}  // namespace w32
-
-typedef float f16v __attribute__((ext_vector_type(16)));
-
-__device__ __forceinline__ f16v mfma32(bf16x8 a, bf16x8 b, f16v c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-struct C32 {
-    kchar_t* kargs;
-    char* smem;
-    char* ximg;           // this wave's operand image / generator and composite scratch
-    __amdgpu_buffer_rsrc_t rimg;
-    int wave, lane, M, n_layers;
-    int cur;              // ring slot of the next register-fed half chunk
-    // stream cursor over the register-fed half chunks (layer, 32-row chunk, half), repeating per tile
-    int d_src, d_kbr, d_n16, d_C, d_h2, d_layer;
-    int d_remaining;
-    // per-layer table, lane l = layer l (v_readlane: no scalar loads inside the chunk loop)
-    int t_off, t_kbr, t_n16, t_next;
-    // the lane's offset inside this wave's pieces (i & 1): k-block (wave >> 1) + 2 (i & 1), half wave & 1
-    unsigned w_voff[2];
-    // the current layer's register-fed input (B operand) per 16-deep k-step
-    bf16x8 xh[16], xl[16];
-    f4 head;              // the last layer's rows 0..3 (lanes h = 0)
-    float sig, cdist;
-    f4 phead;
-    float pcdist;
-    bf16x8 gh[2], gl[2];  // the captured per-ray block (gen_reg), k-steps gp = 0, 1
-};
-
-__device__ __forceinline__ void s_seek(C32& c, int l) {
-    c.d_layer = l;
-    c.d_src = __builtin_amdgcn_readlane(c.t_off, l);
-    c.d_kbr = __builtin_amdgcn_readlane(c.t_kbr, l);
-    c.d_n16 = __builtin_amdgcn_readlane(c.t_n16, l);
-    c.d_C = 0;
-    c.d_h2 = 0;
-}
-
-// This wave's pieces of the stream's current half chunk into registers, then the cursor advances
-// (past the end of the stream the last one is loaded again: every slot issues WPW loads).  Piece u
-// = wave + NW i: 16-row chunk 2 C + (u >> 3), k-block 4 h2 + ((u >> 1) & 3), half u & 1; it lands
-// at u KB of the slot, so that lane (r, h) of k-step (kbl, gp) reads 8 KB (r >> 4) + 2 KB kbl +
-// 1 KB hl + 512 gp + 16 ((r & 15) + 16 h).
-__device__ __forceinline__ void s_load(C32& c, bf16x8 (&w)[w32::WPW]) {
-    // pieces i = 0, 1 of 16-row chunk 2 C, i = 2, 3 of 2 C + 1 (past the layer's chunks: offsets
-    // beyond the image, loading zeros); the k-block / half part of the offset is the lane's constant
-    const int base0 = c.d_src + (2 * c.d_C * c.d_kbr + 4 * c.d_h2) * 2048;
-    const int base1 = 2 * c.d_C + 1 < c.d_n16 ? base0 + c.d_kbr * 2048 : (int)OOB;
-#ifndef NERF_FUSED_DIAG_NODMA          // diagnostic builds only: time the kernel without its weight stream
-#pragma unroll
-    for (int i = 0; i < w32::WPW; ++i)
-        asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen"
-                     : "=v"(w[i])
-                     : "v"(c.w_voff[i & 1]), "s"(c.rimg), "s"(i < 2 ? base0 : base1));
-#else
-#pragma unroll
-    for (int i = 0; i < w32::WPW; ++i) asm volatile("; %0 %1 %2" : "=v"(w[i]) : "s"(base0), "s"(base1));
-#endif
-    if (c.d_remaining > 1) {
-        --c.d_remaining;
-        if (++c.d_h2 == (c.d_kbr >> 2)) {
-            c.d_h2 = 0;
-            if (++c.d_C == ((c.d_n16 + 1) >> 1)) s_seek(c, __builtin_amdgcn_readlane(c.t_next, c.d_layer));
-        }
-    }
-}
-
-// ... into ring slot `slot` once landed (N younger vector-memory operations may be in flight)
-template <int N>
-__device__ __forceinline__ void s_write(C32& c, int slot, bf16x8 (&w)[w32::WPW]) {
-    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : "n"(N));
-    char* base = c.smem + slot * w32::RSLOT + c.lane * 16;
-#pragma unroll
-    for (int i = 0; i < w32::WPW; ++i) *reinterpret_cast<bf16x8*>(base + (c.wave + w32::NW * i) * 1024) = w[i];
-}
-
-struct L32 {
-    int floor_i;          // ReLU as an integer max on the fp32 bits: 0, or INT_MIN for no ReLU
-    int col_chunk;        // 32-row chunk holding the column output (-1: none)
-    int nb;               // 16-row chunks carrying mask bits: min(n16, 16)
-    int img;              // 32-row chunks written into the next layer's operand image
-    unsigned row_off;     // byte offset of the lane's sample row + 16 h (OOB past M)
-    int colok;            // ldo - 4 h: rows 32 C + 8 q + 4 h are stored while 32 C + 8 q < colok
-    unsigned sample_off;  // sample * 4 for lanes h = 0 (OOB otherwise / past M)
-    unsigned mrow_off;    // sample * 32 + 8 h (OOB past M)
-    unsigned bias_off;    // + 16 h
-    __amdgpu_buffer_rsrc_t ro, rm, rc;
-    unsigned mw[2], m0[2];  // mask words of lane groups g = 2 gs + h: accumulating / first half
-};
-
-// Epilogue part P of 32-row chunk cp (-1: none, stores dropped) on its values v (biases included):
-// 0 ReLU (+ the density for compositing), 1 stores, 2 / 3 ReLU mask bits of lane group g = 2 (P - 2)
-// + h, 4 / 5 the hi/lo split of k-step 2 cp + (P - 4) of the next layer into the operand image.
-template <int P>
-__device__ __forceinline__ void w32_epi(C32& c, L32& st, int cp, f16v& v) {
-    if constexpr (P == 0) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float x = v[r];
-            v[r] = __builtin_bit_cast(float, max(__builtin_bit_cast(int, x), st.floor_i));
-        }
-        if (cp >= 0 && cp == st.col_chunk) c.sig = v[0];
-    } else if constexpr (P == 1) {
-        // asm stores: counted by the slot's weight wait (s_write), so never merged or dropped (as
-        // builtins, the dropped stores of chunk -1, all at one offset, were merged into one)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const unsigned off =
-                cp >= 0 && 32 * cp + 8 * q < st.colok ? st.row_off + 128u * (unsigned)cp + 32u * q : OOB;
-            const f4 x = {v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
-#ifndef NERF_FUSED_DIAG_NOSTORE   // diagnostic: no layer-output stores
-            asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen nt" ::"v"(x), "v"(off), "s"(st.ro));
-#else
-            asm volatile("; %0 %1" ::"v"(x), "v"(off));
-#endif
-        }
-        const unsigned coff = cp >= 0 && cp == st.col_chunk ? st.sample_off : OOB;
-        const float x0 = v[0];
-        asm volatile("buffer_store_dword %0, %1, %2, 0 offen" ::"v"(x0), "v"(coff), "s"(st.rc));
-    } else if constexpr (P == 2 || P == 3) {
-        // NERF_FUSED_MASK: 16-row chunk ch's rows 4 g + i at bit 4 (7 - (ch & 7)) + i of word ch >> 3
-        // of lane group g; chunk cp holds 16-row chunks 2 cp (q = gs) and 2 cp + 1 (q = gs + 2)
-        constexpr int gs = P - 2;
-        if (cp >= 0 && 2 * cp < st.nb) {
-            unsigned t = st.mw[gs];
-#pragma unroll
-            for (int r = 3; r >= 0; --r) t = shift_in_dead(t, v[4 * gs + r]);
-            if (2 * cp + 1 < st.nb) {
-#pragma unroll
-                for (int r = 3; r >= 0; --r) t = shift_in_dead(t, v[4 * (gs + 2) + r]);
-            }
-            if (2 * cp + 1 == 7 && st.nb >= 8) {
-                st.m0[gs] = t;
-                t = 0;
-            }
-            st.mw[gs] = t;
-        }
-    } else {
-        constexpr int gp = P - 4;
-        if (cp >= 0 && cp < st.img) {
-            typedef unsigned u4 __attribute__((ext_vector_type(4)));
-            unsigned h0, l0, h1, l1, h2, l2, h3, l3;
-            split2(v[4 * gp], v[4 * gp + 1], h0, l0);
-            split2(v[4 * gp + 2], v[4 * gp + 3], h1, l1);
-            split2(v[8 + 4 * gp], v[8 + 4 * gp + 1], h2, l2);
-            split2(v[8 + 4 * gp + 2], v[8 + 4 * gp + 3], h3, l3);
-            char* d = c.ximg + (2 * cp + gp) * 2048 + c.lane * 16;
-            *reinterpret_cast<u4*>(d) = u4{h0, h1, h2, h3};
-            *reinterpret_cast<u4*>(d + 1024) = u4{l0, l1, l2, l3};
-        }
-    }
-}
-
-template <int OFF>
-__device__ __forceinline__ void w32_frag(bf16x8 (&f)[2], unsigned sa) {
-    lds_frag<OFF>(f[0], sa);
-    lds_frag<OFF + 1024>(f[1], sa);
-}
-// k-step I of a slot: k-block I >> 1 of the slot, gp = I & 1
-template <int I>
-constexpr int w32_off() { return (I >> 1) * 2048 + (I & 1) * 512; }
-
-// The 8 k-steps of one slot (global k-steps T0 .. T0 + 7), fragments FA steps ahead; in the first
-// slot of a chunk the previous chunk's epilogue parts 0-5 at steps 1-6.
-template <int T0, int I>
-__device__ __forceinline__ void w32_steps(C32& c, L32& st, unsigned sa, bf16x8 (&fr)[FA][2], f16v& a, f16v& pv,
-                                          int cp) {
-    if constexpr (I < 8) {
-        constexpr int t = T0 + I;
-        bf16x8(&f)[2] = fr[I % FA];
-        constexpr int later = (I + FA - 1 < 7 ? I + FA - 1 : 7) - I;
-        lds_wait<2 * later>(f[0], f[1]);
-        a = mfma32(f[1], c.xh[t], a);
-        a = mfma32(f[0], c.xl[t], a);
-        a = mfma32(f[0], c.xh[t], a);
-        if constexpr (I + FA < 8) w32_frag<w32_off<I + FA>()>(f, sa);
-        if constexpr (T0 == 0 && I >= 1 && I <= 6) w32_epi<I - 1>(c, st, cp, pv);
-        __builtin_amdgcn_sched_barrier(0);
-        w32_steps<T0, I + 1>(c, st, sa, fr, a, pv, cp);
-    }
-}
-
-template <int I>
-__device__ __forceinline__ void w32_first_reads(bf16x8 (&fr)[FA][2], unsigned sa) {
-    if constexpr (I < FA) {
-        w32_frag<w32_off<I>()>(fr[I], sa);
-        w32_first_reads<I + 1>(fr, sa);
-    }
-}
-
-__device__ __forceinline__ void w32_bias(f4 (&b)[4], const C32& c, unsigned off) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) buf_load16(b[q], off + 32u * q, c.rimg);
-}
-template <int N>
-__device__ __forceinline__ void w32_bias_wait(f4 (&b)[4]) {
-    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]) : "n"(N));
-}
-__device__ __forceinline__ f16v w32_acc(const f4 (&b)[4]) {
-    const f8 lo = __builtin_shufflevector(b[0], b[1], 0, 1, 2, 3, 4, 5, 6, 7);
-    const f8 hi = __builtin_shufflevector(b[2], b[3], 0, 1, 2, 3, 4, 5, 6, 7);
-    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
-}
-
-// One layer of shape (KBR register-fed, KBH HBM-fed 32-deep k-blocks) on 32-row chunks.
-template <int KBR, int KBH>
-__device__ __forceinline__ void w32_layer(C32& c, int l, int base) {
-    constexpr int HPC = KBR / 4;                 // ring slots per chunk
-    const int s = c.lane & 31, h = c.lane >> 5;
-    const int N = LF(int, N, l);
-    const int n16 = n16_of(N);
-    const int NC = (N + 31) >> 5;
-    L32 st;
-    const int ldo = (int)LF(int64_t, ldo, l);
-    st.floor_i = LF(int, relu, l) != 0 ? 0 : (int)0x80000000;
-    st.colok = ldo - 4 * h;
-    st.nb = n16 < 16 ? n16 : 16;
-    st.img = l + 1 < c.n_layers ? (NC < 8 ? NC : 8) : 1;
-    const int sample = base + s;
-    const bool row_ok = sample < c.M;
-    st.row_off = row_ok ? (unsigned)sample * (unsigned)ldo * 4u + 16u * h : OOB;
-    st.sample_off = row_ok && h == 0 ? (unsigned)sample * 4u : OOB;
-    st.mrow_off = row_ok ? (unsigned)sample * 32u + 8u * h : OOB;
-    st.mw[0] = st.mw[1] = st.m0[0] = st.m0[1] = 0;
-    st.ro = __builtin_amdgcn_make_buffer_rsrc(LF(fptr_t, out, l), 0, c.M * ldo * 4, RSRC_W3);
-    st.bias_off = (unsigned)LF(int64_t, bias_off, l) + 16u * h;
-    uint8_t* mptr = LF(u8ptr_t, mask, l);
-    st.rm = __builtin_amdgcn_make_buffer_rsrc(mptr, 0, mptr != nullptr ? c.M * 32 : 0, RSRC_W3);
-    float* cptr = LF(fptr_t, col_out, l);
-    st.col_chunk = cptr != nullptr ? LF(int, col_idx, l) / 32 : -1;
-    st.rc = __builtin_amdgcn_make_buffer_rsrc(cptr, 0, cptr ? c.M * 4 : 0, RSRC_W3);
-
-    // ---- HBM-fed input k-steps: lane (s, h) of k-step (kh, gp) holds columns 32 kh + 16 gp + 8 h .. +7
-    constexpr int KTH = KBH > 0 ? 2 * KBH : 1;
-    bf16x8 hh[KTH], hl[KTH];
-    if constexpr (KBH > 0) {
-        const int kb0 = LFI(int, seg_kb, 0, l);
-#pragma unroll
-        for (int kh = 0; kh < KBH; ++kh) {
-            const int sg = kh < kb0 ? 0 : 1;
-            const int khl = sg ? kh - kb0 : kh;
-            const int gen = sg ? LFI(int, seg_gen, 1, l) : LFI(int, seg_gen, 0, l);
-            if (gen != 0) {
-                if constexpr (KBR == 0) {         // the first layer: generated at the tile start, still in LDS
-#pragma unroll
-                    for (int gp = 0; gp < 2; ++gp)
-                        gen_block(c, s, 32 * khl + 16 * gp + 8 * h, hh[2 * kh + gp], hl[2 * kh + gp]);
-                } else {                          // a later layer: the block captured at the tile start
-#pragma unroll
-                    for (int gp = 0; gp < 2; ++gp) {
-                        hh[2 * kh + gp] = c.gh[gp];
-                        hl[2 * kh + gp] = c.gl[gp];
-                    }
-                }
-                continue;
-            }
-            const float* p = sg ? LFI(cfptr_t, seg_ptr, 1, l) : LFI(cfptr_t, seg_ptr, 0, l);
-            const int64_t ld = sg ? LFI(int64_t, seg_ld, 1, l) : LFI(int64_t, seg_ld, 0, l);
-            const int k = sg ? LFI(int, seg_k, 1, l) : LFI(int, seg_k, 0, l);
-            const int rd = sg ? LFI(int, seg_rd, 1, l) : LFI(int, seg_rd, 0, l);
-            const int rows = sg ? LFI(int, seg_rows, 1, l) : LFI(int, seg_rows, 0, l);
-            const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, (int)((int64_t)rows * ld * 4), RSRC_W3);
-            const unsigned m = (unsigned)(row_ok ? sample : 0);
-            const unsigned row = rd == 1 ? m : m / (unsigned)rd;
-#pragma unroll
-            for (int gp = 0; gp < 2; ++gp) {
-                const int col = 32 * khl + 16 * gp + 8 * h;
-                const unsigned rbase = (unsigned)(((int64_t)row * ld + col) * 4);
-                const f4 x0 = __builtin_amdgcn_raw_buffer_load_b128(rs, col < k ? rbase : OOB, 0, 0);
-                const f4 x1 = __builtin_amdgcn_raw_buffer_load_b128(rs, col + 4 < k ? rbase + 16 : OOB, 0, 0);
-                split8(__builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7), hh[2 * kh + gp], hl[2 * kh + gp]);
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < KTH; ++i) asm volatile("" : "+v"(hh[i]), "+v"(hl[i]));
-    }
-    // HBM-fed weight fragments: lane (r, h) of k-step (kh, gp) reads 16-row-layout lane (r & 15) + 32 gp
-    // + 16 h of fragment kh of 16-row chunk 2 C + (r >> 4)
-    const int p16 = s >> 4;
-    const unsigned hbm_lane = (unsigned)LF(int, hbm_off, l) + (unsigned)(p16 * KBH * 2048) + (unsigned)(((s & 15) + 16 * h) * 16);
-    f4 bc[4], bn[4];
-    w32_bias(bc, c, st.bias_off);
-    f16v pv = {};
-    if constexpr (KBR == 0) {
-        // the first layer: no ring; its fragments (and biases) one chunk ahead by builtin loads
-        typedef bf16x8 fragk_t[KTH][2];
-        auto frag_load = [&](fragk_t& f, int C) __attribute__((always_inline)) {
-            const bool ok = 2 * C + p16 < n16;
-#pragma unroll
-            for (int kh = 0; kh < KBH; ++kh)
-#pragma unroll
-                for (int gp = 0; gp < 2; ++gp)
-#pragma unroll
-                    for (int hl_ = 0; hl_ < 2; ++hl_)
-                        f[2 * kh + gp][hl_] = __builtin_bit_cast(
-                            bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                        c.rimg,
-                                        ok ? hbm_lane + (unsigned)((2 * C * KBH + kh) * 2048 + hl_ * 1024 + gp * 512) : OOB,
-                                        0, 0));
-        };
-        w32_bias_wait<0>(bc);
-        fragk_t hA, hB;
-        frag_load(hA, 0);
-        auto step = [&](int C, fragk_t& cur, fragk_t& nxt) __attribute__((always_inline)) {
-            frag_load(nxt, C + 1 < NC ? C + 1 : C);
-            f16v a = w32_acc(bc);
-            if (C + 1 < NC) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    bc[q] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                       c.rimg, st.bias_off + 128u * (unsigned)(C + 1) + 32u * q, 0, 0));
-            }
-#pragma unroll
-            for (int t = 0; t < 2 * KBH; ++t) {
-                a = mfma32(cur[t][1], hh[t], a);
-                a = mfma32(cur[t][0], hl[t], a);
-                a = mfma32(cur[t][0], hh[t], a);
-            }
-            w32_epi<0>(c, st, C - 1, pv);
-            w32_epi<1>(c, st, C - 1, pv);
-            w32_epi<2>(c, st, C - 1, pv);
-            w32_epi<3>(c, st, C - 1, pv);
-            w32_epi<4>(c, st, C - 1, pv);
-            w32_epi<5>(c, st, C - 1, pv);
-            pv = a;
-        };
-        for (int C = 0; C < NC; C += 2) {
-            step(C, hA, hB);
-            if (C + 1 < NC) step(C + 1, hB, hA);
-        }
-    } else {
-        w32_bias_wait<0>(bc);
-        const unsigned lane_rd = (unsigned)(p16 * 8192 + ((s & 15) + 16 * h) * 16);
-        for (int C = 0; C < NC; ++C) {
-            f16v a = w32_acc(bc);
-            bf16x8 hf[KTH][2];
-            // vector-memory ops of the chunk's first slot issued after its weight loads: the next
-            // chunk's biases, the HBM-fed fragments, the previous chunk's 5 stores
-            constexpr int AFTER_W = 4 + 4 * KBH + 5;
-            auto slot = [&](auto h2_tag) __attribute__((always_inline)) {
-                constexpr int H2 = decltype(h2_tag)::value;
-#ifndef NERF_FUSED_DIAG_NOBARRIER      // diagnostic builds only (timing without the per-slot barrier)
-                barrier();
-#endif
-                const unsigned sa = lds_addr(c.smem) + (unsigned)(c.cur * w32::RSLOT) + lane_rd;
-                bf16x8 fr[FA][2];
-                w32_first_reads<0>(fr, sa);
-                bf16x8 wr[w32::WPW];
-                s_load(c, wr);
-                if constexpr (H2 == 0) {
-                    w32_bias(bn, c, st.bias_off + 128u * (unsigned)(C + 1 < NC ? C + 1 : C));
-                    const bool ok = 2 * C + p16 < n16;
-#pragma unroll
-                    for (int kh = 0; kh < KBH; ++kh)
-#pragma unroll
-                        for (int gp = 0; gp < 2; ++gp)
-#pragma unroll
-                            for (int hl_ = 0; hl_ < 2; ++hl_)
-                                buf_load16(hf[2 * kh + gp][hl_],
-                                           ok ? hbm_lane + (unsigned)((2 * C * KBH + kh) * 2048 + hl_ * 1024 + gp * 512)
-                                              : OOB,
-                                           c.rimg);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                w32_steps<8 * H2, 0>(c, st, sa, fr, a, pv, C - 1);
-                s_write<H2 == 0 ? AFTER_W : 0>(c, c.cur ^ 1, wr);
-                c.cur ^= 1;
-            };
-            slot(std::integral_constant<int, 0>{});
-            if constexpr (HPC > 1) slot(std::integral_constant<int, 1>{});
-            if constexpr (KBH > 0) {
-#pragma unroll
-                for (int t = 0; t < 2 * KBH; ++t) frag_vwait<(HPC > 1 ? 0 : 5)>(hf[t][0], hf[t][1]);
-#pragma unroll
-                for (int t = 0; t < 2 * KBH; ++t) {
-                    a = mfma32(hf[t][1], hh[t], a);
-                    a = mfma32(hf[t][0], hl[t], a);
-                    a = mfma32(hf[t][0], hh[t], a);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            w32_bias_wait<(HPC > 1 ? 0 : 5)>(bn);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) bc[q] = bn[q];
-            pv = a;
-        }
-    }
-    // the last chunk's epilogue
-    w32_epi<0>(c, st, NC - 1, pv);
-    w32_epi<1>(c, st, NC - 1, pv);
-    w32_epi<2>(c, st, NC - 1, pv);
-    w32_epi<3>(c, st, NC - 1, pv);
-    w32_epi<4>(c, st, NC - 1, pv);
-    w32_epi<5>(c, st, NC - 1, pv);
-    {
-        // the lane's mask words, each 16-row chunk's nibble at 4 (7 - (ch & 7)) whatever the count
-        if (st.nb < 8) {
-#pragma unroll
-            for (int g = 0; g < 2; ++g) {
-                st.m0[g] = st.mw[g] << (4 * (8 - st.nb));
-                st.mw[g] = 0;
-            }
-        } else if (st.nb > 8) {
-#pragma unroll
-            for (int g = 0; g < 2; ++g) st.mw[g] <<= 4 * (16 - st.nb);
-        }
-        typedef unsigned u2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-        for (int g = 0; g < 2; ++g)
-            __builtin_amdgcn_raw_buffer_store_b64(u2{st.m0[g], st.mw[g]}, st.rm, st.mrow_off == OOB ? OOB : st.mrow_off + 16u * g,
-                                                  0, 0);
-    }
-    c.head = f4{pv[0], pv[1], pv[2], pv[3]};
-    if (l + 1 == c.n_layers) return;
-    // the next layer's operand: the wave's image back into registers (same wave: LDS ops in order)
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-        c.xh[t] = *reinterpret_cast<const bf16x8*>(c.ximg + t * 2048 + c.lane * 16);
-        c.xl[t] = *reinterpret_cast<const bf16x8*>(c.ximg + t * 2048 + 1024 + c.lane * 16);
-    }
-}
-
-__device__ __forceinline__ void w32_composite_tile(C32& c, int tile) {
-    const int S = CF(int32_t, samples_per_ray);
-    const bool col_sigma = CF(int32_t, sigma_layer) >= 0;
-    char* regions = c.smem + w32::NRS * w32::RSLOT;
-    if (S > w32::TILE) {
-        if ((tile & 1) == 0) {
-            c.phead = c.head;
-            if (col_sigma) c.phead[3] = c.sig;
-            c.pcdist = c.cdist;
-            return;
-        }
-        if (c.lane < 32) {
-            char* reg = regions + COMP_OFF;       // wave 0's region
-            const int j = c.wave * w32::SPW + c.lane;
-            f4 hd = c.head;
-            if (col_sigma) hd[3] = c.sig;
-            *reinterpret_cast<f4*>(reg + j * 16) = c.phead;
-            *reinterpret_cast<float*>(reg + COMP_DEL + j * 4) = c.pcdist;
-            *reinterpret_cast<f4*>(reg + (w32::TILE + j) * 16) = hd;
-            *reinterpret_cast<float*>(reg + COMP_DEL + (w32::TILE + j) * 4) = c.cdist;
-        }
-        barrier();
-        asm volatile("" ::: "memory");
-        if (c.wave == 0) composite_wave<(2 * w32::TILE) / 64>(c, (int64_t)(tile >> 1), S);
-        return;
-    }
-    // ray r of the tile in wave (r % NW)'s region, at 2 KB (r / NW) (S = 16: 8 rays on 4 waves)
-    if (c.lane < 32) {
-        const int j = c.wave * w32::SPW + c.lane;
-        if (tile * w32::TILE + j < c.M) {
-            const int r = j / S, o = j - r * S;
-            char* reg = regions + (r % w32::NW) * w32::XIMG + COMP_OFF + (r / w32::NW) * 2048;
-            f4 hd = c.head;
-            if (col_sigma) hd[3] = c.sig;
-            *reinterpret_cast<f4*>(reg + o * 16) = hd;
-            *reinterpret_cast<float*>(reg + COMP_DEL + o * 4) = c.cdist;
-        }
-    }
-    barrier();
-    asm volatile("" ::: "memory");
-    const int rpt = w32::TILE / S;
-#pragma nounroll
-    for (int k = 0; k < 2; ++k) {
-        const int r = c.wave + w32::NW * k;
-        const int64_t ray = (int64_t)tile * rpt + r;
-        if (r < rpt && ray * S < c.M) {
-            if (S > 64)
-                composite_wave<2>(c, ray, S);
-            else
-                composite_wave<1>(c, ray, S, 2048 * k);
-        }
-    }
-}
-
-__global__ __launch_bounds__(w32::WGS) __attribute__((amdgpu_waves_per_eu(1, 1))) void mlp_fused32_kernel(FusedArgs a) {
-    __shared__ __attribute__((aligned(16))) char smem[w32::NRS * w32::RSLOT + w32::NW * w32::XIMG];
-    C32 c;
-    c.kargs = (kchar_t*)__builtin_amdgcn_kernarg_segment_ptr();
-    c.smem = smem;
-    c.rimg = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(a.img), 0, a.img_bytes, RSRC_W3);
-    c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    c.ximg = smem + w32::NRS * w32::RSLOT + c.wave * w32::XIMG;
-    c.lane = threadIdx.x & 63;
-    c.M = a.M;
-    c.n_layers = a.n_layers;
-    if ((int)blockIdx.x >= a.ntiles) return;
-    const int ngroups = a.ntiles / a.span;
-    const int my_tiles = a.span * ((ngroups - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x);
-    int per_tile = 0;
-    for (int l = 0; l < a.n_layers; ++l)
-        if (dma_units(c, l) > 0) per_tile += ((LF(int, N, l) + 31) >> 5) * (dma_units(c, l) / 8);
-    c.d_remaining = my_tiles * per_tile;
-    {
-        const int l = c.lane < c.n_layers ? c.lane : 0;
-        c.t_off = (int)LF(int64_t, img_off, l);
-        c.t_kbr = dma_units(c, l) / 2;
-        c.t_n16 = n16_of(LF(int, N, l));
-        c.t_next = next_ring_layer(c, l + 1 == c.n_layers ? 0 : l + 1);
-    }
-    const int l0 = next_ring_layer(c, 0);
-    c.cur = 0;
-    c.w_voff[0] = (unsigned)((c.wave >> 1) * 2048 + (c.wave & 1) * 1024 + c.lane * 16);
-    c.w_voff[1] = c.w_voff[0] + 4096u;
-    if (l0 >= 0) {
-        s_seek(c, l0);
-        bf16x8 wr[w32::WPW];
-        s_load(c, wr);
-        s_write<0>(c, 0, wr);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-        c.xh[t] = bf16x8{};
-        c.xl[t] = bf16x8{};
-    }
-#pragma unroll
-    for (int gp = 0; gp < 2; ++gp) {
-        c.gh[gp] = bf16x8{};
-        c.gl[gp] = bf16x8{};
-    }
-    c.sig = 0.f;
-    c.head = f4{0.f, 0.f, 0.f, 0.f};
-    const int span_log = a.span >> 1;
-    for (int it = 0; it < my_tiles; ++it) {
-        const int tile = (((int)blockIdx.x + (it >> span_log) * (int)gridDim.x) << span_log) + (it & span_log);
-        const int base = tile * w32::TILE + c.wave * w32::SPW;
-        if (a.comp_on) {
-            const float* dist = CF(cfptr_t, dist);
-            const int m = base + c.lane;
-            c.cdist = c.lane < 32 && m < c.M ? dist[m] : 0.f;
-        }
-        if (a.gen_mask != 0) {
-            float v0[9], v1[9];
-            if (a.gen_mask & 1) gen_load<w32::SPW>(c, 0, base, v0);
-            if (a.gen_mask & 2) gen_load<w32::SPW>(c, 1, base, v1);
-#pragma nounroll
-            for (int i = 0; i < 2; ++i) {
-                const int e = a.gen_lds == 0 ? 1 - i : i;
-                if ((a.gen_mask >> e) & 1) {
-                    float v[9];
-#pragma unroll
-                    for (int j = 0; j < 9; ++j) v[j] = e == 0 ? v0[j] : v1[j];
-                    gen_rows_lds<w32::SPW>(c, e, base, v);
-                    if (e == a.gen_reg) {
-#pragma unroll
-                        for (int gp = 0; gp < 2; ++gp)
-                            gen_block(c, c.lane & 31, 16 * gp + 8 * (c.lane >> 5), c.gh[gp], c.gl[gp]);
-                    }
-                    gen_store<w32::SPW>(c, e, base);
-                }
-            }
-        }
-        for (int l = 0; l < a.n_layers; ++l) {
-            switch (LF(int, type, l)) {
-                case 1: w32_layer<0, 1>(c, l, base); break;
-                case 2: w32_layer<0, 2>(c, l, base); break;
-                case 3: w32_layer<4, 0>(c, l, base); break;
-                case 6: w32_layer<8, 0>(c, l, base); break;
-                case 7: w32_layer<8, 1>(c, l, base); break;
-                case 8: w32_layer<8, 2>(c, l, base); break;
-                default: break;                          // rejected on the host
-            }
-        }
-        if (a.comp_on) w32_composite_tile(c, tile);
-    }
-}
-
 #undef LF
 #undef LFI
 #undef EF
@@ -2316,13 +1396,6 @@ __global__ __launch_bounds__(256) void fused_pack_kernel(PackArgs p, const int32
     } else {
         reinterpret_cast<float*>(img)[~d] = v;
     }
-}
-
-// NERF_FUSED_W32=1: the forward on 32-sample waves (mlp_fused32_kernel); read at every launch, so
-// that one process can compare the two kernels
-bool fused_w32() {
-    const char* e = getenv("NERF_FUSED_W32");
-    return e != nullptr && e[0] == '1';
 }
 
 int num_cus() {
@@ -2561,14 +1634,6 @@ int fused_launch(const nerf_fused_layer* layers, int32_t n_layers, const void* i
     }
     const int ngroups = a.ntiles / a.span;
     const int grid = ngroups < num_cus() ? ngroups : num_cus();
-    // the forward on 32-sample waves (mlp_fused32_kernel; its composite takes S >= 16: a tile's rays
-    // on two per wave at most)
-    const bool w32_ok = !dgrad && (comp == nullptr || comp->samples_per_ray * 2 * w32::NW >= w32::TILE);
-    if (w32_ok && fused_w32()) {
-        hipLaunchKernelGGL(mlp_fused32_kernel, dim3(grid), dim3(w32::WGS), 0, as_stream(stream), a);
-        NERF_CHECK_LAUNCH();
-        return NERF_OK;
-    }
     if (dgrad)
         hipLaunchKernelGGL(mlp_fused_kernel<MODE_DGRAD>, dim3(grid), dim3(WG), 0, as_stream(stream), a);
     else

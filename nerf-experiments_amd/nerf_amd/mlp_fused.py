@@ -44,8 +44,8 @@ def _pack_image(f) -> None:
 FUSED_TYPES = {(0, 1): 1, (0, 2): 2, (4, 0): 3, (8, 0): 6, (8, 1): 7, (8, 2): 8}   # (kbr, kbh) -> type
 ENABLED = os.environ.get("NERF_FUSED", "1") != "0"     # A/B switch (bench, tests)
 # a per-ray encoding read by a later layer comes from registers captured at the tile start; tests
-# turn this off to check that the library refuses the HBM read-back instead (the ordering rule);
-# NERF_FUSED_CAPTURE=0 lets investigation runs drive a library built before the capture existed
+# turn this off (NERF_FUSED_CAPTURE=0 or the module flag) to check that the library refuses the HBM
+# read-back instead (the ordering rule)
 CAPTURE_PER_RAY = os.environ.get("NERF_FUSED_CAPTURE", "1") != "0"
 
 

@@ -117,7 +117,10 @@ class _HashGridFn(th.autograd.Function):
         ctx.params = params
         ctx.rows = rows
         ctx.meta = (samples_per_ray, n, packed.shape)
-        ctx.save_for_backward(*(t if t is not None else th.empty(0) for t in (x, ray_o, ray_d, t_start, t_end, packed)))
+        # the packed table is read back only by the position gradient: saving it otherwise would make any
+        # in-place table update between forward and backward trip autograd's version check
+        keep = packed if any(ctx.needs_input_grad[4:7]) else None
+        ctx.save_for_backward(*(t if t is not None else th.empty(0) for t in (x, ray_o, ray_d, t_start, t_end, keep)))
         return out
 
     @staticmethod
