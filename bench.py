@@ -455,14 +455,17 @@ def evidence_tag(workload: str, fn: str) -> str:
     return f"{workload}_" + "".join(c if c.isalnum() or c == "_" else "_" for c in fn).strip("_")
 
 
-def _roofline(ks_fn: dict, x3: bool, steps: int, workload: str):
+def _roofline(ks_fn: dict, prec: str, steps: int, workload: str):
     """Roofline object for the MFMA kernel FUNCTION with the most device time in the timed region
     (launches grouped by HIP kernel function, as rocprofv3 reports them: the fused kernel's forward
-    and input-gradient-chain launches are one entry)."""
-    peak = X3_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
+    and input-gradient-chain launches are one entry).  prec: "x3" (peak = bf16 dense / 3 MFMAs per
+    product), "x1" (one bf16 pass: bf16 dense) or "fp32" (fp32 MFMA)."""
+    peak = {"x3": X3_PEAK_TFLOPS, "x1": BF16_MFMA_PEAK_TFLOPS}.get(prec, FP32_MFMA_PEAK_TFLOPS)
     # HIP kernel functions as rocprofv3 names them (template instantiations separately: the fused
-    # kernel's forward is mlp_fused_kernel<0>, its input-gradient chain mlp_fused_kernel<1>)
-    mfma_fns = ("mlp_fused_kernel<0>", "mlp_fused_kernel<1>", "linear_nt_x3_glds_kernel", "linear_nt_x3_kernel",
+    # kernel's forward is mlp_fused_kernel<0>, its input-gradient chain mlp_fused_kernel<1>; <2> / <3>
+    # in one bf16 pass)
+    mfma_fns = ("mlp_fused_kernel<0>", "mlp_fused_kernel<1>", "mlp_fused_kernel<2>", "mlp_fused_kernel<3>",
+                "linear_nt_x3_glds_kernel", "linear_nt_x3_kernel",
                 "linear_wgrad_x3_tr_kernel", "linear_wgrad_x3_stream_kernel", "linear_wgrad_x3_kernel", "linear_nt_kernel",
                 "linear_wgrad_kernel")
     cands = [k for k in mfma_fns if k in ks_fn]
@@ -490,7 +493,8 @@ def _roofline(ks_fn: dict, x3: bool, steps: int, workload: str):
             pmc = json.load(f)
     total_ms = sum(v["ms"] for v in ks_fn.values())
     return {"kernel": dom, "roles": r["tags"],
-            "precision": "3 x bf16 MFMA; peak = bf16 dense / 3" if x3 else "fp32 MFMA 32x32x2",
+            "precision": {"x3": "3 x bf16 MFMA; peak = bf16 dense / 3",
+                          "x1": "1 x bf16 MFMA (matmul precision medium); peak = bf16 dense"}.get(prec, "fp32 MFMA 32x32x2"),
             "bound": "hbm" if hbm_bound else "mfma",
             "achieved": achieved_gbs if hbm_bound else achieved,
             "peak": HBM_PEAK_GBS if hbm_bound else peak,
@@ -752,8 +756,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--matmul-precision", default="high", choices=("highest", "high", "medium"),
                     help="torch.set_float32_matmul_precision for the MLP GEMMs: highest = fp32 MFMA, "
-                         "high/medium = 3 x bf16 split MFMA (fp32-accurate to ~2^-16); the reference's "
-                         "naive-to-vanilla run uses medium + 16-mixed (main.py:53)")
+                         "high = 3 x bf16 split MFMA (fp32-accurate to ~2^-16), medium = one bf16 pass "
+                         "(the reference's naive-to-vanilla run: medium + 16-mixed, main.py:53,58)")
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -815,8 +819,8 @@ def main():
     ks = timer.summary()
     ks_fn = timer.summary(by="fn")
     from nerf_amd.mlp import matmul_precision
-    x3 = matmul_precision() == "x3"
-    roofline = _roofline(ks_fn, x3, args.steps, args.workload)
+    prec = matmul_precision()
+    roofline = _roofline(ks_fn, prec, args.steps, args.workload)
 
     # HBM roofline of the bandwidth-bound kernels BASELINE.json's north_star names (positional
     # encoding + alpha compositing): algorithmic bytes (kernels.py, per launch) / event-timed duration
@@ -838,8 +842,10 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
-            "matmul": ("3xbf16 split MFMA (hi*hi+hi*lo+lo*hi, fp32 accumulate)" if x3 else "fp32 MFMA"),
+            "dtype": "fp32" if prec != "x1" else "bf16 products, fp32 accumulate",
+            "matmul": {"x3": "3xbf16 split MFMA (hi*hi+hi*lo+lo*hi, fp32 accumulate)",
+                       "x1": "1xbf16 MFMA (bf16(w)*bf16(x), fp32 accumulate; matmul precision medium)"}.get(
+                prec, "fp32 MFMA"),
             "matmul_precision": args.matmul_precision,
             "data": ("synthetic: 100 procedural views at Lego scale, a fresh shuffled batch per step from the "
                      "on-device ray feed; random-init weights (torch.manual_seed(0))" if args.feed == "device" else

@@ -47,7 +47,8 @@ extern "C" {
 
 /* Library / ABI version (bumped on any signature or data-layout change; 6: NERF_FUSED_MASK;
  * 7: nerf_fused_composite / nerf_mlp_fused_render; 8: nerf_hashgrid_workspace_n, fused compositing
- * of 256-sample rays; 9: nerf_hashgrid_bwd_pos, seg_gen on later layers of the fused forward). */
+ * of 256-sample rays; 9: nerf_hashgrid_bwd_pos, seg_gen on later layers of the fused forward;
+ * 10: nerf_mlp_fused_run (single-pass bf16 flag), the passes argument of nerf_linear_wgrad_x3*). */
 int nerf_abi_version(void);
 const char* nerf_status_string(int status);
 /* sizeof of the argument structs, for bindings to check their layouts against:
@@ -290,7 +291,9 @@ int nerf_pack_weight(const float* W, int32_t N, int32_t K_orig, const int32_t* c
  * nerf_linear_wgrad_x3 writes the same workspace as nerf_linear_wgrad (reduce with
  * nerf_linear_wgrad_reduce, same M, K and N rounded up to 4); its N may be the true row count
  * (ld_dy >= pad4(N)): N <= 257 with N or K above 128 and K <= 256 runs as one 256 x 256 tile
- * per M split, row 256 on the vector ALUs in fp32. 
+ * per M split, row 256 on the vector ALUs in fp32.
+ * passes (ABI 10): 3 = the 3 x bf16 split products (matmul precision "high"), 1 = one bf16 pass
+ * bf16(dY) * bf16(X) with fp32 accumulation ("medium", as NERF_FUSED_BF16).
  * ------------------------------------------------------------------------- */
 int nerf_linear_fwd_x3(const nerf_seg* segs, int32_t n_segs, int64_t M,
                        const void* W_x, int32_t ldw, int32_t N, const float* bias,
@@ -298,7 +301,7 @@ int nerf_linear_fwd_x3(const nerf_seg* segs, int32_t n_segs, int64_t M,
                        const float* aux, int64_t ld_aux, void* stream);
 int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N,
                          const nerf_seg* segs, int32_t n_segs, int64_t M,
-                         void* workspace, size_t workspace_bytes, void* stream);
+                         void* workspace, size_t workspace_bytes, int32_t passes, void* stream);
 /* The same over two blocks of rows summed into one gradient (the two passes of a field used
  * twice per step: one launch and one reduce instead of two each): rows [0, M0) of (dY, segs),
  * then rows [0, M1) of (dY1, segs1), whose segments have the same widths; workspace and reduce
@@ -306,7 +309,7 @@ int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N,
 int nerf_linear_wgrad_x3_rows(const float* dY, int64_t ld_dy, const nerf_seg* segs, int64_t M0,
                               const float* dY1, int64_t ld_dy1, const nerf_seg* segs1, int64_t M1,
                               int32_t n_segs, int32_t N, void* workspace, size_t workspace_bytes,
-                              void* stream);
+                              int32_t passes, void* stream);
 /* nerf_linear_wgrad_x3_rows that also writes the per-ray sums of dY, raysum[ray][n] (n < N; rays of
  * samples_per_ray0 rows in block 0, then of samples_per_ray1 rows in block 1), from the streamed
  * single-tile kernel (N <= 256, 128 < N or 128 < K <= 256; 16 <= S <= 128 with S | 128, M0 % 128 = 0).
@@ -317,7 +320,7 @@ int nerf_linear_wgrad_x3_rays(const float* dY, int64_t ld_dy, const nerf_seg* se
                               const float* dY1, int64_t ld_dy1, const nerf_seg* segs1, int64_t M1,
                               int32_t n_segs, int32_t N, void* workspace, size_t workspace_bytes,
                               float* raysum, int32_t samples_per_ray0, int32_t samples_per_ray1,
-                              void* stream);
+                              int32_t passes, void* stream);
 int nerf_pack_weight_x3(const float* W, int32_t N, int32_t K_orig, const int32_t* col_map,
                         int32_t Kp, void* Wp_x, void* Wt_x, int32_t ldwt, void* stream);
 
@@ -458,6 +461,15 @@ typedef struct nerf_fused_composite {
 int nerf_mlp_fused_render(const nerf_fused_layer* layers, int32_t n_layers, const void* image, int64_t M,
                           const nerf_fused_encoding* encodings, const nerf_fused_composite* composite,
                           void* stream);
+
+/* nerf_mlp_fused_render with flags (ABI 10).  NERF_FUSED_BF16: every product in one bf16 pass
+ * (bf16(w) * bf16(x), fp32 accumulate: matmul precision "medium", the single-pass products of the
+ * reference's naive-to-vanilla/main.py:53,58 "medium" / 16-mixed C2 configuration) instead of the
+ * 3 x bf16 split (hi*hi + hi*lo + lo*hi, ~2^-17 per product).  Same image, descriptors and outputs. */
+#define NERF_FUSED_BF16 1
+int nerf_mlp_fused_run(const nerf_fused_layer* layers, int32_t n_layers, const void* image, int64_t M,
+                       const nerf_fused_encoding* encodings, const nerf_fused_composite* composite, int32_t flags,
+                       void* stream);
 
 /* Gather + split packer for the fused image: for i < n, v = srcs[map_src[i] >> 24][map_src[i] & 0xffffff]
  * (0 if map_src[i] < 0); map_dst[i] >= 0: bf16 element index of hi = bf16(v) (lo = bf16(v - hi)

@@ -1,7 +1,7 @@
 // Library-level C-ABI helpers (version, status strings).
 #include "common.h"
 
-extern "C" int nerf_abi_version(void) { return 9; }
+extern "C" int nerf_abi_version(void) { return 10; }
 
 extern "C" int64_t nerf_struct_size(int32_t which) {
     switch (which) {

@@ -77,6 +77,14 @@ __device__ __forceinline__ f32x16 mfma_x3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x
     c = mfma16(ah, bl, c);
     return mfma16(ah, bh, c);
 }
+// the weight gradients' products: the 3 x bf16 split, or (X1: matmul precision "medium") one bf16 pass
+template <bool X1>
+__device__ __forceinline__ f32x16 mfma_w(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x16 c) {
+    if constexpr (X1)
+        return mfma16(ah, bh, c);
+    else
+        return mfma_x3(ah, al, bh, bl, c);
+}
 
 __device__ __forceinline__ void split4(f4 v, bf16x4& hi, bf16x4& lo) {
     hi = __builtin_convertvector(v, bf16x4);
@@ -756,6 +764,7 @@ struct TNArgs {
     float* raysum; int rs_S0, rs_S1, rs_B0;
 };
 
+template <bool X1>
 __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
     constexpr int PL = TB * LDB;          // one transposed bf16 plane: 128 rows x 32 samples (swizzled)
     constexpr int BUFB = 4 * PL;          // dY^T hi, lo, X^T hi, lo
@@ -910,7 +919,7 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x3(yh[i], yl[i], xh[j], xl[j], acc[i][j]);
+                    for (int j = 0; j < 2; ++j) acc[i][j] = mfma_w<X1>(yh[i], yl[i], xh[j], xl[j], acc[i][j]);
             }
             if (has_next) sstore(cur ^ 1);
             __syncthreads();
@@ -966,7 +975,7 @@ __global__ __launch_bounds__(256, 2) void linear_wgrad_x3_kernel(TNArgs a) {
 constexpr int WS_T = 16;                        // samples per step
 constexpr int WS_RAW = 2 * WS_T * 1024;         // ring stage: dY rows then X rows, 1 KB each
 constexpr int WS_IMG = 2 * 256 * 64;            // image stage: Y rows then X rows, 64 B each
-template <int NRAW, int NIMG>
+template <int NRAW, int NIMG, bool X1>
 __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void linear_wgrad_x3_stream_kernel(TNArgs a, int npad, int kpad) {
     static_assert(NRAW * WS_RAW + NIMG * WS_IMG <= 160 * 1024, "LDS");
     __shared__ __attribute__((aligned(16))) char smem[NRAW * WS_RAW + NIMG * WS_IMG];
@@ -1184,7 +1193,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[ii][j] = mfma_x3(yh[ii], yl[ii], xh[j], xl[j], acc[ii][j]);
+            for (int j = 0; j < 2; ++j) acc[ii][j] = mfma_w<X1>(yh[ii], yl[ii], xh[j], xl[j], acc[ii][j]);
     };
     if (steps > 0) {
         // prologue: steps 0 .. NRAW-1 issued, step 0 converted, step 1 landed
@@ -1291,7 +1300,7 @@ __device__ __forceinline__ wt_gfp wt_src_row(wt_gfp s0, wt_gfp s1, int64_t ld0, 
     return (b1 ? s1 : s0) + (int64_t)rr * (b1 ? ld1 : ld0);
 }
 
-template <bool ROW257, bool RAYS>
+template <bool ROW257, bool RAYS, bool X1>
 __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void linear_wgrad_x3_tr_kernel(
     TNArgs a, int npad, int kpad) {
     __shared__ __attribute__((aligned(16))) char smem[2 * WT_IMG + (RAYS ? 2 * WT_RS : 0)];
@@ -1502,7 +1511,7 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[ii][j] = mfma_x3(yh[ii], yl[ii], xh[j], xl[j], acc[ii][j]);
+            for (int j = 0; j < 2; ++j) acc[ii][j] = mfma_w<X1>(yh[ii], yl[ii], xh[j], xl[j], acc[ii][j]);
     };
     auto barrier = []() __attribute__((always_inline)) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS writes / reads done
@@ -1884,7 +1893,9 @@ static const bool WGRAD_TR = [] {
 static int wgrad_x3_rows_impl(const float* dY, int64_t ld_dy, const nerf_seg* segs, int64_t M0,
                               const float* dY1, int64_t ld_dy1, const nerf_seg* segs1, int64_t M1,
                               int32_t n_segs, int32_t N, void* workspace, size_t workspace_bytes,
-                              float* raysum, int32_t S0, int32_t S1, void* stream) {
+                              float* raysum, int32_t S0, int32_t S1, int32_t passes, void* stream) {
+    NERF_REQUIRE(passes == 1 || passes == 3);
+    const bool x1 = passes == 1;
     // N need not be a multiple of 4: the kernels read dY in 4-column pieces up to pad4(N) <= ld_dy;
     // slab rows past N are left unspecified (nerf_linear_wgrad_reduce's n_valid <= N)
     const int64_t M = M0 + M1;
@@ -1961,17 +1972,28 @@ static int wgrad_x3_rows_impl(const float* dY, int64_t ld_dy, const nerf_seg* se
         hipStream_t st = as_stream(stream);
         if (WGRAD_TR) {
             // register-staged rows, transposed LDS reads (linear_wgrad_x3_tr_kernel)
-            if (N > 256) hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<true, false>), grid, block, 0, st, a, ntn * TB, ntk * TB);
-            else if (raysum) hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<false, true>), grid, block, 0, st, a, ntn * TB, ntk * TB);
-            else hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<false, false>), grid, block, 0, st, a, ntn * TB, ntk * TB);
+            if (x1) {
+                if (N > 256) hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<true, false, true>), grid, block, 0, st, a, ntn * TB, ntk * TB);
+                else if (raysum) hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<false, true, true>), grid, block, 0, st, a, ntn * TB, ntk * TB);
+                else hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<false, false, true>), grid, block, 0, st, a, ntn * TB, ntk * TB);
+            } else {
+                if (N > 256) hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<true, false, false>), grid, block, 0, st, a, ntn * TB, ntk * TB);
+                else if (raysum) hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<false, true, false>), grid, block, 0, st, a, ntn * TB, ntk * TB);
+                else hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<false, false, false>), grid, block, 0, st, a, ntn * TB, ntk * TB);
+            }
+        } else if (x1) {
+            hipLaunchKernelGGL((linear_wgrad_x3_stream_kernel<3, 2, true>), grid, block, 0, st, a, ntn * TB, ntk * TB);
         } else {
-            hipLaunchKernelGGL((linear_wgrad_x3_stream_kernel<3, 2>), grid, block, 0, st, a, ntn * TB, ntk * TB);
+            hipLaunchKernelGGL((linear_wgrad_x3_stream_kernel<3, 2, false>), grid, block, 0, st, a, ntn * TB, ntk * TB);
         }
         NERF_CHECK_LAUNCH();
         return NERF_OK;
     }
     const int64_t blocks = (int64_t)splits * ntn * ntk;
-    hipLaunchKernelGGL(linear_wgrad_x3_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
+    if (x1)
+        hipLaunchKernelGGL(linear_wgrad_x3_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
+    else
+        hipLaunchKernelGGL(linear_wgrad_x3_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
     NERF_CHECK_LAUNCH();
     return NERF_OK;
 }
@@ -1979,25 +2001,25 @@ static int wgrad_x3_rows_impl(const float* dY, int64_t ld_dy, const nerf_seg* se
 extern "C" int nerf_linear_wgrad_x3_rows(const float* dY, int64_t ld_dy, const nerf_seg* segs, int64_t M0,
                                          const float* dY1, int64_t ld_dy1, const nerf_seg* segs1, int64_t M1,
                                          int32_t n_segs, int32_t N, void* workspace, size_t workspace_bytes,
-                                         void* stream) {
+                                         int32_t passes, void* stream) {
     return wgrad_x3_rows_impl(dY, ld_dy, segs, M0, dY1, ld_dy1, segs1, M1, n_segs, N, workspace, workspace_bytes,
-                              nullptr, 0, 0, stream);
+                              nullptr, 0, 0, passes, stream);
 }
 
 extern "C" int nerf_linear_wgrad_x3_rays(const float* dY, int64_t ld_dy, const nerf_seg* segs, int64_t M0,
                                          const float* dY1, int64_t ld_dy1, const nerf_seg* segs1, int64_t M1,
                                          int32_t n_segs, int32_t N, void* workspace, size_t workspace_bytes,
                                          float* raysum, int32_t samples_per_ray0, int32_t samples_per_ray1,
-                                         void* stream) {
+                                         int32_t passes, void* stream) {
     NERF_REQUIRE(raysum != nullptr);
     return wgrad_x3_rows_impl(dY, ld_dy, segs, M0, dY1, ld_dy1, segs1, M1, n_segs, N, workspace, workspace_bytes,
-                              raysum, samples_per_ray0, samples_per_ray1, stream);
+                              raysum, samples_per_ray0, samples_per_ray1, passes, stream);
 }
 
 extern "C" int nerf_linear_wgrad_x3(const float* dY, int64_t ld_dy, int32_t N, const nerf_seg* segs, int32_t n_segs,
-                                    int64_t M, void* workspace, size_t workspace_bytes, void* stream) {
+                                    int64_t M, void* workspace, size_t workspace_bytes, int32_t passes, void* stream) {
     return nerf_linear_wgrad_x3_rows(dY, ld_dy, segs, M, nullptr, 0, nullptr, 0, n_segs, N, workspace,
-                                     workspace_bytes, stream);
+                                     workspace_bytes, passes, stream);
 }
 
 extern "C" int nerf_pack_weight_x3(const float* W, int32_t N, int32_t K_orig, const int32_t* col_map, int32_t Kp,

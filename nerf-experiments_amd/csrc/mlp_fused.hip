@@ -75,8 +75,13 @@ constexpr int ST_AUX = 2;
 // the forward, the bias load at the start of the chunk itself.  The input-gradient chain has no
 // biases and loads none: a zero-bias load there, waited for at the epilogue, made every chunk wait
 // for the previous chunk's dY stores (profiles/r05ac).
+// kernel modes: bit 0 = the backward's input-gradient chain (else the forward), bit 1 = one bf16
+// pass (hi * hi: matmul precision "medium", the reference's single-pass bf16 / fp16 products) instead
+// of the 3 x bf16 split (lo * hi + hi * lo + hi * hi: "high")
+constexpr bool is_fwd(int mode) { return (mode & 1) == 0; }
+constexpr bool is_x1(int mode) { return (mode & 2) != 0; }
 template <int MODE>
-constexpr int after_dma_vm() { return MODE == 0 ? 1 + 2 * SB : 2 * SB; }
+constexpr int after_dma_vm() { return is_fwd(MODE) ? 1 + 2 * SB : 2 * SB; }
 // Layer-output stores in chunk pairs: a 16-row chunk is 64 B of each sample row, half a 128-B line.
 // The even chunk's values wait in registers for the odd one's.  The input-gradient chain writes each
 // pair as two stores each covering whole lines of 8 samples (lanes s and s ^ 8 trade halves by a DPP
@@ -173,12 +178,20 @@ template <int N>
 __device__ __forceinline__ void lds_wait(bf16x8& f0, bf16x8& f1) {
     asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(f0), "+v"(f1) : "n"(N));
 }
+template <int N>
+__device__ __forceinline__ void lds_wait1(bf16x8& f0) {
+    asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(f0) : "n"(N));
+}
 // The HBM-fed weight fragments and the biases are inline-asm buffer loads waited for by explicit
 // counts (hipcc's own wait for a buffer load in the chunk loop is vmcnt(0), which also waits for the
 // DMA issued before it); the loaded values pass through the wait statements.
 template <int N>
 __device__ __forceinline__ void frag_vwait(bf16x8& f0, bf16x8& f1) {
     asm volatile("s_waitcnt vmcnt(%2)" : "+v"(f0), "+v"(f1) : "n"(N));
+}
+template <int N>
+__device__ __forceinline__ void frag_vwait1(bf16x8& f0) {
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(f0) : "n"(N));
 }
 template <int N>
 __device__ __forceinline__ void bias_wait(f4& b) {
@@ -202,6 +215,7 @@ __device__ __forceinline__ unsigned shift_in_dead(unsigned t, float x) {
 // input-gradient chain (ReLU-bit multiply, second output for encoding rows; no bias)
 constexpr int MODE_FWD = 0;
 constexpr int MODE_DGRAD = 1;
+constexpr int MODE_X1 = 2;
 
 struct Ctx {
     kchar_t* kargs;
@@ -575,6 +589,12 @@ __device__ __forceinline__ void split2(float x, float y, unsigned& hi, unsigned&
     lo = __builtin_bit_cast(unsigned, __builtin_convertvector(d, bf16x2));
 }
 
+// bf16(x), bf16(y) packed (round to nearest even: the hi half of split2)
+__device__ __forceinline__ unsigned hi2(float x, float y) {
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(unsigned, __builtin_convertvector((f4{x, y, 0.f, 0.f}).xy, bf16x2));
+}
+
 __device__ __forceinline__ bool pair_odd(int ch) { return ch >= 0 && (ch & 1) != 0; }
 
 __device__ __forceinline__ float ror8(float x) {      // lane (s ^ 8) of this lane's 16-lane row
@@ -633,7 +653,7 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
         if (p >= SB) return;
         const int sb = p;
         f4& v = a[sb];
-        if constexpr (MODE == MODE_FWD) {
+        if constexpr (is_fwd(MODE)) {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 v[r] = __builtin_bit_cast(float, max(__builtin_bit_cast(int, v[r] + b[r]), st.floor_i));
@@ -710,7 +730,7 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
             }
         }
     } else if (p == 2) {
-        if constexpr (MODE == MODE_FWD) {
+        if constexpr (is_fwd(MODE)) {
             // NERF_FUSED_MASK layout: the lane's own bits, no cross-lane step.  The bits of rows
             // 4 g + r of chunks 0-7 / 8-15 shift into a word of their own, !(a > 0) entering as the
             // carry of t + t (two VALU per value; the NERF_EPI_MASKOUT layout's per-sample words
@@ -740,13 +760,18 @@ __device__ __forceinline__ void epi_part(Ctx& c, LayerState& st, int p, int ch, 
 #pragma unroll
             for (int sb = 0; sb < SB; ++sb) {
                 typedef unsigned u2 __attribute__((ext_vector_type(2)));
-                unsigned h0, l0, h1, l1;
-                split2(a[sb][0], a[sb][1], h0, l0);
-                split2(a[sb][2], a[sb][3], h1, l1);
-                const u2 h = {h0, h1}, lo = {l0, l1};
                 char* d = c.ximg + ((q * SB + sb) * 2) * 1024 + c.lane * 16 + 8 * bb;
-                *reinterpret_cast<u2*>(d) = h;
-                *reinterpret_cast<u2*>(d + 1024) = lo;
+                if constexpr (is_x1(MODE)) {
+                    // the next layer's operand rounded once (the lo half is never read)
+                    *reinterpret_cast<u2*>(d) = u2{hi2(a[sb][0], a[sb][1]), hi2(a[sb][2], a[sb][3])};
+                } else {
+                    unsigned h0, l0, h1, l1;
+                    split2(a[sb][0], a[sb][1], h0, l0);
+                    split2(a[sb][2], a[sb][3], h1, l1);
+                    const u2 h = {h0, h1}, lo = {l0, l1};
+                    *reinterpret_cast<u2*>(d) = h;
+                    *reinterpret_cast<u2*>(d + 1024) = lo;
+                }
             }
         }
     }
@@ -768,18 +793,19 @@ __host__ __device__ constexpr int epi_placed() {                 // parts placed
 // there): forward 3, chain 4.  One box, three rotating repetitions (profiles/r05x), ms per step
 // forward / chain: 1: 3.84 / 3.44, 2: 3.83 / 3.42, 3: 3.77 / 3.41, 4: 3.89 / 3.39
 template <int MODE>
-constexpr int epi0_of() { return MODE == 0 ? 3 : 4; }
+constexpr int epi0_of() { return is_fwd(MODE) ? 3 : 4; }
 
 // k-steps of weight fragments read ahead of the step being multiplied
 constexpr int FA = 2;
 
-// the chunk's first min(FA, KBR) steps' fragment reads (compile-time LDS offsets)
-template <int KBR, int I>
+// the chunk's first min(FA, KBR) steps' fragment reads (compile-time LDS offsets; the hi halves
+// only in a single-pass mode)
+template <int MODE, int KBR, int I>
 __device__ __forceinline__ void first_reads(bf16x8 (&fr)[FA][2], unsigned sa) {
     if constexpr (I < FA && I < KBR) {
         lds_frag<I * 2048>(fr[I][0], sa);
-        lds_frag<I * 2048 + 1024>(fr[I][1], sa);
-        first_reads<KBR, I + 1>(fr, sa);
+        if constexpr (!is_x1(MODE)) lds_frag<I * 2048 + 1024>(fr[I][1], sa);
+        first_reads<MODE, KBR, I + 1>(fr, sa);
     }
 }
 
@@ -796,22 +822,28 @@ __device__ __forceinline__ void reg_steps(Ctx& c, LayerState& st, unsigned sa, b
         // (epilogue part 3's operand-image writes in the previous stage may land on either side of
         // that stage's fragment reads — the asm reads carry no memory clobber — so they are not
         // counted as younger: waiting for them too is the safe side)
-        lds_wait<2 * later>(f[0], f[1]);
-        // products lo*hi + hi*lo + hi*hi per accumulator (small terms first, as linear_x3.hip)
+        if constexpr (is_x1(MODE)) {
+            lds_wait1<later>(f[0]);
 #pragma unroll
-        for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(f[1], c.xh[KB_I][sb], a[sb]);
+            for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(f[0], c.xh[KB_I][sb], a[sb]);
+        } else {
+            lds_wait<2 * later>(f[0], f[1]);
+            // products lo*hi + hi*lo + hi*hi per accumulator (small terms first, as linear_x3.hip)
 #pragma unroll
-        for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(f[0], c.xl[KB_I][sb], a[sb]);
+            for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(f[1], c.xh[KB_I][sb], a[sb]);
 #pragma unroll
-        for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(f[0], c.xh[KB_I][sb], a[sb]);
+            for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(f[0], c.xl[KB_I][sb], a[sb]);
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(f[0], c.xh[KB_I][sb], a[sb]);
+        }
         if constexpr (KB_I + FA < KBR) {
             lds_frag<(KB_I + FA) * 2048>(f[0], sa);
-            lds_frag<(KB_I + FA) * 2048 + 1024>(f[1], sa);
+            if constexpr (!is_x1(MODE)) lds_frag<(KB_I + FA) * 2048 + 1024>(f[1], sa);
         }
         // (placing the epilogue parts of the two waves of a SIMD at different stages, 0-2 and 4-6,
         // measured slower: chain 3.78 -> 4.03-4.09 ms, forward 3.86 -> 3.94-4.00 per mip step)
-        if constexpr (KB_I == EPI0 && MODE == MODE_FWD)
-            bias_wait<(KBR > 0 ? DMA_PER_WAVE : 0) + 2 * KBH>(pb);
+        if constexpr (KB_I == EPI0 && is_fwd(MODE))
+            bias_wait<(KBR > 0 ? DMA_PER_WAVE : 0) + (is_x1(MODE) ? 1 : 2) * KBH>(pb);   // (younger: the DMA, the HBM fragments)
         if constexpr (KB_I >= EPI0 && KB_I < EPI0 + epi_placed<KBR, EPI0>())
             epi_part<MODE, EPAR>(c, st, epi_part_of(KB_I - EPI0), ch - 1, pv, pb);
         __builtin_amdgcn_sched_barrier(0);
@@ -851,7 +883,7 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
     }
     st.ro = __builtin_amdgcn_make_buffer_rsrc(LF(fptr_t, out, l), 0, c.M * ldo * 4, RSRC_W3);
     st.bias_off = (unsigned)LF(int64_t, bias_off, l) + 16u * g;
-    if constexpr (MODE == MODE_FWD) {
+    if constexpr (is_fwd(MODE)) {
         uint8_t* mptr = LF(u8ptr_t, mask, l);
         st.rm = __builtin_amdgcn_make_buffer_rsrc(mptr, 0, mptr != nullptr ? c.M * 32 : 0, RSRC_W3);
         float* cptr = LF(fptr_t, col_out, l);
@@ -898,12 +930,12 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
             const int sg = kh < kb0 ? 0 : 1;            // segment of this block
             const int khl = sg ? kh - kb0 : kh;
             const int gen = sg ? LFI(int, seg_gen, 1, l) : LFI(int, seg_gen, 0, l);
-            if (MODE == MODE_DGRAD && gen >= 3) {       // the fused composite's head / density gradient
+            if (!is_fwd(MODE) && gen >= 3) {       // the fused composite's head / density gradient
                 comp_grad_block(c, gen, sg ? LFI(cfptr_t, seg_ptr, 1, l) : LFI(cfptr_t, seg_ptr, 0, l), sample,
                                 row_ok, hh[kh], hl[kh]);
                 continue;
             }
-            if (MODE == MODE_FWD && gen != 0) {
+            if (is_fwd(MODE) && gen != 0) {
                 if constexpr (KBR == 0) {               // the first layer: generated at the tile start, still in LDS
 #pragma unroll
                     for (int sb = 0; sb < SB; ++sb)
@@ -943,7 +975,12 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
 #pragma unroll
         for (int kh = 0; kh < KBH; ++kh)
 #pragma unroll
-            for (int sb = 0; sb < SB; ++sb) asm volatile("" : "+v"(hh[kh][sb]), "+v"(hl[kh][sb]));
+            for (int sb = 0; sb < SB; ++sb) {
+                if constexpr (is_x1(MODE))
+                    asm volatile("" : "+v"(hh[kh][sb]));
+                else
+                    asm volatile("" : "+v"(hh[kh][sb]), "+v"(hl[kh][sb]));
+            }
     }
     const unsigned hbm_frag = (unsigned)LF(int, hbm_off, l) + (unsigned)c.lane * 16u;
 
@@ -960,14 +997,14 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
 #pragma unroll
             for (int kh = 0; kh < KBH; ++kh)
 #pragma unroll
-                for (int hl_ = 0; hl_ < 2; ++hl_)
+                for (int hl_ = 0; hl_ < (is_x1(MODE) ? 1 : 2); ++hl_)
                     f[kh][hl_] = __builtin_bit_cast(
                         bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
                                     c.rimg, hbm_frag + (unsigned)(((ch * KBH + kh) * 2 + hl_) * 1024), 0, 0));
         };
         auto bias_load = [&](int ch) __attribute__((always_inline)) {
             return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
-                                              c.rimg, st.bias_off + (MODE == MODE_FWD ? 64u * (unsigned)ch : 0u), 0, 0));
+                                              c.rimg, st.bias_off + (is_fwd(MODE) ? 64u * (unsigned)ch : 0u), 0, 0));
         };
         // two fragment / bias buffers used alternately (a register copy of a just-issued load would
         // wait for it): chunk ch multiplies `cur` while chunk ch + 1's loads land in `nxt`
@@ -982,10 +1019,12 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
             for (int sb = 0; sb < SB; ++sb) a[sb] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int kh = 0; kh < KBH; ++kh) {
+                if constexpr (!is_x1(MODE)) {
 #pragma unroll
-                for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(cur[kh][1], hh[kh][sb], a[sb]);
+                    for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(cur[kh][1], hh[kh][sb], a[sb]);
 #pragma unroll
-                for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(cur[kh][0], hl[kh][sb], a[sb]);
+                    for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(cur[kh][0], hl[kh][sb], a[sb]);
+                }
 #pragma unroll
                 for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(cur[kh][0], hh[kh][sb], a[sb]);
             }
@@ -1007,7 +1046,7 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
         // the previous chunk's biases (rows 4 g .. 4 g + 3), for its epilogue in this chunk, issued
         // before this chunk's DMA so that waiting for it does not wait for the DMA
         f4 pb = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (MODE == MODE_FWD)
+        if constexpr (is_fwd(MODE))
             buf_load16(pb, st.bias_off + 64u * (unsigned)(ch > 0 ? ch - 1 : 0), c.rimg);
         const unsigned sa = lds_addr(c.smem + c.cur * SLOT_BYTES + c.lane * 16);
         bf16x8 fr[FA][2];
@@ -1022,7 +1061,7 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
 #ifdef NERF_FUSED_DIAG_BAR2             // diagnostic builds only: a second barrier (the cost of one at aligned waves)
             barrier();
 #endif
-            first_reads<KBR, 0>(fr, sa);
+            first_reads<MODE, KBR, 0>(fr, sa);
             issue_dma(c, c.cur ^ 1);                 // the next register-fed chunk, a whole chunk ahead
             __builtin_amdgcn_sched_barrier(0);      // keep the DMA ahead of this chunk's vmem ops (vmcnt)
         }
@@ -1031,7 +1070,7 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
 #pragma unroll
         for (int kh = 0; kh < KBH; ++kh)
 #pragma unroll
-            for (int hl_ = 0; hl_ < 2; ++hl_)
+            for (int hl_ = 0; hl_ < (is_x1(MODE) ? 1 : 2); ++hl_)
                 buf_load16(hf[kh][hl_], hbm_frag + (unsigned)(((ch * KBH + kh) * 2 + hl_) * 1024), c.rimg);
         f4 a[SB];
 #pragma unroll
@@ -1040,13 +1079,20 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
         // the HBM-fed fragments have landed: with a register-fed part the 4 epilogue stores of parts
         // 0-1 were issued after them
 #pragma unroll
-        for (int kh = 0; kh < KBH; ++kh) frag_vwait<(KBR > 0 ? 2 * SB : 0)>(hf[kh][0], hf[kh][1]);
+        for (int kh = 0; kh < KBH; ++kh) {
+            if constexpr (is_x1(MODE))
+                frag_vwait1<(KBR > 0 ? 2 * SB : 0)>(hf[kh][0]);
+            else
+                frag_vwait<(KBR > 0 ? 2 * SB : 0)>(hf[kh][0], hf[kh][1]);
+        }
 #pragma unroll
         for (int kh = 0; kh < KBH; ++kh) {
+            if constexpr (!is_x1(MODE)) {
 #pragma unroll
-            for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(hf[kh][1], hh[kh][sb], a[sb]);
+                for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(hf[kh][1], hh[kh][sb], a[sb]);
 #pragma unroll
-            for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(hf[kh][0], hl[kh][sb], a[sb]);
+                for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(hf[kh][0], hl[kh][sb], a[sb]);
+            }
 #pragma unroll
             for (int sb = 0; sb < SB; ++sb) a[sb] = mfma16(hf[kh][0], hh[kh][sb], a[sb]);
             __builtin_amdgcn_sched_barrier(0);
@@ -1069,14 +1115,14 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
     }
     {
         f4 lb = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (MODE == MODE_FWD) {
+        if constexpr (is_fwd(MODE)) {
             buf_load16(lb, st.bias_off + 64u * (unsigned)(NC - 1), c.rimg);
             bias_wait<0>(lb);
         }
 #pragma unroll
         for (int p = 0; p < 4; ++p) epi_part<MODE>(c, st, p, NC - 1, pv, lb);
     }
-    if constexpr (MODE == MODE_FWD) {
+    if constexpr (is_fwd(MODE)) {
         // the lane's two mask words, each chunk's nibble at 4 (7 - (ch & 7)) whatever the chunk count
         const int nb = NC < 2 * KBMAX ? NC : 2 * KBMAX;
         if (nb < 8) {
@@ -1094,7 +1140,7 @@ __device__ __forceinline__ void fused_layer(Ctx& c, int l, int base) {
         for (int sb = 0; sb < SB; ++sb)
             __builtin_amdgcn_raw_buffer_store_b64(u2{st.mw[sb][0], st.mw[sb][1]}, st.rm, st.mrow_off[sb], 0, 0);
     }
-    if constexpr (MODE == MODE_FWD) {
+    if constexpr (is_fwd(MODE)) {
 #pragma unroll
         for (int sb = 0; sb < SB; ++sb) c.head[sb] = pv[sb];
     }
@@ -1282,7 +1328,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
     // (their memory round trip no longer opens every tile; at the last / third-to-last layer or before
     // the compositing measured slower, profiles/r05ao)
     float gv0[9], gv1[9];
-    if (MODE == MODE_FWD && a.gen_mask != 0 && my_tiles > 0) {
+    if (is_fwd(MODE) && a.gen_mask != 0 && my_tiles > 0) {
         const int nb = tile_of(0) * TILE + c.wave * SPW;
         if (a.gen_mask & 1) gen_load<SPW>(c, 0, nb, gv0);
         if (a.gen_mask & 2) gen_load<SPW>(c, 1, nb, gv1);
@@ -1290,7 +1336,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
     for (int it = 0; it < my_tiles; ++it) {
         const int tile = tile_of(it);
         const int base = tile * TILE + c.wave * SPW;
-        if (MODE == MODE_FWD && a.comp_on) {
+        if (is_fwd(MODE) && a.comp_on) {
             // the samples' interval lengths for the tile-end compositing (long landed by then)
             const float* dist = CF(cfptr_t, dist);
 #pragma unroll
@@ -1300,7 +1346,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
             }
         }
 #ifndef NERF_FUSED_DIAG_NOGEN           // diagnostic builds only: timing without the tile-start encodings
-        if (MODE == MODE_FWD && a.gen_mask != 0) {
+        if (is_fwd(MODE) && a.gen_mask != 0) {
 #else
         if (false) {
 #endif
@@ -1338,7 +1384,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
             }
         }
         for (int l = 0; l < a.n_layers; ++l) {
-            if (MODE == MODE_FWD && a.gen_mask != 0 && it + 1 < my_tiles &&
+            if (is_fwd(MODE) && a.gen_mask != 0 && it + 1 < my_tiles &&
                 l == (a.n_layers > 2 ? a.n_layers - 2 : 0)) {
                 const int nb = tile_of(it + 1) * TILE + c.wave * SPW;
                 if (a.gen_mask & 1) gen_load<SPW>(c, 0, nb, gv0);
@@ -1354,9 +1400,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWAVE / 4, N
                 default: break;                          // rejected on the host
             }
         }
-        if (MODE == MODE_FWD && a.comp_on) composite_tile(c, tile);
+        if (is_fwd(MODE) && a.comp_on) composite_tile(c, tile);
 #ifdef NERF_FUSED_DIAG_COMP2            // diagnostic builds only: the compositing twice (same outputs, its cost at unchanged data)
-        if (MODE == MODE_FWD && a.comp_on) composite_tile(c, tile);
+        if (is_fwd(MODE) && a.comp_on) composite_tile(c, tile);
 #endif
     }
 #ifdef NERF_FUSED_DIAG_MFMAONLY
@@ -1456,7 +1502,9 @@ bool encoding_ok(const nerf_fused_encoding& e, int64_t M) {
 
 namespace {
 int fused_launch(const nerf_fused_layer* layers, int32_t n_layers, const void* image, int64_t M,
-                 const nerf_fused_encoding* encodings, const nerf_fused_composite* comp, void* stream) {
+                 const nerf_fused_encoding* encodings, const nerf_fused_composite* comp, int32_t flags, void* stream) {
+    NERF_REQUIRE((flags & ~NERF_FUSED_BF16) == 0);
+    const bool single_pass = (flags & NERF_FUSED_BF16) != 0;
     NERF_REQUIRE(layers != nullptr && image != nullptr);
     NERF_REQUIRE(n_layers >= 1 && n_layers <= NERF_FUSED_MAX_LAYERS);
     NERF_REQUIRE(M >= 1 && M <= (int64_t)1 << 30);
@@ -1634,10 +1682,16 @@ int fused_launch(const nerf_fused_layer* layers, int32_t n_layers, const void* i
     }
     const int ngroups = a.ntiles / a.span;
     const int grid = ngroups < num_cus() ? ngroups : num_cus();
-    if (dgrad)
+    if (single_pass) {
+        if (dgrad)
+            hipLaunchKernelGGL(mlp_fused_kernel<MODE_DGRAD | MODE_X1>, dim3(grid), dim3(WG), 0, as_stream(stream), a);
+        else
+            hipLaunchKernelGGL(mlp_fused_kernel<MODE_FWD | MODE_X1>, dim3(grid), dim3(WG), 0, as_stream(stream), a);
+    } else if (dgrad) {
         hipLaunchKernelGGL(mlp_fused_kernel<MODE_DGRAD>, dim3(grid), dim3(WG), 0, as_stream(stream), a);
-    else
+    } else {
         hipLaunchKernelGGL(mlp_fused_kernel<MODE_FWD>, dim3(grid), dim3(WG), 0, as_stream(stream), a);
+    }
     NERF_CHECK_LAUNCH();
     return NERF_OK;
 }
@@ -1645,13 +1699,19 @@ int fused_launch(const nerf_fused_layer* layers, int32_t n_layers, const void* i
 
 extern "C" int nerf_mlp_fused_fwd(const nerf_fused_layer* layers, int32_t n_layers, const void* image, int64_t M,
                                   const nerf_fused_encoding* encodings, void* stream) {
-    return fused_launch(layers, n_layers, image, M, encodings, nullptr, stream);
+    return fused_launch(layers, n_layers, image, M, encodings, nullptr, 0, stream);
 }
 
 extern "C" int nerf_mlp_fused_render(const nerf_fused_layer* layers, int32_t n_layers, const void* image, int64_t M,
                                      const nerf_fused_encoding* encodings, const nerf_fused_composite* composite,
                                      void* stream) {
-    return fused_launch(layers, n_layers, image, M, encodings, composite, stream);
+    return fused_launch(layers, n_layers, image, M, encodings, composite, 0, stream);
+}
+
+extern "C" int nerf_mlp_fused_run(const nerf_fused_layer* layers, int32_t n_layers, const void* image, int64_t M,
+                                  const nerf_fused_encoding* encodings, const nerf_fused_composite* composite,
+                                  int32_t flags, void* stream) {
+    return fused_launch(layers, n_layers, image, M, encodings, composite, flags, stream);
 }
 
 extern "C" int nerf_fused_pack(const float* const* srcs, int32_t n_srcs, const int32_t* map_src,

@@ -35,6 +35,7 @@ NERF_EPI_NARROW_TILE = 512
 NERF_EPI_TANH = 4096
 NERF_EPI_TANH_BWD = 8192
 NERF_ERR_UNSUPPORTED = -2
+NERF_FUSED_BF16 = 1
 NERF_KABSCH_MAX_POINTS = 4096
 NERF_PROP_MAX_EDGES = 512
 NERF_GAUSS_FWD = 0
@@ -210,17 +211,20 @@ _SIGNATURES = {
     "nerf_linear_gauss_workspace": (c_sz, [c_i64, c_i32]),
     "nerf_linear_gauss_x3": (c_i32, [ctypes.POINTER(NerfSeg), c_i32, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp, c_i64,
                                      c_i32, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_sz, c_vp]),
-    "nerf_linear_wgrad_x3": (c_i32, [c_vp, c_i64, c_i32, ctypes.POINTER(NerfSeg), c_i32, c_i64, c_vp, c_sz, c_vp]),
+    "nerf_linear_wgrad_x3": (c_i32, [c_vp, c_i64, c_i32, ctypes.POINTER(NerfSeg), c_i32, c_i64, c_vp, c_sz, c_i32,
+                                     c_vp]),
     "nerf_linear_wgrad_x3_rows": (c_i32, [c_vp, c_i64, ctypes.POINTER(NerfSeg), c_i64, c_vp, c_i64,
-                                          ctypes.POINTER(NerfSeg), c_i64, c_i32, c_i32, c_vp, c_sz, c_vp]),
+                                          ctypes.POINTER(NerfSeg), c_i64, c_i32, c_i32, c_vp, c_sz, c_i32, c_vp]),
     "nerf_linear_wgrad_x3_rays": (c_i32, [c_vp, c_i64, ctypes.POINTER(NerfSeg), c_i64, c_vp, c_i64,
                                           ctypes.POINTER(NerfSeg), c_i64, c_i32, c_i32, c_vp, c_sz, c_vp, c_i32,
-                                          c_i32, c_vp]),
+                                          c_i32, c_i32, c_vp]),
     "nerf_pack_weight_x3": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
     "nerf_mlp_fused_fwd": (c_i32, [ctypes.POINTER(NerfFusedLayer), c_i32, c_vp, c_i64,
                                    ctypes.POINTER(NerfFusedEncoding), c_vp]),
     "nerf_mlp_fused_render": (c_i32, [ctypes.POINTER(NerfFusedLayer), c_i32, c_vp, c_i64,
                                       ctypes.POINTER(NerfFusedEncoding), ctypes.POINTER(NerfFusedComposite), c_vp]),
+    "nerf_mlp_fused_run": (c_i32, [ctypes.POINTER(NerfFusedLayer), c_i32, c_vp, c_i64, ctypes.POINTER(NerfFusedEncoding),
+                                   ctypes.POINTER(NerfFusedComposite), c_i32, c_vp]),
     "nerf_struct_size": (c_i64, [c_i32]),
     "nerf_build_flags": (c_i32, []),
     "nerf_fused_pack": (c_i32, [ctypes.POINTER(c_vp), c_i32, c_vp, c_vp, c_i64, c_vp, c_vp]),
@@ -267,7 +271,7 @@ def load(path: str | None = None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.nerf_abi_version() != 9:
+    if lib.nerf_abi_version() != 10:
         raise RuntimeError("nerf_amd: ABI version mismatch between Python binding and libnerf_amd.so")
     for which, st in enumerate(STRUCTS):
         if lib.nerf_struct_size(which) != ctypes.sizeof(st):

@@ -521,10 +521,11 @@ WGRAD_TILE_FN = ("linear_wgrad_x3_stream_kernel" if os.environ.get("NERF_WGRAD_T
                  else "linear_wgrad_x3_tr_kernel")
 
 
-def linear_wgrad_x3(dY: torch.Tensor, N4: int, segs, M: int, workspace: torch.Tensor) -> None:
+def linear_wgrad_x3(dY: torch.Tensor, N4: int, segs, M: int, workspace: torch.Tensor, passes: int = 3) -> None:
     """Split-precision weight-gradient slabs (nerf_linear_wgrad_x3).  N4 is the row count: rounded
     up to 4 over a padded dY, or the true count (257: one 256 x 256 tile + a vector-ALU row); the
-    workspace and the reduce take it rounded up to 4."""
+    workspace and the reduce take it rounded up to 4.  passes: 3 (3 x bf16 split) or 1 (one bf16
+    pass, matmul precision "medium")."""
     arr = make_segs(segs)
     kt = sum(k for _, k, _ in segs)
     # algorithmic bytes: dY and X read once, dW written once (the split-M slabs are the kernel's)
@@ -536,13 +537,13 @@ def linear_wgrad_x3(dY: torch.Tensor, N4: int, segs, M: int, workspace: torch.Te
                         ("linear_wgrad_smalln_kernel" if N4 <= 16 else "linear_wgrad_x3_kernel")) \
         if TIMER is not None else None
     st = _lib.load().nerf_linear_wgrad_x3(_ptr(dY), dY.stride(0), N4, arr, len(segs), M, _ptr(workspace),
-                                          workspace.numel() * workspace.element_size(), _stream(dY.device))
+                                          workspace.numel() * workspace.element_size(), passes, _stream(dY.device))
     if end is not None:
         end.record()
     _lib.check(st, "nerf_linear_wgrad_x3")
 
 
-def linear_wgrad_x3_rows(blocks, N4: int, workspace: torch.Tensor) -> None:
+def linear_wgrad_x3_rows(blocks, N4: int, workspace: torch.Tensor, passes: int = 3) -> None:
     """Split-precision weight-gradient slabs over two blocks of rows summed into one gradient
     (nerf_linear_wgrad_x3_rows): blocks = [(dY, segs, M), (dY1, segs1, M1)], the segments of the
     same widths; the workspace and the reduce take M + M1."""
@@ -560,13 +561,15 @@ def linear_wgrad_x3_rows(blocks, N4: int, workspace: torch.Tensor) -> None:
         if TIMER is not None else None
     st = _lib.load().nerf_linear_wgrad_x3_rows(_ptr(dY), dY.stride(0), a0, M, _ptr(dY1), dY1.stride(0), a1, M1,
                                                len(segs), N4, _ptr(workspace),
-                                               workspace.numel() * workspace.element_size(), _stream(dY.device))
+                                               workspace.numel() * workspace.element_size(), passes,
+                                               _stream(dY.device))
     if end is not None:
         end.record()
     _lib.check(st, "nerf_linear_wgrad_x3_rows")
 
 
-def linear_wgrad_x3_rays(blocks, N4: int, workspace: torch.Tensor, raysum: torch.Tensor, S0: int, S1: int) -> None:
+def linear_wgrad_x3_rays(blocks, N4: int, workspace: torch.Tensor, raysum: torch.Tensor, S0: int, S1: int,
+                        passes: int = 3) -> None:
     """linear_wgrad_x3_rows (streamed single-tile kernel) that also writes the per-ray sums of dY into
     raysum [B0 + B1, N4] (nerf_linear_wgrad_x3_rays); blocks as linear_wgrad_x3_rows, M1 may be 0."""
     (dY, segs, M), (dY1, segs1, M1) = blocks
@@ -581,7 +584,7 @@ def linear_wgrad_x3_rays(blocks, N4: int, workspace: torch.Tensor, raysum: torch
     st = _lib.load().nerf_linear_wgrad_x3_rays(_ptr(dY), dY.stride(0), a0, M, _ptr(dY1), dY1.stride(0), a1, M1,
                                                len(segs), N4, _ptr(workspace),
                                                workspace.numel() * workspace.element_size(), _ptr(raysum), S0, S1,
-                                               _stream(dY.device))
+                                               passes, _stream(dY.device))
     if end is not None:
         end.record()
     _lib.check(st, "nerf_linear_wgrad_x3_rays")

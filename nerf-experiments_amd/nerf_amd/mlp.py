@@ -34,15 +34,29 @@ from ._lib import (NERF_EPI_ACCUM, NERF_EPI_BIAS, NERF_EPI_MASK, NERF_EPI_MASKBI
 
 
 def matmul_precision() -> str:
-    """"fp32" (exact fp32 MFMA) or "x3" (3 x bf16 split MFMA, ~2^-17 per product).
+    """"fp32" (exact fp32 MFMA), "x3" (3 x bf16 split MFMA, ~2^-17 per product) or "x1" (one bf16
+    pass, bf16(w) * bf16(x) with fp32 accumulation, 2^-8 per product).
 
     Follows torch.get_float32_matmul_precision(), the knob the reference itself sets
-    (barf/run_barf.py:101 "high", naive-to-vanilla/main.py:53 "medium"): "highest" ->
-    exact fp32; "high"/"medium" -> split precision, which is ~64x more accurate than
-    the TF32/bf16 those settings select on the reference's hardware."""
+    (barf/run_barf.py:101 "high", naive-to-vanilla/main.py:53 "medium"): "highest" -> exact fp32;
+    "high" -> split precision, ~64x more accurate than the TF32 it selects on the reference's
+    hardware; "medium" -> single-pass bf16, the class of the single-pass bf16 / fp16 products the
+    reference's C2 run computes (main.py:53,58: "medium" under precision="16-mixed").  The fused
+    field-MLP kernels and the weight gradients run "x1" in one pass; the layer-by-layer GEMMs
+    (Gaussian / tanh layers, fields the fused kernel does not take) keep the 3-pass split there."""
     if PRECISION_OVERRIDE is not None:
         return PRECISION_OVERRIDE
-    return "fp32" if torch.get_float32_matmul_precision() == "highest" else "x3"
+    p = torch.get_float32_matmul_precision()
+    return "fp32" if p == "highest" else ("x1" if p == "medium" else "x3")
+
+
+def is_split(prec: str) -> bool:
+    """The bf16 split-precision kernels (either pass count) rather than the fp32 MFMA ones."""
+    return prec in ("x3", "x1")
+
+
+def passes(prec: str) -> int:
+    return 1 if prec == "x1" else 3
 
 
 PRECISION_OVERRIDE: str | None = None
@@ -84,7 +98,7 @@ def composite_sigma_layer(plan) -> int:
 
 def composite_eligible(plan, M: int, S: int) -> bool:
     """The fused forward runs this plan and its last layer can hand its heads to the compositing."""
-    if not FUSE_COMPOSITE or matmul_precision() != "x3" or not mlp_fused.eligible(plan, M):
+    if not FUSE_COMPOSITE or not is_split(matmul_precision()) or not mlp_fused.eligible(plan, M):
         return False
     # whole rays per 128-sample tile, or rays of 256 samples over two tiles run back to back
     if not ((16 <= S <= 128 and 128 % S == 0) or S == 256) or M % S or M * 32 >= (1 << 31):
@@ -145,7 +159,7 @@ def _ray_split(blocks, N4: int):
     return mains, rays
 
 
-def _wgrad_rays(blocks, N4: int, lp, workspace, gW, gb, acc, split) -> None:
+def _wgrad_rays(blocks, N4: int, lp, workspace, gW, gb, acc, split, npass: int = 3) -> None:
     """The weight gradient of `blocks` (one or two passes' rows) through the per-ray route (_ray_split)."""
     mains, rays = split
     Mt = sum(M for _, _, M in blocks)
@@ -156,32 +170,32 @@ def _wgrad_rays(blocks, N4: int, lp, workspace, gW, gb, acc, split) -> None:
     b0 = (blocks[0][0], mains[0], blocks[0][2])
     b1 = (blocks[1][0], mains[1], blocks[1][2]) if len(blocks) > 1 else (blocks[0][0], mains[0], 0)
     ws = _wgrad_workspace(workspace, Mt, N4, kmain)
-    K.linear_wgrad_x3_rays([b0, b1], N4, ws, raysum, rays[0][2], rays[1][2] if len(blocks) > 1 else 0)
+    K.linear_wgrad_x3_rays([b0, b1], N4, ws, raysum, rays[0][2], rays[1][2] if len(blocks) > 1 else 0, passes=npass)
     K.linear_wgrad_reduce(Mt, N4, kmain, lp.N, ws, lp.col_map[:kmain], gW, gb, accumulate=acc)
     kray = K.pad32(rays[0][1])
     Bt = sum(Bs)
     ws2 = _wgrad_workspace(workspace, Bt, N4, kray)
     r0 = (raysum[:Bs[0]], [(rays[0][0], rays[0][1], 1)], Bs[0])
     if len(blocks) > 1:
-        K.linear_wgrad_x3_rows([r0, (raysum[Bs[0]:], [(rays[1][0], rays[1][1], 1)], Bs[1])], N4, ws2)
+        K.linear_wgrad_x3_rows([r0, (raysum[Bs[0]:], [(rays[1][0], rays[1][1], 1)], Bs[1])], N4, ws2, passes=npass)
     else:
-        K.linear_wgrad_x3(r0[0], N4, r0[1], Bs[0], ws2)
+        K.linear_wgrad_x3(r0[0], N4, r0[1], Bs[0], ws2, passes=npass)
     K.linear_wgrad_reduce(Bt, N4, kray, lp.N, ws2, lp.col_map[kmain:kmain + kray], gW, None, accumulate=acc)
 
 
 def _flush_wgrad(entry, sink) -> None:
     """A stashed pass whose partner never ran its backward (BucketedGradAllReduce.finish()): its
     weight gradient alone, landed as the sink expects."""
-    dZ, segs, M, nrow, N4, lp = entry
+    dZ, segs, M, nrow, N4, lp, npass = entry
     w, b = lp.module.weight, lp.module.bias
     gW, acc = sink.target(w)
     gb, _ = sink.target(b)
     ws = torch.empty((K.linear_wgrad_workspace_bytes(M, N4, lp.Kp) + 3) // 4, device=dZ.device, dtype=torch.float32)
     rsplit = _ray_split([(dZ, segs, M)], N4) if nrow == N4 else None
     if rsplit is not None:          # the route the unmerged backward takes: the same result, bitwise
-        _wgrad_rays([(dZ, segs, M)], N4, lp, ws, gW, gb, acc, rsplit)
+        _wgrad_rays([(dZ, segs, M)], N4, lp, ws, gW, gb, acc, rsplit, npass)
     else:
-        K.linear_wgrad_x3(dZ, nrow, segs, M, ws)
+        K.linear_wgrad_x3(dZ, nrow, segs, M, ws, passes=npass)
         K.linear_wgrad_reduce(M, N4, lp.Kp, lp.N, ws, lp.col_map, gW, gb, accumulate=acc)
     sink.landed(w)
     sink.landed(b)
@@ -289,7 +303,7 @@ class LayerPlan:
         ones the input-gradient GEMMs use (Wt / Wtx) when forward=False.  Every call packs (no
         version-keyed cache: see the module docstring)."""
         w = self.module.weight.detach().contiguous()
-        x3 = precision == "x3"
+        x3 = is_split(precision)
         # in split precision the fp32 packs only serve GEMMs with <= 32 output columns: this
         # layer's forward (N <= 32) and the input gradients of sources <= 32 columns wide
         p = forward and (not x3 or self.N <= 32)
@@ -309,7 +323,7 @@ class LayerPlan:
         """Forward (W) or input-gradient (W^T) GEMM in the requested precision; outputs of at
         most 32 columns always use the fp32 kernel's 128 x 32 tile (measured: the 4-wide head at
         M = 262144 takes 42 us there against 55 us on the split-precision 256 x 128 tile)."""
-        if precision == "x3" and N > 32:
+        if is_split(precision) and N > 32:
             K.linear_fwd_x3(segs, M, self.Wtx if transpose else self.Wpx, self.ldwt if transpose else self.Kp, N, bias,
                             out, epi, aux=aux, w_row_offset=row_offset)
         else:
@@ -405,7 +419,7 @@ class MLPFunction(torch.autograd.Function):
         masks: list[torch.Tensor | None] = []
         pre: list[torch.Tensor] = []
         cols = None
-        if prec == "x3" and mlp_fused.eligible(plan, M):
+        if is_split(prec) and mlp_fused.eligible(plan, M):
             # the whole network in one launch (csrc/mlp_fused.hip); same outputs as the loop below
             fused = plan.fused.get(pos.device)
             if fused is None:
@@ -430,7 +444,8 @@ class MLPFunction(torch.autograd.Function):
                 comp.coef = (torch.empty(M, 8, device=pos.device, dtype=torch.float32)
                              if keep_all else None)
             fused.run(M, pos, dirs, dir_rd, acts, masks, col_t, (K.deferred(pos), K.deferred(dirs)),
-                      comp=(comp, rgb, w, composite_sigma_layer(plan)) if comp is not None else None)
+                      comp=(comp, rgb, w, composite_sigma_layer(plan)) if comp is not None else None,
+                      passes=passes(prec))
             K.mark_filled(pos)
             K.mark_filled(dirs)
             cols = tuple(col_t[li] for li, _ in plan.column_outputs)
@@ -449,7 +464,7 @@ class MLPFunction(torch.autograd.Function):
                 # in split precision, exp(-z^2 v) into the layer's output from the same epilogue;
                 # otherwise nerf_gauss_act_fwd applies the activation in a second pass
                 target = torch.empty_like(out) if lp.gauss is not None else out
-                if (GAUSS_EPILOGUE and lp.gauss is not None and prec == "x3" and lp.N > 32 and lp.residual < 0
+                if (GAUSS_EPILOGUE and lp.gauss is not None and is_split(prec) and lp.N > 32 and lp.residual < 0
                         and not lp.relu and K.linear_gauss_x3(segs, M, lp.Wpx, lp.Kp, lp.N, target, lp.gauss, bias=lp.module.bias,
                                               y=out)):
                     pre.append(target)
@@ -602,7 +617,7 @@ class MLPFunction(torch.autograd.Function):
             for (l, _, _, _, x, *_rest) in fd.steps:
                 if x is not None:
                     x_out[l] = torch.empty(M, x.k_pad, device=dev, dtype=torch.float32)
-            fd.run(M, g_head, dY, ctx.masks, g_cols, x_out, comp=comp_rt)
+            fd.run(M, g_head, dY, ctx.masks, g_cols, x_out, comp=comp_rt, passes=passes(ctx.prec))
             for (l, _, _, _, x, *_rest) in fd.steps:
                 if x is None:
                     continue
@@ -665,13 +680,13 @@ class MLPFunction(torch.autograd.Function):
             N4 = (lp.N + 3) // 4 * 4
             # the true row count: 257 (density + features) runs as one 256 x 256 tile + a row
             nrow = lp.N if (lp.N == 257 and WGRAD_ROW257) else N4
-            merge = sink is not None and ctx.prec == "x3" and MERGE_PASSES and gs is None
+            merge = sink is not None and is_split(ctx.prec) and MERGE_PASSES and gs is None
             prev = sink.stash.pop((id(plan), li), (None, None))[0] if merge else None
             if merge and prev is None and sink.remaining(w) >= 2:
                 # another pass of this field lands its contribution later in this backward: its
                 # weight gradient runs once over both passes' rows (one launch, one reduce); the
                 # sink flushes the stash alone if that pass never comes
-                sink.stash[(id(plan), li)] = ((dZ, segs, M, nrow, N4, lp), _flush_wgrad)
+                sink.stash[(id(plan), li)] = ((dZ, segs, M, nrow, N4, lp, passes(ctx.prec)), _flush_wgrad)
                 layer_grads[li] = [None, None]
             else:
                 if sink is not None:
@@ -683,17 +698,18 @@ class MLPFunction(torch.autograd.Function):
                     gW, gb, acc = torch.empty_like(w), torch.empty_like(lp.module.bias), False
                 rsplit = None
                 wblocks = [(prev[0], prev[1], prev[2]), (dZ, segs, M)] if prev is not None else [(dZ, segs, M)]
-                if ctx.prec == "x3" and nrow == N4:
+                if is_split(ctx.prec) and nrow == N4:
                     rsplit = _ray_split(wblocks, N4)
+                npass = passes(ctx.prec)
                 if rsplit is not None:
-                    _wgrad_rays(wblocks, N4, lp, workspace, gW, gb, acc, rsplit)
+                    _wgrad_rays(wblocks, N4, lp, workspace, gW, gb, acc, rsplit, npass)
                 elif prev is not None:
                     pdZ, psegs, pM = prev[0], prev[1], prev[2]
                     ws = _wgrad_workspace(workspace, M + pM, N4, lp.Kp)
-                    K.linear_wgrad_x3_rows([(pdZ, psegs, pM), (dZ, segs, M)], nrow, ws)
+                    K.linear_wgrad_x3_rows([(pdZ, psegs, pM), (dZ, segs, M)], nrow, ws, passes=npass)
                     K.linear_wgrad_reduce(M + pM, N4, lp.Kp, lp.N, ws, lp.col_map, gW, gb, accumulate=acc)
-                elif ctx.prec == "x3":
-                    K.linear_wgrad_x3(dZ, nrow, segs, M, workspace)
+                elif is_split(ctx.prec):
+                    K.linear_wgrad_x3(dZ, nrow, segs, M, workspace, passes=npass)
                     K.linear_wgrad_reduce(M, N4, lp.Kp, lp.N, workspace, lp.col_map, gW, gb, accumulate=acc)
                 else:
                     K.linear_wgrad(dZ, N4, segs, M, workspace)
@@ -714,7 +730,7 @@ class MLPFunction(torch.autograd.Function):
                     j = s.layer
                     prod = plan.layers[j]
                     if (GAUSS_EPILOGUE and prod.gauss is not None and plan.contributors[j] == 1 and dY[j] is None
-                            and not prod.relu and ctx.prec == "x3" and s.k_valid > 32):
+                            and not prod.relu and is_split(ctx.prec) and s.k_valid > 32):
                         # sole consumer: dL/dz of the Gaussian layer straight from this GEMM's epilogue
                         dz = torch.empty(M, prod.out_ld, device=dev, dtype=torch.float32)
                         gsj = torch.empty_like(prod.gauss)

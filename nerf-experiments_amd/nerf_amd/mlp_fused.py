@@ -41,6 +41,13 @@ def _pack_image(f) -> None:
     _lib.check(st, "nerf_fused_pack")
 
 
+def _flags(passes: int) -> int:
+    """nerf_mlp_fused_run flags of a pass count (3: the 3 x bf16 split, 1: NERF_FUSED_BF16)."""
+    if passes not in (1, 3):
+        raise ValueError(f"fused MLP: passes must be 1 or 3 (got {passes})")
+    return _lib.NERF_FUSED_BF16 if passes == 1 else 0
+
+
 FUSED_TYPES = {(0, 1): 1, (0, 2): 2, (4, 0): 3, (8, 0): 6, (8, 1): 7, (8, 2): 8}   # (kbr, kbh) -> type
 ENABLED = os.environ.get("NERF_FUSED", "1") != "0"     # A/B switch (bench, tests)
 # a per-ray encoding read by a later layer comes from registers captured at the tile start; tests
@@ -207,13 +214,14 @@ class FusedForward:
         _pack_image(self)
 
     def run(self, M: int, pos: torch.Tensor, dirs: torch.Tensor | None, dir_rd: int, acts, masks, col_outs,
-            gens=(None, None), comp=None):
+            gens=(None, None), comp=None, passes: int = 3):
         """Launch on the current stream.  acts[l]: [M, out_ld] fp32 or None (not stored),
         masks[l]: [M, 32] uint8 or None, col_outs: {layer: [M] fp32}.  gens: the DeferredEncoding
         of pos / dirs or None: generated in-kernel at every tile start (kernels.encode_fwd(defer=True))
         and stored into the tensor, which later layers read; the first layer reads them from LDS.
         comp: (CompositeSpec, rgb [B, 3], weights [B, S], sigma layer) — the rays composited at the
-        end of every tile (nerf_mlp_fused_render), coefficients into spec.coef when it is set."""
+        end of every tile (nerf_mlp_fused_render), coefficients into spec.coef when it is set.
+        passes: 3 (3 x bf16 split products) or 1 (one bf16 pass: matmul precision "medium")."""
         self.pack()
         L = len(self.plan.layers)
         descs = (_lib.NerfFusedLayer * L)()
@@ -309,14 +317,11 @@ class FusedForward:
             nbytes += 4.0 * M + 12.0 * (M // spec.S) + (4.0 * M if w is not None else 0.0) \
                 + (32.0 * M if spec.coef is not None else 0.0)
         end = K.TIMER.bracket("mlp_fused_fwd", flops, nbytes + self.image.numel() * self.image.element_size(),
-                              fn="mlp_fused_kernel<0>") \
+                              fn="mlp_fused_kernel<0>" if passes == 3 else "mlp_fused_kernel<2>") \
             if K.TIMER is not None else None
-        if cdesc is not None:
-            st = _lib.load().nerf_mlp_fused_render(descs, L, self.image.data_ptr(), M, encs if gen_of else None,
-                                                   ctypes.byref(cdesc), K._stream(self.device))
-        else:
-            st = _lib.load().nerf_mlp_fused_fwd(descs, L, self.image.data_ptr(), M, encs if gen_of else None,
-                                                K._stream(self.device))
+        st = _lib.load().nerf_mlp_fused_run(descs, L, self.image.data_ptr(), M, encs if gen_of else None,
+                                            ctypes.byref(cdesc) if cdesc is not None else None,
+                                            _flags(passes), K._stream(self.device))
         if end is not None:
             end.record()
         _lib.check(st, "nerf_mlp_fused_fwd")
@@ -451,7 +456,8 @@ class FusedInputGrad:
     def pack(self):
         _pack_image(self)
 
-    def run(self, M: int, g_head: torch.Tensor | None, dY, masks, g_cols=None, x_out=None, comp=None):
+    def run(self, M: int, g_head: torch.Tensor | None, dY, masks, g_cols=None, x_out=None, comp=None,
+            passes: int = 3):
         """g_head: [M, ld] gradient of the last layer's output; g_cols: {layer: [M, 4] buffer whose
         column 0 is the gradient of the layer's column output}; x_out: {layer: [M, k_pad] buffer for
         the gradient of the layer's encoding input}.  Fills dY[l] ([M, out_ld] fp32, the columns of
@@ -531,13 +537,11 @@ class FusedInputGrad:
             # algorithmic bytes beyond the coefficient rows counted above: grad_rgb, the rows stored
             nbytes += 12.0 * (M // spec.S) + 16.0 * M * (2 if gsig is not None else 1)
         end = K.TIMER.bracket("mlp_fused_dgrad", flops, nbytes + self.image.numel() * self.image.element_size(),
-                              fn="mlp_fused_kernel<1>") \
+                              fn="mlp_fused_kernel<1>" if passes == 3 else "mlp_fused_kernel<3>") \
             if K.TIMER is not None else None
-        if cdesc is not None:
-            st = _lib.load().nerf_mlp_fused_render(descs, S, self.image.data_ptr(), M, None, ctypes.byref(cdesc),
-                                                   K._stream(self.device))
-        else:
-            st = _lib.load().nerf_mlp_fused_fwd(descs, S, self.image.data_ptr(), M, None, K._stream(self.device))
+        st = _lib.load().nerf_mlp_fused_run(descs, S, self.image.data_ptr(), M, None,
+                                            ctypes.byref(cdesc) if cdesc is not None else None, _flags(passes),
+                                            K._stream(self.device))
         if end is not None:
             end.record()
         _lib.check(st, "nerf_mlp_fused_fwd (input-gradient chain)")

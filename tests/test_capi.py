@@ -44,7 +44,7 @@ def test_exported_dynamic_symbols_with_nm():
 def test_abi_version_and_status_strings():
     from nerf_amd import _lib
     lib = _lib.load()
-    assert lib.nerf_abi_version() == 9
+    assert lib.nerf_abi_version() == 10
     assert lib.nerf_status_string(0) == b"ok"
     assert b"invalid" in lib.nerf_status_string(-1)
     assert b"workspace" in lib.nerf_status_string(-4)

@@ -103,7 +103,7 @@ def _record_fused_outputs(monkeypatch, lib):
 
         monkeypatch.setattr(lib, fname, call)
 
-    for f in ("nerf_mlp_fused_fwd", "nerf_mlp_fused_render"):
+    for f in ("nerf_mlp_fused_fwd", "nerf_mlp_fused_render", "nerf_mlp_fused_run"):
         wrap(f)
     return regions
 
@@ -168,6 +168,6 @@ def _step(name, monkeypatch, rays):
 def test_guard_bands_full_step(name, monkeypatch):
     gt, regions, n_pad = _step(name, monkeypatch, 1024)
     # the step ran the fused forward and chain (layer outputs recorded) and guarded their buffers
-    assert any(f == "nerf_mlp_fused_render" for f, *_ in regions)
+    assert any(f == "nerf_mlp_fused_run" for f, *_ in regions)
     assert len(gt.allocs) > 20
     assert n_pad > 0, "no fused layer output with pad columns was checked"
