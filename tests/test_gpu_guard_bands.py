@@ -3,7 +3,8 @@
 (linear_wgrad_x3_*, linear_wgrad_smalln) and their slab reduce, over one full training step
 (forward, backward, optimizer) of the mip workload (C3's shared coarse / fine field,
 barf/model_interpolation.py:356-414, barf/model_interpolation_architecture.py:96-141) and of the
-ingp workload (C5, NaiveINGP).
+ingp workload (C5, NaiveINGP), in split precision ("high") and for mip also in one bf16 pass
+("medium").
 
 Every device buffer the nerf_amd host code allocates with `torch.empty` / `torch.empty_like`
 (layer outputs, ReLU bits, density columns, dY rows, encoding rows and their gradients, compositing
@@ -15,7 +16,9 @@ step:
   before each dY row — lands there);
 * for every layer output a fused launch named in its descriptors (`out` [M][ldo], `out2` [M][ldo2]),
   the pad columns between the layer's columns and the row stride hold either the sentinel (never
-  written) or zero (the zero-padded weight rows' outputs), never data.
+  written) or zero (the zero-padded weight rows' outputs), never data — except the columns another
+  output of the same launch is declared to write (the composite descriptor's head / density
+  gradient rows, which the chain stores into columns 256.. of the 257-wide layer's dY).
 The sentinel pattern fills memory torch.empty leaves undefined anyway: the product never reads it.
 """
 import sys
@@ -47,7 +50,16 @@ class _GuardedTorch:
         buf = torch.empty(nbytes + 2 * GUARD, dtype=torch.uint8, device=device)
         buf.fill_(SENT)
         self.allocs.append((buf, GUARD, nbytes))
-        return buf[GUARD:GUARD + nbytes].view(dtype).view(shape)
+        # a base tensor (not an autograd view) on the buffer's storage: the product code sets Python
+        # attributes on its buffers and returns them from autograd Functions, which treat views apart
+        esz = torch.empty((), dtype=dtype).element_size()
+        stride, acc = [], 1
+        for dim in reversed(shape):
+            stride.append(acc)
+            acc *= dim
+        t = torch.empty(0, dtype=dtype, device=device)
+        t.set_(buf.untyped_storage(), GUARD // esz, shape, tuple(reversed(stride)))
+        return t
 
     def empty(self, *size, device=None, dtype=None, requires_grad=False, **kw):
         if len(size) == 1 and isinstance(size[0], (tuple, list, torch.Size)):
@@ -85,30 +97,43 @@ def _install(monkeypatch):
 
 
 def _record_fused_outputs(monkeypatch, lib):
-    """Wrap the fused entry points: (pointer, rows, row stride, written columns) of every layer output."""
-    regions = []
+    """Wrap the fused entry points: (pointer, rows, row stride, written columns) of every layer
+    output.  Every other entry point is wrapped too, to count the calls the step made."""
+    regions, calls = [], {}
+    extra = []     # 4-column outputs of the composite descriptor (head / density gradient rows): (ptr, ld)
 
     def wrap(fname):
         fn = getattr(lib, fname)
+        fused = fname.startswith("nerf_mlp_fused_")
 
-        def call(layers, n_layers, image, M, *rest):
-            for i in range(int(n_layers)):
-                L = layers[i]
-                if L.out:
+        def call(*args):
+            calls[fname] = calls.get(fname, 0) + 1
+            if fused:
+                layers, n_layers, M = args[0], args[1], args[3]
+                for i in range(int(n_layers)):
+                    L = layers[i]
                     ncols = min(32 * L.n1, L.N) if L.out2 else L.N
-                    regions.append((fname, i, int(L.out), int(M), int(L.ldo), ncols))
-                if L.out2:
-                    regions.append((fname, i, int(L.out2), int(M), int(L.ldo2), L.N - 32 * L.n1))
-            return fn(layers, n_layers, image, M, *rest)
+                    if L.out and ncols > 0:          # (n1 = 0: every chunk goes to out2, none to out)
+                        regions.append((fname, i, int(L.out), int(M), int(L.ldo), ncols))
+                    if L.out2:
+                        regions.append((fname, i, int(L.out2), int(M), int(L.ldo2), L.N - 32 * L.n1))
+                comp = args[5] if fname != "nerf_mlp_fused_fwd" and len(args) > 6 else None
+                c = getattr(comp, "_obj", None)
+                if c is not None:
+                    for ptr, ld in ((c.grad_head, c.ld_head), (c.grad_sigma, c.ld_sigma)):
+                        if ptr:
+                            extra.append((int(ptr), int(ld)))
+            return fn(*args)
 
         monkeypatch.setattr(lib, fname, call)
 
-    for f in ("nerf_mlp_fused_fwd", "nerf_mlp_fused_render", "nerf_mlp_fused_run"):
+    from nerf_amd import _lib as libmod
+    for f in libmod._SIGNATURES:
         wrap(f)
-    return regions
+    return regions, calls, extra
 
 
-def _check(gt, regions):
+def _check(gt, regions, extra=()):
     torch.cuda.synchronize()
     assert gt.allocs, "no guarded allocation: the nerf_amd modules were not patched"
     bad = []
@@ -131,7 +156,15 @@ def _check(gt, regions):
         start = ptr - (buf.data_ptr() + off)
         assert start % 4 == 0 and start + rows * ld * 4 <= nbytes, (fname, layer, "region outside its buffer")
         view = buf[off + start:off + start + rows * ld * 4].view(torch.float32).view(rows, ld)
-        pad = view[:, ncols:]
+        # columns another output of the same launch writes (the chain's density-gradient rows are
+        # columns 256.. of the 257-wide layer's dY, written from the composite descriptor)
+        keep = torch.ones(ld - ncols, dtype=torch.bool, device=view.device)
+        for eptr, eld in extra:
+            off = eptr - ptr
+            if eld == ld and 4 * ncols <= off < 4 * ld and off % 4 == 0:
+                c0 = off // 4 - ncols
+                keep[c0:c0 + 4] = False
+        pad = view[:, ncols:][:, keep]
         bits = pad.contiguous().view(torch.int32)
         ok = (bits == torch.tensor([SENT] * 4, dtype=torch.uint8).view(torch.int32).to(bits.device)) | (pad == 0)
         assert bool(ok.all()), (f"{fname} layer {layer}: pad columns {ncols}..{ld - 1} hold data "
@@ -151,7 +184,7 @@ def _step(name, monkeypatch, rays):
             importlib.import_module("nerf_amd." + m.name)
     nerf_amd._lib.load()
     gt = _install(monkeypatch)
-    regions = _record_fused_outputs(monkeypatch, nerf_amd._lib.load())
+    regions, calls, extra = _record_fused_outputs(monkeypatch, nerf_amd._lib.load())
     monkeypatch.setitem(bench.WORKLOADS, name, dict(bench.WORKLOADS[name], rays=rays))
     dev = torch.device("cuda", 0)
     _, _, opt, loss_fn, _ = bench.build_workload(name, dev, 0)
@@ -160,14 +193,22 @@ def _step(name, monkeypatch, rays):
     opt.step()
     opt.zero_grad(set_to_none=True)
     assert torch.isfinite(loss).item()
-    n_regions = _check(gt, regions)
-    return gt, regions, n_regions
+    n_regions = _check(gt, regions, extra)
+    return gt, regions, n_regions, calls
 
 
-@pytest.mark.parametrize("name", ["mip", "ingp"])
-def test_guard_bands_full_step(name, monkeypatch):
-    gt, regions, n_pad = _step(name, monkeypatch, 1024)
+@pytest.mark.parametrize("name,precision", [("mip", "high"), ("mip", "medium"), ("ingp", "high")])
+def test_guard_bands_full_step(name, precision, monkeypatch):
+    # the fused kernels run in split ("high": mlp_fused_kernel<0> / <1>) or single-pass ("medium":
+    # <2> / <3>) precision; torch's default "highest" takes the fp32 layer-by-layer GEMMs instead
+    old = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision(precision)
+    try:
+        gt, regions, n_pad, calls = _step(name, monkeypatch, 1024)
+    finally:
+        torch.set_float32_matmul_precision(old)
     # the step ran the fused forward and chain (layer outputs recorded) and guarded their buffers
-    assert any(f == "nerf_mlp_fused_run" for f, *_ in regions)
+    assert calls.get("nerf_mlp_fused_run", 0) >= 2, calls
+    assert any(f == "nerf_mlp_fused_run" for f, *_ in regions), calls
     assert len(gt.allocs) > 20
     assert n_pad > 0, "no fused layer output with pad columns was checked"
