@@ -74,9 +74,9 @@ def _spy(monkeypatch):
     calls = []
     real = mlp_fused.FusedForward.run
 
-    def run(self, M, pos, dirs, dir_rd, acts, masks, col_outs, gens=(None, None), comp=None):
+    def run(self, M, pos, dirs, dir_rd, acts, masks, col_outs, gens=(None, None), comp=None, **kw):
         calls.append((M, dir_rd, gens[0] is not None, gens[1] is not None))
-        return real(self, M, pos, dirs, dir_rd, acts, masks, col_outs, gens, comp)
+        return real(self, M, pos, dirs, dir_rd, acts, masks, col_outs, gens, comp, **kw)
     monkeypatch.setattr(mlp_fused.FusedForward, "run", run)
     return calls
 
