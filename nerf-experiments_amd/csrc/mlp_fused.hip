@@ -147,18 +147,7 @@ __device__ __forceinline__ f4 mfma16(bf16x8 a, bf16x8 b, f4 c) {
 }
 __device__ __forceinline__ void split8(f8 v, bf16x8& hi, bf16x8& lo) {
     hi = __builtin_convertvector(v, bf16x8);
-#ifdef NERF_FUSED_SCALAR_SPLIT
-    const f8 hf = __builtin_convertvector(hi, f8);
-    f8 d;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const float vi = v[i], hi_ = hf[i];
-        d[i] = vi - hi_;
-    }
-    lo = __builtin_convertvector(d, bf16x8);
-#else
     lo = __builtin_convertvector(v - __builtin_convertvector(hi, f8), bf16x8);
-#endif
 }
 
 __device__ __forceinline__ void barrier() {
@@ -595,12 +584,11 @@ __device__ __forceinline__ void split2(float x, float y, unsigned& hi, unsigned&
     typedef float f2 __attribute__((ext_vector_type(2)));
     const bf16x2 h = __builtin_convertvector((f4{x, y, 0.f, 0.f}).xy, bf16x2);
     hi = __builtin_bit_cast(unsigned, h);
-#ifdef NERF_FUSED_SCALAR_SPLIT
-    const f2 d = {x - __builtin_bit_cast(float, hi << 16), y - __builtin_bit_cast(float, hi & 0xffff0000u)};
-#else
+    // one packed subtract (exact: hi is x rounded).  Scalar subtracts / no SLP packing anywhere in
+    // the kernel (no v_pk_*_f32 beside the MFMAs) measured within noise: step 11.33 / 11.24 vs
+    // 11.26 ms, three rotating repetitions (profiles/r06f)
     const f2 hf = {__builtin_bit_cast(float, hi << 16), __builtin_bit_cast(float, hi & 0xffff0000u)};
-    const f2 d = f2{x, y} - hf;                     // one packed subtract (exact: hi is x rounded)
-#endif
+    const f2 d = f2{x, y} - hf;
     lo = __builtin_bit_cast(unsigned, __builtin_convertvector(d, bf16x2));
 }
 
