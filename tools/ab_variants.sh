@@ -7,14 +7,14 @@ set -u
 TAG=$1; REPS=$2; shift 2
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
-WL=${AB_WORKLOAD:-mip}
+WL=${AB_WORKLOAD:-mip}   # AB_ARGS: extra bench.py arguments (e.g. --matmul-precision medium)
 for rep in $(seq 1 "$REPS"); do
   for v in nerf-experiments_amd/nerf_amd/libnerf_amd.so "$@"; do
     lib=$v; envset=NERF_AB_NONE=1
     case "$v" in env:*) envset=${v#env:}; lib=nerf-experiments_amd/nerf_amd/libnerf_amd.so;; esac
     name=$(basename "$lib" .so); [ "$envset" != NERF_AB_NONE=1 ] && name="$name-$envset"
     f="$OUT/${name}_${rep}.json"
-    env "$envset" NERF_AMD_LIB=$lib timeout -k 10 150 python3 bench.py --workload "$WL" --steps 60 --warmup 10 --no-cpu-baseline \
+    env "$envset" NERF_AMD_LIB=$lib timeout -k 10 150 python3 bench.py --workload "$WL" --steps 60 --warmup 10 --no-cpu-baseline ${AB_ARGS:-} \
       --no-frame-roofline > "$f" 2> "$f.err" || { echo "failed $lib"; exit 1; }
     python3 - "$f" "$name" <<'PY'
 import json, sys
