@@ -113,7 +113,8 @@ class BucketedGradAllReduce:
     weight gradients and resets the per-step claims).  A forward that claims parameters after
     gradients of the previous backward have landed, without a ``finish()`` in between, raises."""
 
-    def __init__(self, params, bucket_bytes: int = 1 << 20, group=None, direct: bool = False):
+    def __init__(self, params, bucket_bytes: int = 1 << 20, group=None, direct: bool = False,
+                 force: bool = False):
         seen, plist = set(), []
         for p in params:
             if p.requires_grad and id(p) not in seen:
@@ -121,7 +122,9 @@ class BucketedGradAllReduce:
                 plist.append(p)
         self.params = plist
         self.group = group
-        self.active = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        # force: run the buckets and their collectives even in a world of one process (the all-reduce
+        # is then the identity: tests/test_gpu_rccl.py drives RCCL through this path on one GPU)
+        self.active = dist.is_available() and dist.is_initialized() and (dist.get_world_size(group) > 1 or force)
         self.world = dist.get_world_size(group) if self.active else 1
         self.buckets: list[_Bucket] = []
         self._where = {}
