@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from bench import evidence_tag  # noqa: E402
 
-FNS = ("mlp_fused_kernel<0>", "mlp_fused_kernel<1>", "linear_nt_x3_glds_kernel", "linear_nt_x3_kernel", "linear_wgrad_smalln_kernel",
+FNS = ("mlp_fused_kernel<0>", "mlp_fused_kernel<1>", "mlp_fused_kernel<2>", "mlp_fused_kernel<3>", "linear_nt_x3_glds_kernel", "linear_nt_x3_kernel", "linear_wgrad_smalln_kernel",
        "linear_wgrad_x3_tr_kernel", "linear_wgrad_x3_stream_kernel", "linear_wgrad_x3_kernel", "linear_nt_kernel",
        "linear_wgrad_kernel",
        "hashgrid_bwd_kernel", "hashgrid_fwd_kernel", "hashgrid_fwd_level_kernel", "hashgrid_fwd_tile_kernel",
