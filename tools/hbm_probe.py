@@ -24,7 +24,7 @@ y = torch.empty_like(x)
 x.fill_(1.0)
 out = torch.empty((), device="cuda")
 w = timed(lambda: x.fill_(2.0))
-r = timed(lambda: torch.sum(x, out=out))
+r = timed(lambda: torch.sum(x, dim=0, out=out))
 c = timed(lambda: y.copy_(x))
 gb = 4 * n / 1e9
 print(json.dumps({"write_only_TBs": gb / w / 1e3, "read_only_TBs": gb / r / 1e3, "copy_TBs_read_plus_write": 2 * gb / c / 1e3,
