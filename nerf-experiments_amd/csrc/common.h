@@ -29,7 +29,8 @@
 #else
 #define NERF_TU_DIAG_FUSED 0
 #endif
-#if defined(NERF_WS_DIAG_YD_FIXED) || defined(NERF_WS_DIAG_NOCONV) || defined(NERF_WS_DIAG_NOMFMA)
+#if defined(NERF_WS_DIAG_YD_FIXED) || defined(NERF_WS_DIAG_NOCONV) || defined(NERF_WS_DIAG_NOMFMA) || \
+    defined(NERF_WT_DIAG_NOMFMA) || defined(NERF_WT_DIAG_NOLOAD)
 #define NERF_TU_DIAG_WGRAD NERF_BUILD_DIAG_WGRAD
 #else
 #define NERF_TU_DIAG_WGRAD 0

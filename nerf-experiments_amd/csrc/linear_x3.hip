@@ -1281,6 +1281,14 @@ constexpr int WT_IMG = 4 * WT_T * 512;            // image stage: [op][hi | lo][
 constexpr int WT_RS = 4 * 256 * 4;                // per-ray partials of the 4 dY waves
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4_t;
+// The two waves of a SIMD (wave w loads dY rows, wave w + 4 X rows) multiply at different times: the
+// X-loading wave runs step i's MFMAs before converting step i + 1, its partner after (profiles/r06k:
+// the tr kernel 1.5-2 % faster in the mip step than all-convert-first; 2 = the roles swapped, 3 = half
+// of every wave's MFMAs before the conversion, both no better).  Same products, same order per
+// accumulator: bitwise the same gradients.
+#ifndef NERF_WT_STAGGER
+#define NERF_WT_STAGGER 1
+#endif
 
 // byte offset of columns col .. col + 3 (8-byte aligned) of image row `row` of plane (op, pl)
 __device__ __forceinline__ unsigned wt_off(int op, int pl, int row, int col) {
@@ -1300,7 +1308,7 @@ __device__ __forceinline__ wt_gfp wt_src_row(wt_gfp s0, wt_gfp s1, int64_t ld0, 
     return (b1 ? s1 : s0) + (int64_t)rr * (b1 ? ld1 : ld0);
 }
 
-template <bool ROW257, bool RAYS, bool X1>
+template <bool ROW257, bool RAYS, bool X1, int JN>
 __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void linear_wgrad_x3_tr_kernel(
     TNArgs a, int npad, int kpad) {
     __shared__ __attribute__((aligned(16))) char smem[2 * WT_IMG + (RAYS ? 2 * WT_RS : 0)];
@@ -1366,6 +1374,9 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     f4 ra[4], rb[4];                          // the two register stages: steps in flight
     float ya[4], yb[4];
     auto issue = [&](int i, f4 (&r)[4], float (&y)[4]) __attribute__((always_inline)) {
+#ifdef NERF_WT_DIAG_NOLOAD     // diagnostic builds only: no row loads (converts the registers' stale values)
+        if (i < 2)
+#endif
 #pragma unroll
         for (int q = 0; q < 4; ++q) r[q] = __builtin_nontemporal_load((gf4p)WT_SRC_ROW(i, q));
         if constexpr (ROW257) {
@@ -1472,46 +1483,70 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         return (rel + 1) % S == 0 ? (b1 ? rs_B0 : 0) + rel / S : -1;
     };
 
-    // ---- MFMA role: wave (wr, wc) owns dW rows wr*128 .. +127 (4 x 32) and columns wc*64 .. +63 (2 x 32)
+    // ---- MFMA role: wave (wr, wc) owns dW rows wr*128 .. +127 (4 x 32) and columns wc*32JN ..
+    // +32JN-1 (JN x 32; JN = 1 for inputs of <= 128 columns, so that all four SIMDs multiply)
     const int wr = wave >> 2, wc = wave & 3;
-    const bool active = wc * 64 < a.X.ktot && wr * 128 < N;
+#ifndef NERF_WT_DIAG_NOMFMA     // diagnostic builds only: no MFMA step (loads, conversion, barriers)
+    const bool active = wc * 32 * JN < a.X.ktot && wr * 128 < N;
+#else
+    const bool active = false;
+#endif
     // transposed-read addresses: lane 4q + p of 16-lane group G supplies row 8 (G >> 1) + q (+ 4 for
     // the fragment's second half), columns c0 + 16 (G & 1) + 4 p of the 32-column block c0
     const int G = lane >> 4, qq = (lane & 15) >> 2, pq = lane & 3;
-    unsigned ya_off[4], xa_off[2];
+    unsigned ya_off[4], xa_off[JN];
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii) ya_off[ii] = wt_off(0, 0, 8 * (G >> 1) + qq, wr * 128 + 32 * ii + 16 * (G & 1) + 4 * pq);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) xa_off[j] = wt_off(1, 0, 8 * (G >> 1) + qq, wc * 64 + 32 * j + 16 * (G & 1) + 4 * pq);
+    for (int j = 0; j < JN; ++j) xa_off[j] = wt_off(1, 0, 8 * (G >> 1) + qq, wc * 32 * JN + 32 * j + 16 * (G & 1) + 4 * pq);
     auto frag = [&](const char* img, unsigned off) __attribute__((always_inline)) {
         const s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(img + off));
         const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(img + off + 4 * 512));
         return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
     };
-    f32x16 acc[4][2];
+    f32x16 acc[4][JN];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < JN; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    auto mfma_step = [&](int i) __attribute__((always_inline)) {
+    // the MFMAs of step i over row blocks ii0 .. ii1 - 1
+    auto mfma_step = [&](int i, int ii0 = 0, int ii1 = 4) __attribute__((always_inline)) {
         const char* img = smem + (i & 1) * WT_IMG;
-        bf16x8 xh[2], xl[2], yh[4], yl[4];
+        bf16x8 xh[JN], xl[JN], yh[4], yl[4];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < JN; ++j) {
             xh[j] = frag(img, xa_off[j]);
             xl[j] = frag(img, xa_off[j] + WT_T * 512);
         }
 #pragma unroll
-        for (int ii = 0; ii < 4; ++ii) {
+        for (int ii = ii0; ii < ii1; ++ii) {
             yh[ii] = frag(img, ya_off[ii]);
             yl[ii] = frag(img, ya_off[ii] + WT_T * 512);
         }
 #pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
+        for (int ii = ii0; ii < ii1; ++ii)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[ii][j] = mfma_w<X1>(yh[ii], yl[ii], xh[j], xl[j], acc[ii][j]);
+            for (int j = 0; j < JN; ++j) acc[ii][j] = mfma_w<X1>(yh[ii], yl[ii], xh[j], xl[j], acc[ii][j]);
+    };
+    // NERF_WT_STAGGER: 1 the X-loading waves multiply before converting, 2 the dY-loading waves do,
+    // 3 every wave multiplies half its row blocks before converting; 0 all convert first
+    auto mfma_pre = [&](int i) __attribute__((always_inline)) {
+        if constexpr (NERF_WT_STAGGER == 3) {
+            if (active) mfma_step(i, 0, 2);
+        } else if constexpr (NERF_WT_STAGGER == 1 || NERF_WT_STAGGER == 2) {
+            if (op == (NERF_WT_STAGGER == 1 ? 1 : 0) && active) mfma_step(i);
+        }
+    };
+    auto mfma_post = [&](int i) __attribute__((always_inline)) {
+        if constexpr (NERF_WT_STAGGER == 3) {
+            if (active) mfma_step(i, 2, 4);
+        } else if constexpr (NERF_WT_STAGGER == 1 || NERF_WT_STAGGER == 2) {
+            if (op == (NERF_WT_STAGGER == 1 ? 0 : 1) && active) mfma_step(i);
+        } else {
+            if (active) mfma_step(i);
+        }
     };
     auto barrier = []() __attribute__((always_inline)) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS writes / reads done
@@ -1533,17 +1568,19 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         // stage nobody reads, masked to zero: no branch around them, so the counted waits are exact)
         int i = 0;
         for (; i + 1 < steps; i += 2) {
+            mfma_pre(i);
             convert(i + 1, rb, yb);
             issue(i + 3, rb, yb);
             flush_ray();
             if constexpr (RAYS) pend_ray = op == 0 ? ray_of_step(i + 1) : -1;
-            if (active) mfma_step(i);
+            mfma_post(i);
             barrier();
+            mfma_pre(i + 1);
             convert(i + 2, ra, ya);
             issue(i + 4, ra, ya);
             flush_ray();
             if constexpr (RAYS) pend_ray = i + 2 < steps && op == 0 ? ray_of_step(i + 2) : -1;
-            if (active) mfma_step(i + 1);
+            mfma_post(i + 1);
             barrier();
         }
         if (i < steps) {                       // odd step count: the last step, converted already
@@ -1559,8 +1596,8 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int k = wc * 64 + j * 32 + (lane & 31);
+        for (int j = 0; j < JN; ++j) {
+            const int k = wc * 32 * JN + j * 32 + (lane & 31);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int n = wr * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
@@ -1971,16 +2008,25 @@ static int wgrad_x3_rows_impl(const float* dY, int64_t ld_dy, const nerf_seg* se
         const dim3 grid((unsigned)splits), block(512);
         hipStream_t st = as_stream(stream);
         if (WGRAD_TR) {
-            // register-staged rows, transposed LDS reads (linear_wgrad_x3_tr_kernel)
+            // register-staged rows, transposed LDS reads (linear_wgrad_x3_tr_kernel); inputs of <= 128
+            // columns spread their 4 column blocks over the 4 SIMDs (JN = 1)
+            const bool narrow = L.ktot <= 128 && !raysum;
+#define NERF_WT_LAUNCH(R257, RAYS, X1, JN) \
+    hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<R257, RAYS, X1, JN>), grid, block, 0, st, a, ntn * TB, ntk * TB)
             if (x1) {
-                if (N > 256) hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<true, false, true>), grid, block, 0, st, a, ntn * TB, ntk * TB);
-                else if (raysum) hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<false, true, true>), grid, block, 0, st, a, ntn * TB, ntk * TB);
-                else hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<false, false, true>), grid, block, 0, st, a, ntn * TB, ntk * TB);
+                if (narrow && N > 256) NERF_WT_LAUNCH(true, false, true, 1);
+                else if (narrow) NERF_WT_LAUNCH(false, false, true, 1);
+                else if (N > 256) NERF_WT_LAUNCH(true, false, true, 2);
+                else if (raysum) NERF_WT_LAUNCH(false, true, true, 2);
+                else NERF_WT_LAUNCH(false, false, true, 2);
             } else {
-                if (N > 256) hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<true, false, false>), grid, block, 0, st, a, ntn * TB, ntk * TB);
-                else if (raysum) hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<false, true, false>), grid, block, 0, st, a, ntn * TB, ntk * TB);
-                else hipLaunchKernelGGL((linear_wgrad_x3_tr_kernel<false, false, false>), grid, block, 0, st, a, ntn * TB, ntk * TB);
+                if (narrow && N > 256) NERF_WT_LAUNCH(true, false, false, 1);
+                else if (narrow) NERF_WT_LAUNCH(false, false, false, 1);
+                else if (N > 256) NERF_WT_LAUNCH(true, false, false, 2);
+                else if (raysum) NERF_WT_LAUNCH(false, true, false, 2);
+                else NERF_WT_LAUNCH(false, false, false, 2);
             }
+#undef NERF_WT_LAUNCH
         } else if (x1) {
             hipLaunchKernelGGL((linear_wgrad_x3_stream_kernel<3, 2, true>), grid, block, 0, st, a, ntn * TB, ntk * TB);
         } else {

@@ -183,6 +183,48 @@ def _wgrad_rays(blocks, N4: int, lp, workspace, gW, gb, acc, split, npass: int =
     K.linear_wgrad_reduce(Bt, N4, kray, lp.N, ws2, lp.col_map[kmain:kmain + kray], gW, None, accumulate=acc)
 
 
+# The weight gradient of a layer whose inputs span more than the single-tile kernel's 256 padded
+# columns (mip-NeRF's skip layer: [trunk activation 256 | encoding 96], barf/model_mip.py:85-130
+# through NerfModel's skip connections) as two launches of it over a cut between its segments
+# (256-column block, then the rest: the <= 128-column block spreads over all four SIMDs), instead of
+# the 128-tile kernel that re-reads dY per 128-column block (profiles/r06k; NERF_WGRAD_COLSPLIT=0: the
+# 128-tile kernel, as before)
+WGRAD_COLSPLIT = os.environ.get("NERF_WGRAD_COLSPLIT", "1") != "0"
+
+
+def _col_split(segs, nrow: int):
+    """The segment index at which the layer's inputs split into two single-tile launches (nrow: the
+    weight-gradient row count the kernels take, 257 or the padded N), or None."""
+    if not WGRAD_COLSPLIT or nrow <= 128 or nrow > 257:
+        return None
+    kp = [K.pad32(k) for _, k, _ in segs]
+    if sum(kp) <= 256:
+        return None
+    acc = 0
+    for j, k in enumerate(kp):
+        if acc + k > 256:
+            return j if j > 0 and sum(kp[j:]) <= 256 else None
+        acc += k
+    return None
+
+
+def _wgrad_cols(blocks, nrow: int, N4: int, lp, workspace, gW, gb, acc, cut: int, npass: int) -> None:
+    """The weight gradient of `blocks` (one or two passes' rows) in two column blocks (_col_split)."""
+    Mt = sum(M for _, _, M in blocks)
+    k0 = 0
+    for part, (a, b) in enumerate(((0, cut), (cut, len(blocks[0][1])))):
+        pb = [(dZ, segs[a:b], M) for dZ, segs, M in blocks]
+        kp = sum(K.pad32(k) for _, k, _ in pb[0][1])
+        ws = _wgrad_workspace(workspace, Mt, N4, kp)
+        if len(pb) > 1:
+            K.linear_wgrad_x3_rows(pb, nrow, ws, passes=npass)
+        else:
+            K.linear_wgrad_x3(pb[0][0], nrow, pb[0][1], pb[0][2], ws, passes=npass)
+        K.linear_wgrad_reduce(Mt, N4, kp, lp.N, ws, lp.col_map[k0:k0 + kp], gW, gb if part == 0 else None,
+                              accumulate=acc)
+        k0 += kp
+
+
 def _flush_wgrad(entry, sink) -> None:
     """A stashed pass whose partner never ran its backward (BucketedGradAllReduce.finish()): its
     weight gradient alone, landed as the sink expects."""
@@ -192,8 +234,11 @@ def _flush_wgrad(entry, sink) -> None:
     gb, _ = sink.target(b)
     ws = torch.empty((K.linear_wgrad_workspace_bytes(M, N4, lp.Kp) + 3) // 4, device=dZ.device, dtype=torch.float32)
     rsplit = _ray_split([(dZ, segs, M)], N4) if nrow == N4 else None
+    cut = _col_split(segs, nrow) if rsplit is None else None
     if rsplit is not None:          # the route the unmerged backward takes: the same result, bitwise
         _wgrad_rays([(dZ, segs, M)], N4, lp, ws, gW, gb, acc, rsplit, npass)
+    elif cut is not None:
+        _wgrad_cols([(dZ, segs, M)], nrow, N4, lp, ws, gW, gb, acc, cut, npass)
     else:
         K.linear_wgrad_x3(dZ, nrow, segs, M, ws, passes=npass)
         K.linear_wgrad_reduce(M, N4, lp.Kp, lp.N, ws, lp.col_map, gW, gb, accumulate=acc)
@@ -701,8 +746,11 @@ class MLPFunction(torch.autograd.Function):
                 if is_split(ctx.prec) and nrow == N4:
                     rsplit = _ray_split(wblocks, N4)
                 npass = passes(ctx.prec)
+                cut = _col_split(segs, nrow) if rsplit is None and is_split(ctx.prec) else None
                 if rsplit is not None:
                     _wgrad_rays(wblocks, N4, lp, workspace, gW, gb, acc, rsplit, npass)
+                elif cut is not None:
+                    _wgrad_cols(wblocks, nrow, N4, lp, workspace, gW, gb, acc, cut, npass)
                 elif prev is not None:
                     pdZ, psegs, pM = prev[0], prev[1], prev[2]
                     ws = _wgrad_workspace(workspace, M + pM, N4, lp.Kp)

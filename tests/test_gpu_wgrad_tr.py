@@ -4,7 +4,8 @@ is read once per process).  Same 16-sample MFMA steps in sample order, same spli
 gradients are bitwise equal; the bias gradients, the 257th row and the per-ray dY sums come from
 per-wave partials added in a fixed order, equal to fp32 summation order (1e-6 of scale).  Shapes
 cover one and two row blocks, ragged splits (M not a multiple of 16), padded columns (N, K < 256,
-a 60-wide segment padded to 64), the 257-row layer and the per-ray route."""
+a 60-wide segment padded to 64), inputs of <= 128 columns (JN = 1), the 257-row layer and the per-ray
+route."""
 import json
 import os
 import subprocess
@@ -26,6 +27,9 @@ CASES = [  # (name, M0, M1, N, [(k, row_div)], rays S0/S1 or None)
     ("row257", 65536, 0, 257, [(256, 1)], None),
     ("row257_two_blocks", 32768, 65536, 257, [(256, 1)], None),
     ("rays", 64 * 300, 128 * 200, 256, [(256, 1)], (64, 128)),
+    # inputs of <= 128 columns: the column blocks spread over the four SIMDs (JN = 1)
+    ("narrow_k_row257", 65536, 0, 257, [(96, 1)], None),
+    ("narrow_k_two_segs", 30000, 20001, 256, [(64, 1), (24, 1)], None),
 ]
 
 SCRIPT = r"""
