@@ -1786,6 +1786,14 @@ extern "C" size_t nerf_linear_wgrad_workspace(int64_t M, int32_t N, int32_t K);
 int nerf_wgrad_choose_splits(int64_t M, int tiles);
 int nerf_wgrad_split_tiles(int N, int K);
 
+// Layers wider than 256 outputs (GARF's Linear(3, 1024), Linear(131, 512) and the input gradients
+// into them) as column blocks of <= 256 on the 256-row tile kernel, A re-read per block, instead of
+// the 128 x 128-tile kernel.  NERF_NT_NBLOCK=0: the 128-tile kernel (A/B switch, read once).
+static const bool NT_NBLOCK = [] {
+    const char* e = getenv("NERF_NT_NBLOCK");
+    return !(e && e[0] == '0');
+}();
+
 extern "C" int nerf_linear_fwd_x3(const nerf_seg* segs, int32_t n_segs, int64_t M, const void* W_x, int32_t ldw,
                                   int32_t N, const float* bias, float* out, int64_t ldo, int32_t epilogue,
                                   const float* aux, int64_t ld_aux, void* stream) {
@@ -1806,29 +1814,37 @@ extern "C" int nerf_linear_fwd_x3(const nerf_seg* segs, int32_t n_segs, int64_t 
                        (!(epilogue & NERF_EPI_TANH_BWD) || (aligned16(aux) && (ld_aux % 4) == 0));
     NTArgs a{L, (int)M, reinterpret_cast<const __bf16*>(W_x), ldw, N, bias, out, ldo, epilogue, aux, ld_aux, vec_ok};
     hipStream_t st = as_stream(stream);
-    // tanh epilogues run on the 128 x 128 tile kernel (runtime epilogue flags)
-    if (N <= 256 && !(epilogue & (NERF_EPI_NARROW_TILE | NERF_EPI_TANH | NERF_EPI_TANH_BWD))) {
+    // tanh epilogues run on the 128 x 128 tile kernel (runtime epilogue flags); mask bits need N <= 256
+    if ((N <= 256 || (NT_NBLOCK && !mbits)) && !(epilogue & (NERF_EPI_NARROW_TILE | NERF_EPI_TANH | NERF_EPI_TANH_BWD))) {
         const int ntiles = (int)((M + 255) / 256);
         int grid = cu_count_x3();
         if (grid > ntiles) grid = ntiles;
         const dim3 g3((unsigned)grid), b3(512);
-#define NERF_GLDS_LAUNCH(E)                                                                          \
-    do {                                                                                            \
-        if (N > 128) hipLaunchKernelGGL((linear_nt_x3_glds_kernel<E, 2>), g3, b3, 0, st, a, ntiles); \
-        else hipLaunchKernelGGL((linear_nt_x3_glds_kernel<E, 1>), g3, b3, 0, st, a, ntiles);         \
+        for (int n0 = 0; n0 < N; n0 += 256) {          // column blocks of <= 256 (one when N <= 256)
+            NTArgs b = a;
+            b.N = N - n0 < 256 ? N - n0 : 256;
+            b.Wx = a.Wx + (size_t)n0 * 2 * ldw;
+            b.bias = bias ? bias + n0 : nullptr;
+            b.out = out + n0;
+            b.aux = aux && !mbits ? aux + n0 : aux;
+#define NERF_GLDS_LAUNCH(E)                                                                            \
+    do {                                                                                              \
+        if (b.N > 128) hipLaunchKernelGGL((linear_nt_x3_glds_kernel<E, 2>), g3, b3, 0, st, b, ntiles); \
+        else hipLaunchKernelGGL((linear_nt_x3_glds_kernel<E, 1>), g3, b3, 0, st, b, ntiles);         \
     } while (0)
-        switch (epilogue & 15) {
-            case NERF_EPI_BIAS | NERF_EPI_RELU: NERF_GLDS_LAUNCH(NERF_EPI_BIAS | NERF_EPI_RELU); break;
-            case NERF_EPI_BIAS: NERF_GLDS_LAUNCH(NERF_EPI_BIAS); break;
-            case NERF_EPI_BIAS | NERF_EPI_ACCUM: NERF_GLDS_LAUNCH(NERF_EPI_BIAS | NERF_EPI_ACCUM); break;
-            case 0: NERF_GLDS_LAUNCH(0); break;
-            case NERF_EPI_MASK: NERF_GLDS_LAUNCH(NERF_EPI_MASK); break;
-            case NERF_EPI_MASK | NERF_EPI_ACCUM: NERF_GLDS_LAUNCH(NERF_EPI_MASK | NERF_EPI_ACCUM); break;
-            case NERF_EPI_ACCUM: NERF_GLDS_LAUNCH(NERF_EPI_ACCUM); break;
-            default: return NERF_ERR_UNSUPPORTED;
-        }
+            switch (epilogue & 15) {
+                case NERF_EPI_BIAS | NERF_EPI_RELU: NERF_GLDS_LAUNCH(NERF_EPI_BIAS | NERF_EPI_RELU); break;
+                case NERF_EPI_BIAS: NERF_GLDS_LAUNCH(NERF_EPI_BIAS); break;
+                case NERF_EPI_BIAS | NERF_EPI_ACCUM: NERF_GLDS_LAUNCH(NERF_EPI_BIAS | NERF_EPI_ACCUM); break;
+                case 0: NERF_GLDS_LAUNCH(0); break;
+                case NERF_EPI_MASK: NERF_GLDS_LAUNCH(NERF_EPI_MASK); break;
+                case NERF_EPI_MASK | NERF_EPI_ACCUM: NERF_GLDS_LAUNCH(NERF_EPI_MASK | NERF_EPI_ACCUM); break;
+                case NERF_EPI_ACCUM: NERF_GLDS_LAUNCH(NERF_EPI_ACCUM); break;
+                default: return NERF_ERR_UNSUPPORTED;
+            }
 #undef NERF_GLDS_LAUNCH
-        NERF_CHECK_LAUNCH();
+            NERF_CHECK_LAUNCH();
+        }
         return NERF_OK;
     }
     const int ntm = (int)((M + 127) / 128);
@@ -1882,6 +1898,44 @@ extern "C" int nerf_linear_gauss_x3(const nerf_seg* segs, int32_t n_segs, int64_
     NTArgs a{L, (int)M, reinterpret_cast<const __bf16*>(W_x), ldw, N, bias, out, ldo, epi, z, ld_z, 1,
              inv_std, y, ld_y, part};
     int64_t slabs;
+    if (N > 256 && NT_NBLOCK) {
+        // wider layers (GARF's Linear(3, 1024), Linear(131, 512) and the input gradients into them):
+        // column blocks of <= 256 on the 256-row tile kernel, each re-reading A, with the fp64
+        // column partials of block n0 in their own [tiles][nb] slab block (part + n0 * tiles)
+        const int ntiles = (int)((M + 255) / 256);
+        int grid = cu_count_x3();
+        if (grid > ntiles) grid = ntiles;
+        const dim3 g3((unsigned)grid), b3(512);
+        for (int n0 = 0; n0 < N; n0 += 256) {
+            NTArgs b = a;
+            b.N = N - n0 < 256 ? N - n0 : 256;
+            b.Wx = a.Wx + (size_t)n0 * 2 * ldw;
+            b.bias = bias ? bias + n0 : nullptr;
+            b.out = out + n0;
+            b.gs = inv_std + n0;
+            if (fwd) b.y2 = y + n0;
+            else b.aux = z + n0;
+            b.part = part + (size_t)n0 * ntiles;
+            if (b.N > 128) {
+                if (epi == (NERF_EPI_GAUSS | NERF_EPI_BIAS)) hipLaunchKernelGGL((linear_nt_x3_glds_kernel<NERF_EPI_GAUSS | NERF_EPI_BIAS, 2>), g3, b3, 0, st, b, ntiles);
+                else if (epi == NERF_EPI_GAUSS) hipLaunchKernelGGL((linear_nt_x3_glds_kernel<NERF_EPI_GAUSS, 2>), g3, b3, 0, st, b, ntiles);
+                else hipLaunchKernelGGL((linear_nt_x3_glds_kernel<NERF_EPI_GAUSS_BWD, 2>), g3, b3, 0, st, b, ntiles);
+            } else {
+                if (epi == (NERF_EPI_GAUSS | NERF_EPI_BIAS)) hipLaunchKernelGGL((linear_nt_x3_glds_kernel<NERF_EPI_GAUSS | NERF_EPI_BIAS, 1>), g3, b3, 0, st, b, ntiles);
+                else if (epi == NERF_EPI_GAUSS) hipLaunchKernelGGL((linear_nt_x3_glds_kernel<NERF_EPI_GAUSS, 1>), g3, b3, 0, st, b, ntiles);
+                else hipLaunchKernelGGL((linear_nt_x3_glds_kernel<NERF_EPI_GAUSS_BWD, 1>), g3, b3, 0, st, b, ntiles);
+            }
+            NERF_CHECK_LAUNCH();
+        }
+        if (fwd) return NERF_OK;
+        for (int n0 = 0; n0 < N; n0 += 256) {
+            const int nb = N - n0 < 256 ? N - n0 : 256;
+            const int rc = nerf::gauss_reduce(part + (size_t)n0 * ntiles, ntiles, nb, inv_std + n0, grad_inv_std + n0,
+                                              accumulate, part + (size_t)ntiles * N, st);
+            if (rc != NERF_OK) return rc;
+        }
+        return NERF_OK;
+    }
     if (N <= 256) {
         const int ntiles = (int)((M + 255) / 256);
         int grid = cu_count_x3();

@@ -31,22 +31,24 @@ class KernelTimer:
     def __init__(self):
         self.records = []
 
-    def bracket(self, tag: str, flops: float = 0.0, nbytes: float = 0.0, fn: str | None = None):
+    def bracket(self, tag: str, flops: float = 0.0, nbytes: float = 0.0, fn: str | None = None, launches: int = 1):
+        """launches: kernel launches inside the bracket (a wide layer's column blocks), so that the
+        per-launch averages match rocprofv3's"""
         start = torch.cuda.Event(enable_timing=True)
         end = torch.cuda.Event(enable_timing=True)
         start.record()
-        self.records.append((tag, flops, nbytes, start, end, fn or tag))
+        self.records.append((tag, flops, nbytes, start, end, fn or tag, launches))
         return end
 
     def summary(self, by: str = "tag"):
         out = {}
-        for *_, e, _fn in self.records:
+        for *_, e, _fn, _n in self.records:
             e.synchronize()                     # (every end event recorded: durations are final)
-        for tag, flops, nbytes, s, e, fn in self.records:
+        for tag, flops, nbytes, s, e, fn, n in self.records:
             ms = s.elapsed_time(e)
             d = out.setdefault(fn if by == "fn" else tag,
                                {"launches": 0, "flops": 0.0, "bytes": 0.0, "ms": 0.0, "tags": set()})
-            d["launches"] += 1
+            d["launches"] += n
             d["flops"] += flops
             d["bytes"] += nbytes
             d["ms"] += ms
@@ -463,6 +465,24 @@ def linear_wgrad_reduce(M: int, N4: int, K: int, n_valid: int, workspace: torch.
     _lib.check(st, "nerf_linear_wgrad_reduce")
 
 
+# nerf_linear_fwd_x3 / nerf_linear_gauss_x3 run layers wider than 256 outputs as column blocks on
+# the 256-row tile kernel unless NERF_NT_NBLOCK=0 (read once by the library, mirrored here for the
+# timer's kernel names)
+NT_NBLOCK = os.environ.get("NERF_NT_NBLOCK", "1") != "0"
+
+
+def _nt_x3_fn(N: int, epilogue: int = 0) -> str:
+    """The kernel function nerf_linear_fwd_x3 / nerf_linear_gauss_x3 launches for N outputs."""
+    if epilogue & (_lib.NERF_EPI_NARROW_TILE | _lib.NERF_EPI_TANH | _lib.NERF_EPI_TANH_BWD):
+        return "linear_nt_x3_kernel"
+    wide_ok = NT_NBLOCK and not epilogue & (_lib.NERF_EPI_MASKBITS | _lib.NERF_EPI_MASKOUT)
+    return "linear_nt_x3_glds_kernel" if N <= 256 or wide_ok else "linear_nt_x3_kernel"
+
+
+def _nt_x3_launches(N: int, epilogue: int = 0) -> int:
+    return (N + 255) // 256 if _nt_x3_fn(N, epilogue) == "linear_nt_x3_glds_kernel" else 1
+
+
 def linear_fwd_x3(segs, M: int, Wx: torch.Tensor, ldw: int, N: int, bias: torch.Tensor | None,
                   out: torch.Tensor, epilogue: int, aux: torch.Tensor | None = None, w_row_offset: int = 0) -> None:
     """3 x bf16 split-precision variant of linear_fwd; Wx holds the interleaved hi|lo
@@ -470,7 +490,7 @@ def linear_fwd_x3(segs, M: int, Wx: torch.Tensor, ldw: int, N: int, bias: torch.
     arr = make_segs(segs)
     off = w_row_offset * ldw * 2 * 2
     end = TIMER.bracket("linear_nt_x3", 2.0 * M * N * ldw, _segs_bytes(segs, M) + 4.0 * M * N + 4.0 * N * ldw,
-                        fn="linear_nt_x3_glds_kernel" if N <= 256 else "linear_nt_x3_kernel") \
+                        fn=_nt_x3_fn(N, epilogue), launches=_nt_x3_launches(N, epilogue)) \
         if TIMER is not None else None
     st = _lib.load().nerf_linear_fwd_x3(arr, len(segs), M, Wx.data_ptr() + off, ldw, N, _ptr(bias), _ptr(out),
                                         out.stride(0), epilogue, _ptr(aux), aux.stride(0) if aux is not None else 0,
@@ -499,7 +519,7 @@ def linear_gauss_x3(segs, M: int, Wx: torch.Tensor, ldw: int, N: int, out: torch
                          dtype=torch.float64)
     nbytes = _segs_bytes(segs, M) + 4.0 * N * ldw + (8.0 * M * N if fwd else 12.0 * M * N)
     end = TIMER.bracket("linear_gauss_x3" if fwd else "linear_gauss_bwd_x3", 2.0 * M * N * ldw, nbytes,
-                        fn="linear_nt_x3_glds_kernel" if N <= 256 else "linear_nt_x3_kernel") \
+                        fn=_nt_x3_fn(N), launches=_nt_x3_launches(N)) \
         if TIMER is not None else None
     st = lib.nerf_linear_gauss_x3(arr, len(segs), M, Wx.data_ptr() + off, ldw, N, _ptr(bias), _ptr(out),
                                   out.stride(0), _lib.NERF_GAUSS_FWD if fwd else _lib.NERF_GAUSS_BWD,

@@ -162,8 +162,8 @@ def test_garf_gauss_epilogue_matches_separate_passes(name):
     exp(-z^2 v) from one launch; backward: dL/dz and the inverse-std column partials from the
     consumer's input-gradient GEMM) against the separate nerf_gauss_act passes on the same GEMMs:
     outputs and input gradients bit-identical, inverse-std gradients equal up to the fp64 summation
-    order, every other parameter gradient bit-identical.  M = 70,001 rows: ragged 256- and 128-row
-    tiles, 1024-wide layer on the 128 x 128 tile kernel."""
+    order, every other parameter gradient bit-identical.  M = 70,001 rows: ragged 256-row tiles, the
+    1024- and 512-wide layers in 256-column blocks of the 256-row tile kernel."""
     from nerf_amd import ProposalNetwork, RadianceNetwork
     from nerf_amd import mlp as mlp_mod
     torch.manual_seed(3)
@@ -202,3 +202,50 @@ def test_garf_gauss_epilogue_matches_separate_passes(name):
             torch.testing.assert_close(g1[k], g2[k], rtol=1e-5, atol=1e-6, msg=k)
         else:
             assert torch.equal(g1[k], g2[k]), k
+
+
+NBLOCK_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, {pkg!r})
+from nerf_amd import RadianceNetwork
+torch.set_float32_matmul_precision("high")
+dev = torch.device("cuda", 0)
+torch.manual_seed(3)
+M = 70_001
+pos = (torch.rand(M, 3) * 2 - 1).to(dev).requires_grad_(True)
+d = torch.nn.functional.normalize(torch.randn(M, 3), dim=-1).to(dev)
+gc, gd = torch.randn(M, 3).to(dev), torch.randn(M, 1).to(dev)
+torch.manual_seed(0)
+m = RadianceNetwork(0.5, 2.0).to(dev)
+rgb, dens = m(pos, d)
+((rgb * gc).sum() + (dens * gd).sum()).backward()
+out = {{"rgb": rgb.detach().cpu(), "dens": dens.detach().cpu(), "dpos": pos.grad.cpu()}}
+out.update({{k: v.grad.cpu() for k, v in m.named_parameters()}})
+torch.save(out, sys.argv[1])
+"""
+
+
+@pytest.mark.gpu
+def test_wide_layers_column_blocks_match_the_128_tile_kernel(tmp_path):
+    """GARF's radiance network with its 1024- and 512-wide layers (forward with the Gaussian epilogue,
+    and the input gradients into them) as 256-column blocks of the 256-row tile kernel
+    (NERF_NT_NBLOCK=1, the default) against the 128 x 128 tile kernel (NERF_NT_NBLOCK=0; the switch
+    is read once per process, so each runs in a child): the two kernels round their 3 x bf16 split
+    products differently (each within 2^-16 of scale), so outputs agree within 1e-5 of scale and the
+    gradients, through several such layers, within 1e-4."""
+    import os
+    import subprocess
+    import sys
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "nerf-experiments_amd")
+    res = []
+    for on in ("1", "0"):
+        f = tmp_path / f"nb{on}.pt"
+        r = subprocess.run([sys.executable, "-c", NBLOCK_SCRIPT.format(pkg=pkg), str(f)],
+                           env=dict(os.environ, NERF_NT_NBLOCK=on), capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res.append(torch.load(f, weights_only=True))
+    for k, a in res[0].items():
+        b = res[1][k]
+        assert torch.isfinite(a).all(), k
+        tol = 1e-5 if k in ("rgb", "dens") else 1e-4
+        assert (a - b).abs().max() <= tol * b.abs().max() + 1e-12, (k, (a - b).abs().max().item())
