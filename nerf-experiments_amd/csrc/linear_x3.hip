@@ -1281,14 +1281,6 @@ constexpr int WT_IMG = 4 * WT_T * 512;            // image stage: [op][hi | lo][
 constexpr int WT_RS = 4 * 256 * 4;                // per-ray partials of the 4 dY waves
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4_t;
-// The two waves of a SIMD (wave w loads dY rows, wave w + 4 X rows) multiply at different times: the
-// X-loading wave runs step i's MFMAs before converting step i + 1, its partner after (profiles/r06k:
-// the tr kernel 1.5-2 % faster in the mip step than all-convert-first; 2 = the roles swapped, 3 = half
-// of every wave's MFMAs before the conversion, both no better).  Same products, same order per
-// accumulator: bitwise the same gradients.
-#ifndef NERF_WT_STAGGER
-#define NERF_WT_STAGGER 1
-#endif
 
 // byte offset of columns col .. col + 3 (8-byte aligned) of image row `row` of plane (op, pl)
 __device__ __forceinline__ unsigned wt_off(int op, int pl, int row, int col) {
@@ -1530,23 +1522,16 @@ __global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll
             for (int j = 0; j < JN; ++j) acc[ii][j] = mfma_w<X1>(yh[ii], yl[ii], xh[j], xl[j], acc[ii][j]);
     };
-    // NERF_WT_STAGGER: 1 the X-loading waves multiply before converting, 2 the dY-loading waves do,
-    // 3 every wave multiplies half its row blocks before converting; 0 all convert first
+    // The two waves of a SIMD (wave w loads dY rows, wave w + 4 X rows) multiply at different times:
+    // the X-loading wave runs step i's MFMAs before converting step i + 1, its partner after, so one
+    // wave's conversion (VALU) runs under the other's MFMAs (profiles/r06k: the kernel 1.5-2 % faster
+    // in the mip step than both converting first; the roles swapped, or half of every wave's MFMAs
+    // before the conversion, no better).  Same products in the same order per accumulator.
     auto mfma_pre = [&](int i) __attribute__((always_inline)) {
-        if constexpr (NERF_WT_STAGGER == 3) {
-            if (active) mfma_step(i, 0, 2);
-        } else if constexpr (NERF_WT_STAGGER == 1 || NERF_WT_STAGGER == 2) {
-            if (op == (NERF_WT_STAGGER == 1 ? 1 : 0) && active) mfma_step(i);
-        }
+        if (op == 1 && active) mfma_step(i);
     };
     auto mfma_post = [&](int i) __attribute__((always_inline)) {
-        if constexpr (NERF_WT_STAGGER == 3) {
-            if (active) mfma_step(i, 2, 4);
-        } else if constexpr (NERF_WT_STAGGER == 1 || NERF_WT_STAGGER == 2) {
-            if (op == (NERF_WT_STAGGER == 1 ? 0 : 1) && active) mfma_step(i);
-        } else {
-            if (active) mfma_step(i);
-        }
+        if (op == 0 && active) mfma_step(i);
     };
     auto barrier = []() __attribute__((always_inline)) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS writes / reads done
