@@ -183,46 +183,80 @@ def _wgrad_rays(blocks, N4: int, lp, workspace, gW, gb, acc, split, npass: int =
     K.linear_wgrad_reduce(Bt, N4, kray, lp.N, ws2, lp.col_map[kmain:kmain + kray], gW, None, accumulate=acc)
 
 
-# The weight gradient of a layer whose inputs span more than the single-tile kernel's 256 padded
-# columns (mip-NeRF's skip layer: [trunk activation 256 | encoding 96], barf/model_mip.py:85-130
-# through NerfModel's skip connections) as two launches of it over a cut between its segments
-# (256-column block, then the rest: the <= 128-column block spreads over all four SIMDs), instead of
-# the 128-tile kernel that re-reads dY per 128-column block (profiles/r06k; NERF_WGRAD_COLSPLIT=0: the
-# 128-tile kernel, as before)
-WGRAD_COLSPLIT = os.environ.get("NERF_WGRAD_COLSPLIT", "1") != "0"
+# The weight gradient of a layer larger than the single-tile kernel's 256 (257) rows x 256 padded
+# columns — mip-NeRF's skip layer [trunk activation 256 | encoding 96] (barf/model_mip.py:85-130
+# through NerfModel's skip connections), GARF's Linear(1024, 256), Linear(512, 256) and
+# Linear(131, 512) (garf/model_radiance.py, model_proposal.py) — as single-tile launches over row
+# blocks of <= 256 output rows (views of dY and of the gradient) and column groups of <= 256 padded
+# input columns (whole segments, or 256-column slices of a wider one), one reduce per tile into its
+# rows and columns, instead of the 128 x 128-tile kernel that re-reads dY per 128-column block
+# (profiles/r06k; NERF_WGRAD_TILESPLIT=0: the 128-tile kernel, as before).  Only when every tile
+# can take the single-tile kernel (more than 128 rows or columns).
+WGRAD_TILESPLIT = os.environ.get("NERF_WGRAD_TILESPLIT", "1") != "0"
 
 
-def _col_split(segs, nrow: int):
-    """The segment index at which the layer's inputs split into two single-tile launches (nrow: the
-    weight-gradient row count the kernels take, 257 or the padded N), or None."""
-    if not WGRAD_COLSPLIT or nrow <= 128 or nrow > 257:
+def _tile_split(segs, nrow: int):
+    """(row blocks [(n0, nb)], column groups [[(segment, c0, c1)]]) of the layer's weight gradient
+    as single-tile launches (nrow: the row count the kernels take, 257 or the padded N), or None.
+    The pieces of a group are consecutive in the packed layout: one col_map range per group."""
+    if not WGRAD_TILESPLIT:
         return None
     kp = [K.pad32(k) for _, k, _ in segs]
-    if sum(kp) <= 256:
+    if nrow <= 257 and sum(kp) <= 256:
+        return None                                        # one tile already
+    rows = [(0, nrow)] if nrow <= 257 else [(n0, min(256, nrow - n0)) for n0 in range(0, nrow, 256)]
+    groups, cur, used = [], [], 0
+    for j, (_, k, rd) in enumerate(segs):
+        if kp[j] > 256 and rd != 1:
+            return None
+        for c0 in range(0, k, 256):                        # 256-column slices of a wider segment
+            c1 = min(c0 + 256, k)
+            w = K.pad32(c1 - c0)
+            if used + w > 256:
+                groups.append(cur)
+                cur, used = [], 0
+            cur.append((j, c0, c1))
+            used += w
+    groups.append(cur)
+    gk = [sum(K.pad32(c1 - c0) for _, c0, c1 in g) for g in groups]
+    if len(rows) > 1 and min(gk) <= 128:
+        # row blocks of a narrow input (GARF's Linear(3, 1024)): the 128-tile kernel streams dY
+        # faster than single-tile launches whose X side is nearly empty (profiles/r06k)
         return None
-    acc = 0
-    for j, k in enumerate(kp):
-        if acc + k > 256:
-            return j if j > 0 and sum(kp[j:]) <= 256 else None
-        acc += k
-    return None
+    if any(not (nb > 128 or k > 128) for _, nb in rows for k in gk):
+        return None                                        # a tile the single-tile kernel does not take
+    return rows, groups
 
 
-def _wgrad_cols(blocks, nrow: int, N4: int, lp, workspace, gW, gb, acc, cut: int, npass: int) -> None:
-    """The weight gradient of `blocks` (one or two passes' rows) in two column blocks (_col_split)."""
+def _wgrad_tiles(blocks, nrow: int, N4: int, lp, workspace, gW, gb, acc, split, npass: int) -> None:
+    """The weight gradient of `blocks` (one or two passes' rows) tile by tile (_tile_split)."""
+    rows, groups = split
     Mt = sum(M for _, _, M in blocks)
-    k0 = 0
-    for part, (a, b) in enumerate(((0, cut), (cut, len(blocks[0][1])))):
-        pb = [(dZ, segs[a:b], M) for dZ, segs, M in blocks]
-        kp = sum(K.pad32(k) for _, k, _ in pb[0][1])
-        ws = _wgrad_workspace(workspace, Mt, N4, kp)
-        if len(pb) > 1:
-            K.linear_wgrad_x3_rows(pb, nrow, ws, passes=npass)
-        else:
-            K.linear_wgrad_x3(pb[0][0], nrow, pb[0][1], pb[0][2], ws, passes=npass)
-        K.linear_wgrad_reduce(Mt, N4, kp, lp.N, ws, lp.col_map[k0:k0 + kp], gW, gb if part == 0 else None,
-                              accumulate=acc)
-        k0 += kp
+    poff = [0]                                             # packed column offset of each segment
+    for _, k, _ in blocks[0][1]:
+        poff.append(poff[-1] + K.pad32(k))
+
+    def piece(segs, j, c0, c1):
+        t, k, rd = segs[j]
+        return (t, k, rd) if (c0, c1) == (0, k) else (t[:, c0:c1], c1 - c0, rd)
+
+    whole = len(rows) == 1
+    for n0, nb in rows:
+        nr = nrow if whole else nb                         # 257: the 256 x 256 tile + its 257th row
+        n4 = N4 if whole else nb
+        nvalid = lp.N if whole else min(nb, lp.N - n0)
+        for gi, g in enumerate(groups):
+            pb = [(dZ if whole else dZ[:, n0:n0 + nb], [piece(segs, j, c0, c1) for j, c0, c1 in g], M)
+                  for dZ, segs, M in blocks]
+            p0 = poff[g[0][0]] + g[0][1]
+            kp = sum(K.pad32(c1 - c0) for _, c0, c1 in g)
+            ws = _wgrad_workspace(workspace, Mt, n4, kp)
+            if len(pb) > 1:
+                K.linear_wgrad_x3_rows(pb, nr, ws, passes=npass)
+            else:
+                K.linear_wgrad_x3(pb[0][0], nr, pb[0][1], pb[0][2], ws, passes=npass)
+            K.linear_wgrad_reduce(Mt, n4, kp, nvalid, ws, lp.col_map[p0:p0 + kp], gW[n0:n0 + nvalid],
+                                  gb[n0:n0 + nvalid] if gi == 0 else None, accumulate=acc)
 
 
 def _flush_wgrad(entry, sink) -> None:
@@ -234,11 +268,11 @@ def _flush_wgrad(entry, sink) -> None:
     gb, _ = sink.target(b)
     ws = torch.empty((K.linear_wgrad_workspace_bytes(M, N4, lp.Kp) + 3) // 4, device=dZ.device, dtype=torch.float32)
     rsplit = _ray_split([(dZ, segs, M)], N4) if nrow == N4 else None
-    cut = _col_split(segs, nrow) if rsplit is None else None
+    tsplit = _tile_split(segs, nrow) if rsplit is None else None
     if rsplit is not None:          # the route the unmerged backward takes: the same result, bitwise
         _wgrad_rays([(dZ, segs, M)], N4, lp, ws, gW, gb, acc, rsplit, npass)
-    elif cut is not None:
-        _wgrad_cols([(dZ, segs, M)], nrow, N4, lp, ws, gW, gb, acc, cut, npass)
+    elif tsplit is not None:
+        _wgrad_tiles([(dZ, segs, M)], nrow, N4, lp, ws, gW, gb, acc, tsplit, npass)
     else:
         K.linear_wgrad_x3(dZ, nrow, segs, M, ws, passes=npass)
         K.linear_wgrad_reduce(M, N4, lp.Kp, lp.N, ws, lp.col_map, gW, gb, accumulate=acc)
@@ -746,11 +780,11 @@ class MLPFunction(torch.autograd.Function):
                 if is_split(ctx.prec) and nrow == N4:
                     rsplit = _ray_split(wblocks, N4)
                 npass = passes(ctx.prec)
-                cut = _col_split(segs, nrow) if rsplit is None and is_split(ctx.prec) else None
+                tsplit = _tile_split(segs, nrow) if rsplit is None and is_split(ctx.prec) else None
                 if rsplit is not None:
                     _wgrad_rays(wblocks, N4, lp, workspace, gW, gb, acc, rsplit, npass)
-                elif cut is not None:
-                    _wgrad_cols(wblocks, nrow, N4, lp, workspace, gW, gb, acc, cut, npass)
+                elif tsplit is not None:
+                    _wgrad_tiles(wblocks, nrow, N4, lp, workspace, gW, gb, acc, tsplit, npass)
                 elif prev is not None:
                     pdZ, psegs, pM = prev[0], prev[1], prev[2]
                     ws = _wgrad_workspace(workspace, M + pM, N4, lp.Kp)
